@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident receive-path transform (checksum + parse + demux) on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W          (N > 1: launched by torch.distributed.run)
+
+A step = one dk_rx_process pass over one HBM-resident batch of the workload (default: BASELINE config 2,
+1,048,576 x 1500 B IPv4/TCP frames over 1,024 flows, 1 % corrupted tail), plus, for N > 1, the RCCL all-reduce of the
+per-flow packet counts (the only collective on this path). Weak scaling: every rank owns one batch (its packet shard).
+`value` = sum of frame bytes processed by all ranks / max-over-ranks time.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DESC_BYTES = 6         # u32 offset + u16 length per frame
+RESULT_BYTES = 24      # meta, src_ip, dst_ip, ports, payload, flow_id (u32 each)
+
+WORKLOADS = {
+    # name: (description, frames, ip_len spec, flow kind, nflows)
+    "c2_tcp1500": ("1M x 1500B IPv4/TCP, 1024 flows, device-resident", 1 << 20, 1486, "tcp", 1024),
+    "c3_udp64": ("1M x 64B IPv4/UDP (min-size), device-resident, 8 rotating batches", 1 << 20, 50, "udp", 1024),
+    "c4_imix": ("IMIX 40/576/1500 at 7:4:1, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, "imix", "tcp", 1024),
+    "c5_tcp1500_10k": ("1500B IPv4/TCP, 10k flows, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, 1486, "tcp", 10000),
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")), ws
+
+
+def make_batch(eng, name, rank, seed_base):
+    from demikernel_amd import synth
+
+    _, n, ip_len, kind, nflows = WORKLOADS[name]
+    flows = synth.make_flows(nflows, kind=kind)
+    seed = seed_base + 7919 * rank
+    lens = synth.imix_ip_lengths(n, seed) if ip_len == "imix" else ip_len
+    tr = synth.traffic(n, lens, flows, seed=seed)
+    eng.set_sockets(flows)
+    batch = synth.build_device(tr, eng, seed=seed)
+    synth.corrupt_device(batch, batch.off.cpu().numpy().view(np.uint32), synth.corruption_plan(n, 0.01, tr, seed))
+    return batch, flows, tr
+
+
+def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allreduce=False):
+    """Run warmup + timed steps; returns (wall seconds for `steps`, list of per-launch kernel seconds)."""
+    import torch
+
+    def step(k):
+        b = batches[k % len(batches)]
+        eng.receive_batch(b, res, stream=stream)
+
+    for k in range(warmup):
+        step(k)
+        if counts_allreduce:
+            dist.all_reduce(res.t["flow_counts"])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        step(k)
+        ev[k][1].record(stream)
+        if counts_allreduce:
+            dist.all_reduce(res.t["flow_counts"])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern = [a.elapsed_time(b) / 1e3 for a, b in ev]
+    return wall, kern
+
+
+def cpu_baseline(batch, flows, sample_frames, min_seconds, threads=1):
+    """Oracle (CPU restatement of the reference) on a bounded sample of the same workload, host cores."""
+    from demikernel_amd import ipv4, synth
+    from oracle.oracle import OraclePeer
+
+    n = min(sample_frames, batch.n)
+    off = batch.off[:n].cpu().numpy().view(np.uint32).copy()
+    lens = batch.len[:n].cpu().numpy().view(np.uint16).copy()
+    end = int(off[-1]) + int(lens[-1])
+    blob = batch.blob[:end].cpu().numpy()
+    peer = OraclePeer(ipv4(synth.BOB_IPV4))
+    peer.set_flows(flows)
+    nbytes = int(lens.astype(np.int64).sum())
+    rates, used, t_all = [], 1, time.perf_counter()
+    while time.perf_counter() - t_all < min_seconds or len(rates) < 3:
+        t = time.perf_counter()
+        if threads == 1:
+            peer.process(blob, off, lens)
+        else:
+            _, used = peer.process_mt(blob, off, lens, threads)
+        rates.append(nbytes / (time.perf_counter() - t) / 1e9)
+    return float(np.median(rates)), used, n, nbytes, len(rates)
+
+
+def load_traffic_profile(workload):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), if one exists for this workload."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2_tcp1500", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 17)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    rank, local_rank, world = dist_env()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from demikernel_amd import Config, RxEngine, synth
+
+    eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
+    stream = torch.cuda.current_stream(dev)
+    name = args.workload
+    batch, flows, tr = make_batch(eng, name, rank, synth.SEED)
+    batches = [batch]
+    if name == "c3_udp64":  # 64 B batches fit in the 256 MB MALL: rotate 8 distinct batches (> 512 MB)
+        batches += [make_batch(eng, name, rank + 1000 * k, synth.SEED)[0] for k in range(1, 8)]
+    res = eng.results(batch.n)
+    frame_bytes = int(tr.frame_len.astype(np.int64).sum())
+
+    wall, kern = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist, counts_allreduce=world > 1)
+    if dist is not None:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        tb = torch.tensor([frame_bytes, batch.n], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tb)
+        total_bytes, total_frames = int(tb[0]), int(tb[1])
+    else:
+        total_bytes, total_frames = frame_bytes, batch.n
+
+    value = total_bytes * args.steps / wall / 1e9
+    kern_avg = float(np.mean(kern))
+    algo = frame_bytes + batch.n * (DESC_BYTES + RESULT_BYTES)
+    achieved = algo / kern_avg / 1e9
+    traffic = load_traffic_profile(name)
+
+    out = {
+        "metric": "GB/s packet bytes checksummed+parsed (device-resident)",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded frames generated on device; 1% corrupted tail)",
+        "config": {"workload": WORKLOADS[name][0], "name": name, "frames_per_gpu": batch.n,
+                   "global_frames": total_frames, "parallelism": f"packet-shard x{world}",
+                   "collective": "all_reduce(flow_counts, u64) per step" if world > 1 else "none"},
+        "mpkt_s": round(total_frames * args.steps / wall / 1e6, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel_ms_avg": round(kern_avg * 1e3, 4),
+                     "algorithmic_bytes_per_launch": algo},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        gbs, used, n_s, nb_s, reps = cpu_baseline(batch, flows, args.cpu_sample, args.cpu_seconds)
+        out["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s", "cores": used, "kind": "port",
+                               "sample": f"first {n_s} frames of the same batch ({nb_s / 1e6:.0f} MB), "
+                                         f"{reps} reps over >= {args.cpu_seconds:.0f} s, median"}
+    if rank == 0 and world == 1 and not args.no_extras and name == "c2_tcp1500":
+        # secondary: 64 B UDP Mpkt/s (config 3) on rotating batches
+        eng3 = RxEngine(Config(synth.BOB_IPV4), device=dev)
+        b3 = [make_batch(eng3, "c3_udp64", 1000 * k, synth.SEED)[0] for k in range(8)]
+        r3 = eng3.results(b3[0].n)
+        w3, k3 = time_kernel(eng3, b3, r3, 40, 4, stream)
+        n3 = b3[0].n
+        out["c3_udp64"] = {"gbps": round(n3 * 64 * 40 / w3 / 1e9, 2), "mpkt_s": round(n3 * 40 / w3 / 1e6, 1),
+                           "kernel_ms_avg": round(float(np.mean(k3)) * 1e3, 4)}
+        del b3, r3, eng3
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""ctypes binding of include/dk_rx.h (libdk_rx.so, built in-tree for gfx950 by __graft_entry__.build()).
+
+No fallback: if the HIP library is missing, importing the engine raises. The structures below mirror the C header
+field for field; tests/test_abi.py checks their sizes and that every function the header declares is exported.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_int32, c_uint8, c_uint16, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libdk_rx.so")
+
+DK_FLOW_NONE = 0xFFFFFFFF
+DK_FLOW_TCP_ACTIVE, DK_FLOW_TCP_PASSIVE, DK_FLOW_UDP = 1, 2, 3
+
+# enum dk_verdict (include/dk_rx.h), SURVEY.md Appendix A.
+VERDICTS = [
+    "OK_TCP", "OK_UDP", "ARP", "ICMP", "IPV6", "ETH_SHORT", "ETH_TYPE", "IP_SHORT", "IP_VERSION", "IP_IHL_SMALL",
+    "IP_HDR_TRUNC", "IP_TOTLEN_SMALL", "IP_TOTLEN_BIG", "IP_EVIL", "IP_MF", "IP_FRAGOFF", "IP_TTL", "IP_PROTO",
+    "IP_CSUM_FFFF", "IP_CSUM", "IP_DST", "IP_SRC", "TCP_SHORT", "TCP_DOFF_TRUNC", "TCP_DOFF_SMALL", "TCP_CSUM",
+    "TCP_OPT", "TCP_OPT_EIO", "TCP_NOSOCK", "UDP_SHORT", "UDP_LEN", "UDP_CSUM", "UDP_NOSOCK", "BAD_DESC",
+]
+V = {name: i for i, name in enumerate(VERDICTS)}
+DK_V_COUNT = len(VERDICTS)
+
+# numpy mirror of struct dk_flow (16 bytes).
+FLOW_DTYPE = np.dtype([("kind", "<u4"), ("local_ip", "<u4"), ("remote_ip", "<u4"),
+                       ("local_port", "<u2"), ("remote_port", "<u2")])
+assert FLOW_DTYPE.itemsize == 16
+
+
+class DkRxCfg(ctypes.Structure):
+    _fields_ = [("local_ipv4", c_uint32), ("tcp_rx_checksum_offload", c_uint8),
+                ("udp_rx_checksum_offload", c_uint8), ("reserved", c_uint16), ("device", c_int32)]
+
+
+class DkFlow(ctypes.Structure):
+    _fields_ = [("kind", c_uint32), ("local_ip", c_uint32), ("remote_ip", c_uint32),
+                ("local_port", c_uint16), ("remote_port", c_uint16)]
+
+
+class DkRxBatch(ctypes.Structure):
+    _fields_ = [("frames", c_void_p), ("frames_bytes", c_uint64), ("off", c_void_p), ("len", c_void_p),
+                ("n", c_uint32), ("reserved", c_uint32)]
+
+
+RESULT_FIELDS = ["meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win",
+                 "flow_counts", "verdict_counts"]
+
+
+class DkRxResults(ctypes.Structure):
+    _fields_ = [(name, c_void_p) for name in RESULT_FIELDS]
+
+
+# (name, restype, argtypes) of every function include/dk_rx.h declares.
+FUNCTIONS = [
+    ("dk_rx_ctx_create", c_int, [POINTER(DkRxCfg), POINTER(c_void_p)]),
+    ("dk_rx_ctx_destroy", None, [c_void_p]),
+    ("dk_rx_flow_table_set", c_int, [c_void_p, c_void_p, c_uint32]),
+    ("dk_rx_flow_table_size", c_uint32, [c_void_p]),
+    ("dk_rx_process", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_void_p]),
+    ("dk_rx_process_host", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_uint32]),
+    ("dk_tx_checksum", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
+    ("dk_rx_verdict_name", c_char_p, [c_int]),
+    ("dk_rx_verdict_errno", c_int, [c_int]),
+    ("dk_rx_abi_version", c_uint32, []),
+    ("dk_rx_device_count", c_int, []),
+]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libdk_rx.so (fails loudly: there is no CPU fallback for the product path)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7, NEEDED as
+    # "libamdhip64.so"). Loaded first, it also satisfies our NEEDED libamdhip64.so.7; loaded after us, it would be a
+    # second runtime and device pointers/streams would not be shared.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(path)
+    for name, restype, argtypes in FUNCTIONS:
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    if path == LIB_PATH:
+        _lib = lib
+    return lib

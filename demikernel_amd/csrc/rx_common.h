@@ -1,0 +1,62 @@
+// rx_common.h — definitions shared by the host driver (rx_host.cpp) and the HIP kernels (rx_kernels.hip).
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/dk_rx.h"
+
+#if defined(__HIPCC__)
+#define DK_HD __host__ __device__ __forceinline__
+#else
+#define DK_HD inline
+#endif
+
+namespace dk {
+
+// Device socket table: open addressing, linear probing, power-of-two capacity >= 2 * entries (never full).
+// Slot = 16 bytes, one dwordx4 load per probe:
+//   x = kind << 24 | flow_id   (0 = empty; kind in 1..3, flow_id < 2^24)
+//   y = local_ip, z = remote_ip, w = local_port | remote_port << 16
+// Keys are normalised exactly as the reference builds them for lookups:
+//   TCP Active  (1, local_ip, remote_ip, local_port, remote_port)  SocketId::Active(local, remote)
+//   TCP Passive (2, local_ip, 0,         local_port, 0)            SocketId::Passive(local)
+//   UDP         (3, ip or 0.0.0.0, 0,    port,       0)            SocketAddrV4 (udp/peer.rs:38)
+constexpr uint32_t kMaxFlows = (1u << 24) - 1;
+constexpr uint32_t kMinTableSlots = 16;
+
+DK_HD uint32_t flow_hash(uint32_t kind, uint32_t lip, uint32_t rip, uint32_t ports) {
+    uint32_t h = kind * 0x9E3779B1u;
+    h ^= lip;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h ^= rip;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    h ^= ports;
+    h *= 0x27D4EB2Fu;
+    h ^= h >> 15;
+    return h;
+}
+
+// Kernel parameters (passed by value).
+struct RxParams {
+    const uint8_t* frames;
+    uint64_t frames_bytes;
+    const uint32_t* off;
+    const uint16_t* len;
+    uint32_t n;
+    uint32_t local_ip;
+    uint32_t tcp_offload;
+    uint32_t udp_offload;
+    const uint32_t* table;  // slots as 4 x u32
+    uint32_t table_mask;
+    uint32_t nflows;
+    dk_rx_results res;
+};
+
+}  // namespace dk
+
+// Launchers implemented in rx_kernels.hip (internal symbols, not part of the C ABI).
+int dk_launch_rx(const dk::RxParams& p, void* stream);
+int dk_launch_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
+                          uint32_t n, void* stream);

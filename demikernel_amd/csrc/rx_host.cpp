@@ -1,0 +1,366 @@
+// rx_host.cpp — host driver behind include/dk_rx.h: receive contexts, the device socket table, the HBM-resident
+// batch call, and the pinned-host pipeline (NIC ring / raw-socket buffer -> HBM -> results -> host).
+//
+// Replaces, on the receive side, the state SharedInetStack::new sets up (src/rust/inetstack/mod.rs:69-93): the local
+// IPv4 address (demikernel/config.rs:115), the rx checksum offload flags (runtime/network/config/tcp.rs:48-51,
+// udp.rs:26-30) and the socket maps TcpPeer::addresses / UdpPeer::addresses (tcp/peer.rs, udp/peer.rs:38).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <vector>
+
+#include "rx_common.h"
+
+namespace {
+
+constexpr int kPipeStreams = 3;
+constexpr uint32_t kDefaultChunkFrames = 1u << 16;
+constexpr uint64_t kMaxChunkBytes = 256ull << 20;
+
+struct Stage {  // device staging for one pipeline stream
+    hipStream_t stream = nullptr;
+    uint8_t* frames = nullptr;
+    uint64_t frames_cap = 0;
+    uint32_t* desc_off = nullptr;
+    uint16_t* desc_len = nullptr;
+    uint32_t* res = nullptr;  // 9 result arrays of chunk_cap entries
+    uint32_t cap = 0;
+};
+
+}  // namespace
+
+struct dk_rx_ctx {
+    dk_rx_cfg cfg{};
+    uint32_t* table = nullptr;  // device, (mask + 1) * 4 u32
+    uint32_t table_mask = 0;
+    uint32_t nflows = 0;
+    // host pipeline state (lazily allocated)
+    Stage stages[kPipeStreams];
+    uint64_t* d_flow_counts = nullptr;
+    uint32_t d_flow_cap = 0;
+    uint64_t* d_verdict_counts = nullptr;
+};
+
+namespace {
+
+struct DeviceGuard {  // set cfg.device for the duration of a call, restore afterwards
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+uint32_t next_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask) {
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, slots.size() * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+    if (hipMemcpy(d, slots.data(), slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return EIO;
+    }
+    if (c->table) (void)hipFree(c->table);
+    c->table = d;
+    c->table_mask = mask;
+    return 0;
+}
+
+void free_stage(Stage& s) {
+    if (s.frames) (void)hipFree(s.frames);
+    if (s.desc_off) (void)hipFree(s.desc_off);
+    if (s.desc_len) (void)hipFree(s.desc_len);
+    if (s.res) (void)hipFree(s.res);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Stage{};
+}
+
+int ensure_stage(Stage& s, uint32_t cap, uint64_t bytes) {
+    if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return EIO;
+    if (s.cap < cap) {
+        if (s.desc_off) (void)hipFree(s.desc_off);
+        if (s.desc_len) (void)hipFree(s.desc_len);
+        if (s.res) (void)hipFree(s.res);
+        s.desc_off = nullptr; s.desc_len = nullptr; s.res = nullptr; s.cap = 0;
+        if (hipMalloc(&s.desc_off, cap * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+        if (hipMalloc(&s.desc_len, cap * sizeof(uint16_t)) != hipSuccess) return ENOMEM;
+        if (hipMalloc(&s.res, (size_t)cap * 9 * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+        s.cap = cap;
+    }
+    if (s.frames_cap < bytes) {
+        if (s.frames) (void)hipFree(s.frames);
+        s.frames = nullptr; s.frames_cap = 0;
+        if (hipMalloc(&s.frames, bytes) != hipSuccess) return ENOMEM;
+        s.frames_cap = bytes;
+    }
+    return 0;
+}
+
+dk::RxParams base_params(const dk_rx_ctx* c) {
+    dk::RxParams p{};
+    p.local_ip = c->cfg.local_ipv4;
+    p.tcp_offload = c->cfg.tcp_rx_checksum_offload ? 1u : 0u;
+    p.udp_offload = c->cfg.udp_rx_checksum_offload ? 1u : 0u;
+    p.table = c->table;
+    p.table_mask = c->table_mask;
+    p.nflows = c->nflows;
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t dk_rx_abi_version(void) { return DK_RX_ABI_VERSION; }
+
+int dk_rx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
+    if (!cfg || !out) return EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) return EINVAL;
+    DeviceGuard g(cfg->device);
+    dk_rx_ctx* c = new dk_rx_ctx();
+    c->cfg = *cfg;
+    // Empty socket table: every probe misses.
+    std::vector<uint32_t> slots(dk::kMinTableSlots * 4, 0u);
+    int rc = upload_table(c, slots, dk::kMinTableSlots - 1);
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+void dk_rx_ctx_destroy(dk_rx_ctx* c) {
+    if (!c) return;
+    DeviceGuard g(c->cfg.device);
+    if (c->table) (void)hipFree(c->table);
+    for (Stage& s : c->stages) free_stage(s);
+    if (c->d_flow_counts) (void)hipFree(c->d_flow_counts);
+    if (c->d_verdict_counts) (void)hipFree(c->d_verdict_counts);
+    delete c;
+}
+
+int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
+    if (!c || (n && !flows) || n > dk::kMaxFlows) return EINVAL;
+    const uint32_t cap = std::max(dk::kMinTableSlots, next_pow2(2 * std::max(n, 1u)));
+    const uint32_t mask = cap - 1;
+    std::vector<uint32_t> slots((size_t)cap * 4, 0u);
+    for (uint32_t i = 0; i < n; i++) {
+        const dk_flow& f = flows[i];
+        uint32_t lip = f.local_ip, rip = 0, ports = f.local_port;
+        if (f.kind == DK_FLOW_TCP_ACTIVE) {
+            rip = f.remote_ip;
+            ports |= (uint32_t)f.remote_port << 16;
+        } else if (f.kind != DK_FLOW_TCP_PASSIVE && f.kind != DK_FLOW_UDP) {
+            return EINVAL;
+        }
+        uint32_t h = dk::flow_hash(f.kind, lip, rip, ports) & mask;
+        for (;;) {
+            uint32_t* s = &slots[(size_t)h * 4];
+            if (s[0] == 0 || ((s[0] >> 24) == f.kind && s[1] == lip && s[2] == rip && s[3] == ports)) {
+                s[0] = (f.kind << 24) | i;  // HashMap::insert: the last duplicate wins
+                s[1] = lip;
+                s[2] = rip;
+                s[3] = ports;
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+    }
+    DeviceGuard g(c->cfg.device);
+    int rc = upload_table(c, slots, mask);
+    if (rc == 0) c->nflows = n;
+    return rc;
+}
+
+uint32_t dk_rx_flow_table_size(const dk_rx_ctx* c) { return c ? c->nflows : 0; }
+
+int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, void* stream) {
+    if (!c || !b || !r) return EINVAL;
+    if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
+    if (b->n && (!r->meta || !r->src_ip || !r->dst_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
+    if (b->frames_bytes > (1ull << 32)) return EINVAL;
+    DeviceGuard g(c->cfg.device);
+    dk::RxParams p = base_params(c);
+    p.frames = b->frames;
+    p.frames_bytes = b->frames_bytes;
+    p.off = b->off;
+    p.len = b->len;
+    p.n = b->n;
+    p.res = *r;
+    return dk_launch_rx(p, stream);
+}
+
+int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, uint32_t chunk_frames) {
+    if (!c || !b || !r) return EINVAL;
+    if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
+    if (b->n && (!r->meta || !r->src_ip || !r->dst_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
+    if (b->frames_bytes > (1ull << 32)) return EINVAL;
+    if (b->n == 0) return 0;
+    DeviceGuard g(c->cfg.device);
+    const uint32_t chunk = chunk_frames ? chunk_frames : kDefaultChunkFrames;
+
+    // Chunk boundaries: consecutive frame ranges whose covering byte range stays under kMaxChunkBytes.
+    struct Chunk { uint32_t a, e; uint64_t lo, hi; };
+    std::vector<Chunk> chunks;
+    uint64_t max_bytes = 0;
+    for (uint32_t a = 0; a < b->n;) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        uint32_t e = a;
+        while (e < b->n && e - a < chunk) {
+            const uint64_t o = b->off[e], end = o + b->len[e];
+            if (end <= b->frames_bytes) {  // out-of-blob frames copy nothing; the kernel flags them BAD_DESC
+                const uint64_t nlo = std::min<uint64_t>(lo, o & ~(uint64_t)15), nhi = std::max(hi, end);
+                if (e > a && nhi - nlo > kMaxChunkBytes) break;
+                lo = nlo;
+                hi = nhi;
+            }
+            e++;
+        }
+        if (lo == UINT64_MAX) lo = hi = 0;
+        chunks.push_back({a, e, lo, hi});
+        max_bytes = std::max(max_bytes, hi - lo);
+        a = e;
+    }
+    uint32_t cap = 0;
+    for (auto& ch : chunks) cap = std::max(cap, ch.e - ch.a);
+    for (Stage& s : c->stages) {
+        int rc = ensure_stage(s, cap, std::max<uint64_t>(max_bytes, 16));
+        if (rc) return rc;
+    }
+    const uint32_t nfl = std::max(c->nflows, 1u);
+    if (r->flow_counts && c->d_flow_cap < nfl) {
+        if (c->d_flow_counts) (void)hipFree(c->d_flow_counts);
+        c->d_flow_counts = nullptr;
+        c->d_flow_cap = 0;
+        if (hipMalloc(&c->d_flow_counts, nfl * sizeof(uint64_t)) != hipSuccess) return ENOMEM;
+        c->d_flow_cap = nfl;
+    }
+    if (r->verdict_counts && !c->d_verdict_counts &&
+        hipMalloc(&c->d_verdict_counts, DK_V_COUNT * sizeof(uint64_t)) != hipSuccess)
+        return ENOMEM;
+    hipStream_t s0 = c->stages[0].stream;
+    if (r->flow_counts && hipMemsetAsync(c->d_flow_counts, 0, nfl * sizeof(uint64_t), s0) != hipSuccess) return EIO;
+    if (r->verdict_counts && hipMemsetAsync(c->d_verdict_counts, 0, DK_V_COUNT * sizeof(uint64_t), s0) != hipSuccess)
+        return EIO;
+    // Counter memsets on stage 0 must land before any stage's kernel: make the other stages wait on stage 0.
+    hipEvent_t ev0;
+    if (hipEventCreateWithFlags(&ev0, hipEventDisableTiming) != hipSuccess) return EIO;
+    (void)hipEventRecord(ev0, s0);
+    for (int k = 1; k < kPipeStreams; k++) (void)hipStreamWaitEvent(c->stages[k].stream, ev0, 0);
+
+    int rc = 0;
+    for (size_t k = 0; k < chunks.size() && rc == 0; k++) {
+        const Chunk& ch = chunks[k];
+        Stage& st = c->stages[k % kPipeStreams];
+        const uint32_t m = ch.e - ch.a;
+        // The staged copy starts at a 16-aligned host offset; a virtual base keeps the descriptors unchanged.
+        if (hipMemcpyAsync(st.frames, b->frames + ch.lo, ch.hi - ch.lo, hipMemcpyHostToDevice, st.stream) != hipSuccess ||
+            hipMemcpyAsync(st.desc_off, b->off + ch.a, m * sizeof(uint32_t), hipMemcpyHostToDevice, st.stream) != hipSuccess ||
+            hipMemcpyAsync(st.desc_len, b->len + ch.a, m * sizeof(uint16_t), hipMemcpyHostToDevice, st.stream) != hipSuccess) {
+            rc = EIO;
+            break;
+        }
+        dk::RxParams p = base_params(c);
+        p.frames = st.frames - ch.lo;
+        p.frames_bytes = ch.hi;
+        p.off = st.desc_off;
+        p.len = st.desc_len;
+        p.n = m;
+        uint32_t* R = st.res;
+        p.res.meta = R;
+        p.res.src_ip = R + (size_t)st.cap;
+        p.res.dst_ip = R + 2 * (size_t)st.cap;
+        p.res.ports = R + 3 * (size_t)st.cap;
+        p.res.payload = R + 4 * (size_t)st.cap;
+        p.res.flow_id = R + 5 * (size_t)st.cap;
+        p.res.tcp_seq = r->tcp_seq ? R + 6 * (size_t)st.cap : nullptr;
+        p.res.tcp_ack = r->tcp_ack ? R + 7 * (size_t)st.cap : nullptr;
+        p.res.tcp_win = r->tcp_win ? R + 8 * (size_t)st.cap : nullptr;
+        p.res.flow_counts = r->flow_counts ? c->d_flow_counts : nullptr;
+        p.res.verdict_counts = r->verdict_counts ? c->d_verdict_counts : nullptr;
+        rc = dk_launch_rx(p, st.stream);
+        if (rc) break;
+        uint32_t* outs[9] = {r->meta, r->src_ip, r->dst_ip, r->ports, r->payload, r->flow_id,
+                             r->tcp_seq, r->tcp_ack, r->tcp_win};
+        for (int a = 0; a < 9; a++) {
+            if (!outs[a]) continue;
+            if (hipMemcpyAsync(outs[a] + ch.a, R + a * (size_t)st.cap, m * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               st.stream) != hipSuccess) {
+                rc = EIO;
+                break;
+            }
+        }
+    }
+    for (Stage& s : c->stages)
+        if (s.stream && hipStreamSynchronize(s.stream) != hipSuccess) rc = rc ? rc : EIO;
+    (void)hipEventDestroy(ev0);
+    if (rc) return rc;
+    if (r->flow_counts) {
+        std::vector<uint64_t> tmp(nfl);
+        if (hipMemcpy(tmp.data(), c->d_flow_counts, nfl * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return EIO;
+        for (uint32_t k = 0; k < c->nflows; k++) r->flow_counts[k] += tmp[k];
+    }
+    if (r->verdict_counts) {
+        uint64_t tmp[DK_V_COUNT];
+        if (hipMemcpy(tmp, c->d_verdict_counts, sizeof(tmp), hipMemcpyDeviceToHost) != hipSuccess) return EIO;
+        for (int k = 0; k < DK_V_COUNT; k++) r->verdict_counts[k] += tmp[k];
+    }
+    return 0;
+}
+
+int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
+                   void* stream) {
+    if (n && (!frames || !off || !len)) return EINVAL;
+    return dk_launch_tx_checksum(frames, frames_bytes, off, len, n, stream);
+}
+
+const char* dk_rx_verdict_name(int v) {
+    static const char* const names[DK_V_COUNT] = {
+        "OK_TCP",         "OK_UDP",        "ARP",          "ICMP",           "IPV6",          "ETH_SHORT",
+        "ETH_TYPE",       "IP_SHORT",      "IP_VERSION",   "IP_IHL_SMALL",   "IP_HDR_TRUNC",  "IP_TOTLEN_SMALL",
+        "IP_TOTLEN_BIG",  "IP_EVIL",       "IP_MF",        "IP_FRAGOFF",     "IP_TTL",        "IP_PROTO",
+        "IP_CSUM_FFFF",   "IP_CSUM",       "IP_DST",       "IP_SRC",         "TCP_SHORT",     "TCP_DOFF_TRUNC",
+        "TCP_DOFF_SMALL", "TCP_CSUM",      "TCP_OPT",      "TCP_OPT_EIO",    "TCP_NOSOCK",    "UDP_SHORT",
+        "UDP_LEN",        "UDP_CSUM",      "UDP_NOSOCK",   "BAD_DESC"};
+    return (v >= 0 && v < DK_V_COUNT) ? names[v] : "UNKNOWN";
+}
+
+int dk_rx_verdict_errno(int v) {
+    switch (v) {
+        case DK_V_ETH_TYPE: case DK_V_IP_VERSION: case DK_V_IP_MF: case DK_V_IP_FRAGOFF: case DK_V_IP_PROTO:
+            return 95;  // ENOTSUP
+        case DK_V_TCP_OPT_EIO:
+            return 5;   // EIO
+        case DK_V_BAD_DESC:
+            return 22;  // EINVAL
+        case DK_V_ETH_SHORT: case DK_V_IP_SHORT: case DK_V_IP_IHL_SMALL: case DK_V_IP_HDR_TRUNC:
+        case DK_V_IP_TOTLEN_SMALL: case DK_V_IP_TOTLEN_BIG: case DK_V_IP_EVIL: case DK_V_IP_TTL:
+        case DK_V_IP_CSUM_FFFF: case DK_V_IP_CSUM: case DK_V_TCP_SHORT: case DK_V_TCP_DOFF_TRUNC:
+        case DK_V_TCP_DOFF_SMALL: case DK_V_TCP_CSUM: case DK_V_TCP_OPT: case DK_V_UDP_SHORT: case DK_V_UDP_LEN:
+        case DK_V_UDP_CSUM:
+            return 74;  // EBADMSG
+        default:
+            return 0;
+    }
+}
+
+}  // extern "C"

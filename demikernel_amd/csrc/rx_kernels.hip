@@ -1,0 +1,514 @@
+// rx_kernels.hip — CDNA4 (gfx950) kernels for the Demikernel receive-path transform.
+//
+// One kernel, dk_rx_kernel, does for a whole batch what the reference does frame by frame in
+//   Ethernet2Header::parse_and_strip  (src/rust/inetstack/protocols/layer2/ethernet2/header.rs:50-65)
+//   Ipv4Header::parse_and_strip       (layer3/ipv4/header.rs:111-225, compute_checksum :280-301)
+//   SharedLayer3Endpoint::receive     (layer3/mod.rs:71-120: dst/src filters, ICMP/ARP diversion)
+//   TcpHeader::parse_and_strip        (layer4/tcp/header.rs:162-327, tcp_checksum :433-509)
+//   UdpHeader::parse_and_strip        (layer4/udp/header.rs:57-94, checksum :140-193)
+//   TcpPeer::receive / UdpPeer::receive demux (layer4/tcp/peer.rs:220-255, layer4/udp/peer.rs:129-168)
+//
+// Work decomposition (one 256-thread workgroup = 4 waves = 256 consecutive frames):
+//   Phase A, lane per frame: load descriptor + the first 64 frame bytes (4 x dwordx4), parse every header field from
+//     registers, run every check that precedes the L4 checksum (Appendix A order), verify the IPv4 header checksum,
+//     sum the L4 bytes that sit in the 64-byte header window, and prefetch the partial tail block.
+//   Phase B, quarter-wave per frame: the full 16-byte blocks of the L4 region past byte 64 are summed by 16 lanes
+//     (6 x dwordx4 in flight per lane, 1.5 KB per quarter per round; 4 frames per wave per round), reduced with
+//     4 lane shuffles and handed to the owning lane through LDS.
+//   Phase C, lane per frame: close the one's-complement sum (pseudo-header, stored field removed), T4/U3 verdicts,
+//     TCP option walk (T5, byte loads: only option-bearing segments), hash-table demux, SoA result stores, counters.
+// Frames whose start is not 16-byte aligned, or whose IPv4 IHL != 5, take a per-lane byte-load path that implements
+// the same checks (phase A "slow"); they skip phase B.
+//
+// Checksum arithmetic: the reference sums big-endian 16-bit words into a u32 seeded with
+// 0xFFFF and folds by repeated subtraction of 0xFFFF. We sum little-endian 16-bit halves of dwords with
+// v_dot2_u32_u16 (x . {1,1}), in any order and grouping (the true integer sum, < 2^31 for 64 KiB), reduce mod 0xFFFF,
+// byte-swap (sum_BE == 256 * sum_LE mod 0xFFFF), add the pseudo-header and map the residue back to the reference's
+// result (0 -> 0, m -> 0xFFFF - m). Bit-exactness against the CPU restatement is tested, not assumed.
+#include <hip/hip_runtime.h>
+
+#include "rx_common.h"
+
+namespace dk {
+namespace {
+
+constexpr uint32_t kNone = 0xFFu;      // not yet decided
+constexpr uint32_t kPendTcp = 0xF0u;   // TCP header parsed; awaiting T4/T5/demux
+constexpr uint32_t kPendUdp = 0xF1u;   // UDP header parsed; awaiting U3/demux
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr uint32_t kCoopU = 6;         // dwordx4 loads per lane per phase-B round
+constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave covers per round
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t hsum2(uint32_t x, uint32_t acc) {  // acc + lo16(x) + hi16(x)
+    const us2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, x), one, acc, false);
+}
+__device__ __forceinline__ uint32_t block_sum(const uint4& b, uint32_t acc) {
+    acc = hsum2(b.x, acc);
+    acc = hsum2(b.y, acc);
+    acc = hsum2(b.z, acc);
+    return hsum2(b.w, acc);
+}
+// Mask of bytes [l, h) of one dword, 0 <= l, h <= 4 (empty when h <= l).
+__device__ __forceinline__ uint32_t bytes_mask(int l, int h) {
+    const uint32_t mh = h >= 4 ? 0xFFFFFFFFu : ((1u << (8 * h)) - 1u);
+    const uint32_t ml = l >= 4 ? 0xFFFFFFFFu : ((1u << (8 * l)) - 1u);
+    return mh & ~ml;
+}
+__device__ __forceinline__ int clamp4(int x) { return min(max(x, 0), 4); }
+// Sum of the LE halves of bytes [lo, hi) of a 16-byte block given as 4 dwords (lo even; bytes outside zeroed).
+__device__ __forceinline__ uint32_t block_sum_masked(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int lo, int hi,
+                                                     uint32_t acc) {
+    acc = hsum2(a & bytes_mask(clamp4(lo), clamp4(hi)), acc);
+    acc = hsum2(b & bytes_mask(clamp4(lo - 4), clamp4(hi - 4)), acc);
+    acc = hsum2(c & bytes_mask(clamp4(lo - 8), clamp4(hi - 8)), acc);
+    return hsum2(d & bytes_mask(clamp4(lo - 12), clamp4(hi - 12)), acc);
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+// x mod 0xFFFF in [0, 0xFFFE].
+__device__ __forceinline__ uint32_t mod_ffff(uint32_t x) {
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return x == 0xFFFFu ? 0u : x;
+}
+// The reference's `!fold(0xFFFF + S)` given m = S mod 0xFFFF (S = sum of BE words incl. pseudo-header).
+__device__ __forceinline__ uint32_t csum_from_residue(uint32_t m) { return m == 0 ? 0u : 0xFFFFu - m; }
+// BE residue of a LE-half sum.
+__device__ __forceinline__ uint32_t be_residue(uint32_t le_sum) { return bswap16(mod_ffff(le_sum)); }
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Byte accessors: registers (fast path, constant offsets < 64 after inlining) or global memory (slow path).
+// ---------------------------------------------------------------------------------------------------------------------
+struct RegAcc {
+    uint32_t w[16];  // frame bytes [0, 64), little-endian dwords
+    __device__ __forceinline__ uint32_t b8(uint32_t k) const { return (w[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
+    __device__ __forceinline__ uint32_t le16(uint32_t k) const { return (w[k >> 2] >> ((k & 2) * 8)) & 0xFFFFu; }
+    __device__ __forceinline__ uint32_t be16(uint32_t k) const { return bswap16(le16(k)); }
+    __device__ __forceinline__ uint32_t u32(uint32_t k) const {
+        return (k & 2) ? ((w[k >> 2] >> 16) | (w[(k >> 2) + 1] << 16)) : w[k >> 2];
+    }
+    __device__ __forceinline__ uint32_t be32(uint32_t k) const { return __builtin_bswap32(u32(k)); }
+};
+struct MemAcc {
+    const uint8_t* f;
+    __device__ __forceinline__ uint32_t b8(uint32_t k) const { return f[k]; }
+    __device__ __forceinline__ uint32_t le16(uint32_t k) const { return (uint32_t)f[k] | ((uint32_t)f[k + 1] << 8); }
+    __device__ __forceinline__ uint32_t be16(uint32_t k) const { return ((uint32_t)f[k] << 8) | f[k + 1]; }
+    __device__ __forceinline__ uint32_t u32(uint32_t k) const { return le16(k) | (le16(k + 2) << 16); }
+    __device__ __forceinline__ uint32_t be32(uint32_t k) const { return (be16(k) << 16) | be16(k + 2); }
+    // LE-half sum over frame bytes [s, e), s even, odd tail padded with zero (tcp/header.rs:497-499).
+    __device__ uint32_t sum_le16(uint32_t s, uint32_t e) const {
+        uint32_t acc = 0, k = s;
+        if ((reinterpret_cast<uintptr_t>(f) & 1) == 0) {
+            const uint16_t* h = reinterpret_cast<const uint16_t*>(f);
+            for (; k + 2 <= e; k += 2) acc += h[k >> 1];
+        } else {
+            for (; k + 2 <= e; k += 2) acc += le16(k);
+        }
+        if (k < e) acc += f[k];
+        return acc;
+    }
+};
+
+// Per-frame state carried from phase A to phase C.
+struct Lane {
+    uint32_t v;       // verdict or kPend*
+    uint32_t src, dst;
+    uint32_t ports;   // src_port | dst_port << 16
+    uint32_t b1213;   // tcp byte 12 | byte 13 << 8
+    uint32_t seq, ack, winurg;
+    uint32_t S, E;    // L4 region [S, E), frame-relative
+    uint32_t hlen;    // TCP data offset / 8 for UDP
+    uint32_t stored;  // stored L4 checksum (BE value)
+    uint32_t need;    // L4 checksum must be verified
+    uint32_t lsum;    // LE-half sum of the part of [S, E) summed in-lane
+};
+
+// Everything up to (not including) the L4 checksum, in Appendix A order. kFast: IHL == 5 asserted by the caller,
+// so S == 34 is a compile-time constant and every field offset folds to a register extract.
+template <bool kFast, class A>
+__device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const RxParams& P, Lane& L) {
+    L.v = kNone;
+    if (len < 14) { L.v = DK_V_ETH_SHORT; return; }                          // E1
+    const uint32_t et = a.be16(12);
+    if (et != 0x0806u && et != 0x0800u && et != 0x86ddu) { L.v = DK_V_ETH_TYPE; return; }  // E2
+    if (et == 0x0806u) { L.v = DK_V_ARP; return; }
+    if (et == 0x86ddu) { L.v = DK_V_IPV6; return; }
+    const uint32_t iplen = len - 14;
+    if (iplen < 20) { L.v = DK_V_IP_SHORT; return; }                         // I1
+    const uint32_t b14 = a.b8(14);
+    if ((b14 >> 4) != 4) { L.v = DK_V_IP_VERSION; return; }                  // I2
+    const uint32_t hs = (b14 & 15u) * 4;
+    if (hs < 20) { L.v = DK_V_IP_IHL_SMALL; return; }                        // I3
+    if (iplen < hs) { L.v = DK_V_IP_HDR_TRUNC; return; }                     // I4
+    const uint32_t tot = a.be16(16);
+    if (tot < hs) { L.v = DK_V_IP_TOTLEN_SMALL; return; }                    // I5
+    if (tot > iplen) { L.v = DK_V_IP_TOTLEN_BIG; return; }                   // I6
+    const uint32_t flags = a.b8(20) >> 5;
+    if (flags & 4u) { L.v = DK_V_IP_EVIL; return; }                          // I7
+    if (flags & 1u) { L.v = DK_V_IP_MF; return; }                            // I8
+    if (a.be16(20) & 0x1FFFu) { L.v = DK_V_IP_FRAGOFF; return; }             // I9
+    if (a.b8(22) == 0) { L.v = DK_V_IP_TTL; return; }                        // I10
+    const uint32_t proto = a.b8(23);
+    if (proto != 1u && proto != 6u && proto != 17u) { L.v = DK_V_IP_PROTO; return; }  // I11
+    const uint32_t ipcs = a.be16(24);
+    if (ipcs == 0xFFFFu) { L.v = DK_V_IP_CSUM_FFFF; return; }                // I12
+    // compute_checksum: 9 words of the first 20 bytes, checksum word skipped (ipv4/header.rs:280-301).
+    const uint32_t hsum = a.le16(14) + a.le16(16) + a.le16(18) + a.le16(20) + a.le16(22) + a.le16(26) + a.le16(28) +
+                          a.le16(30) + a.le16(32);
+    if (csum_from_residue(be_residue(hsum)) != ipcs) { L.v = DK_V_IP_CSUM; return; }  // I13
+    const uint32_t src = a.u32(26), dst = a.u32(30);
+    if (dst != P.local_ip && dst != 0xFFFFFFFFu) { L.v = DK_V_IP_DST; return; }       // F1
+    if (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) { L.v = DK_V_IP_SRC; return; }  // F2
+    if (proto == 1u) { L.v = DK_V_ICMP; return; }
+    const uint32_t S = kFast ? 34u : 14u + hs;
+    const uint32_t seg = tot - hs;
+    L.src = src;
+    L.dst = dst;
+    L.S = S;
+    L.E = 14 + tot;
+    if (proto == 6u) {
+        if (seg < 20) { L.v = DK_V_TCP_SHORT; return; }                      // T1
+        const uint32_t b12 = a.b8(S + 12);
+        const uint32_t doff = (b12 >> 4) * 4;
+        if (seg < doff) { L.v = DK_V_TCP_DOFF_TRUNC; return; }               // T2
+        if (doff < 20) { L.v = DK_V_TCP_DOFF_SMALL; return; }                // T3
+        L.ports = a.be16(S) | (a.be16(S + 2) << 16);
+        L.seq = a.be32(S + 4);
+        L.ack = a.be32(S + 8);
+        L.b1213 = b12 | (a.b8(S + 13) << 8);
+        L.winurg = a.be16(S + 14) | (a.be16(S + 18) << 16);
+        L.stored = a.be16(S + 16);
+        L.hlen = doff;
+        L.need = P.tcp_offload ? 0u : 1u;
+        L.v = kPendTcp;
+    } else {
+        if (seg < 8) { L.v = DK_V_UDP_SHORT; return; }                       // U1
+        if (a.be16(S + 4) != seg) { L.v = DK_V_UDP_LEN; return; }            // U2
+        L.ports = a.be16(S) | (a.be16(S + 2) << 16);
+        L.stored = a.be16(S + 6);
+        L.hlen = 8;
+        L.need = (!P.udp_offload && L.stored != 0) ? 1u : 0u;                // U3 precondition (udp/header.rs:78-82)
+        L.v = kPendUdp;
+    }
+}
+
+// TCP option walk (tcp/header.rs:215-302), over the option bytes in global memory. Returns 0 (ok), DK_V_TCP_OPT
+// (EBADMSG) or DK_V_TCP_OPT_EIO (truncated read: std::io::Cursor::read_exact -> io::Error -> EIO).
+__device__ __noinline__ uint32_t tcp_options(const uint8_t* o, uint32_t n) {
+    uint32_t pos = 0, nopt = 0;
+    while (pos < n) {
+        const uint32_t kind = o[pos++];
+        if (kind == 0) break;
+        if (kind == 1) continue;
+        uint32_t body;
+        if (kind == 2 || kind == 3 || kind == 4 || kind == 5 || kind == 8) {
+            if (pos >= n) return DK_V_TCP_OPT_EIO;
+            const uint32_t l = o[pos++];
+            if (kind == 2) { if (l != 4) return DK_V_TCP_OPT; body = 2; }
+            else if (kind == 3) { if (l != 3) return DK_V_TCP_OPT; body = 1; }
+            else if (kind == 4) { if (l != 2) return DK_V_TCP_OPT; body = 0; }
+            else if (kind == 5) {
+                if (l != 10 && l != 18 && l != 26 && l != 34) return DK_V_TCP_OPT;
+                body = l - 2;  // num_sacks * 8, read in 4-byte pieces
+            } else { if (l != 10) return DK_V_TCP_OPT; body = 8; }
+            if (n - pos < body) return DK_V_TCP_OPT_EIO;
+            pos += body;
+        } else {
+            return DK_V_TCP_OPT;
+        }
+        if (nopt >= 5) return DK_V_TCP_OPT;  // "too many TCP options provided"
+        nopt++;
+    }
+    return 0;
+}
+
+// Open-addressing probe of the device socket table (see rx_common.h).
+__device__ __forceinline__ uint32_t probe(const RxParams& P, uint32_t kind, uint32_t lip, uint32_t rip,
+                                          uint32_t lport_rport) {
+    const uint4* T = reinterpret_cast<const uint4*>(P.table);
+    uint32_t h = flow_hash(kind, lip, rip, lport_rport) & P.table_mask;
+    for (uint32_t i = 0; i <= P.table_mask; i++) {
+        const uint4 s = T[h];
+        if (s.x == 0) break;
+        if ((s.x >> 24) == kind && s.y == lip && s.z == rip && s.w == lport_rport) return s.x & 0xFFFFFFu;
+        h = (h + 1) & P.table_mask;
+    }
+    return DK_FLOW_NONE;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__global__ __launch_bounds__(kBlock) void dk_rx_kernel(RxParams P) {
+    __shared__ uint32_t s_list[kWaves][64];   // phase B: coop frame lanes, in rank order
+    __shared__ uint32_t s_csum[kWaves][64];   // phase B: coop sums by owner lane
+    __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6;
+    const uint32_t i = blockIdx.x * kBlock + tid;
+    const bool live = i < P.n;
+    if (tid < DK_V_COUNT) s_vh[tid] = 0;
+
+    // ---------------- Phase A: descriptor, header window, parse ----------------
+    uint32_t off = 0, len = 0;
+    if (live) {
+        off = P.off[i];
+        len = P.len[i];
+    }
+    const bool inb = live && (uint64_t)off + len <= P.frames_bytes;
+    const uint8_t* f = P.frames + off;
+    const bool aligned = (reinterpret_cast<uintptr_t>(f) & 15) == 0;
+
+    RegAcc R;
+    {
+        const uint4* fp = reinterpret_cast<const uint4*>(f);
+        const bool al = inb && aligned;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (al && (uint32_t)(16 * k) < len) q = fp[k];
+            R.w[4 * k + 0] = q.x;
+            R.w[4 * k + 1] = q.y;
+            R.w[4 * k + 2] = q.z;
+            R.w[4 * k + 3] = q.w;
+        }
+    }
+    // Fast path: aligned, whole Ethernet + IPv4 fixed header present, IHL == 5.
+    const bool fast = inb && aligned && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u;
+
+    Lane L;
+    L.v = kNone; L.src = L.dst = L.ports = L.b1213 = L.seq = L.ack = L.winurg = 0;
+    L.S = L.E = L.hlen = L.stored = L.need = L.lsum = 0;
+    uint4 tail = make_uint4(0, 0, 0, 0);
+    uint32_t nblk = 0;  // phase-B blocks of this frame
+
+    if (!live) {
+        L.v = kNone;
+    } else if (!inb) {
+        L.v = DK_V_BAD_DESC;
+    } else if (fast) {
+        parse_headers<true>(R, len, P, L);
+        if (L.need) {
+            const int E = (int)L.E;
+            // bytes [34, min(E, 64)) from the header window: block 2 (bytes 32..47) and block 3 (48..63)
+            uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
+            s = block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
+            L.lsum = s;
+            if (E > 64) {
+                const uint32_t fe = L.E & ~15u;
+                nblk = (fe - 64) >> 4;
+                if (L.E & 15u) tail = *reinterpret_cast<const uint4*>(f + fe);  // prefetch; summed in phase C
+            }
+        }
+    } else {
+        const MemAcc M{f};
+        parse_headers<false>(M, len, P, L);
+        if (L.need) L.lsum = M.sum_le16(L.S, L.E);
+    }
+
+    // ---------------- Phase B: quarter-wave sums of the full 16-byte blocks in [64, E & ~15) ----------------
+    {
+        const uint64_t cm = __ballot(nblk != 0);
+        const uint32_t ncoop = (uint32_t)__popcll(cm);
+        if (ncoop) {
+            if (nblk) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+                s_list[wv][rank] = lane;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t q = lane >> 4, l16 = lane & 15;
+            const uint32_t cbase = off + 64;
+            for (uint32_t r = 0; r * 4 < ncoop; r++) {
+                const uint32_t k = r * 4 + q;
+                const bool has = k < ncoop;
+                const uint32_t j = has ? s_list[wv][k] : 0u;
+                // Both shuffles run with every lane active: ds_bpermute reads 0 from a source lane that is
+                // exec-masked off, and the owner lane j may sit in a quarter with no frame this round.
+                const uint32_t fb = __shfl(cbase, (int)j);
+                const uint32_t nb_j = __shfl(nblk, (int)j);
+                const uint32_t nb = has ? nb_j : 0u;
+                uint32_t nit = (nb + kCoopSpan - 1) / kCoopSpan;
+                nit = max(nit, (uint32_t)__shfl_xor(nit, 16));
+                nit = max(nit, (uint32_t)__shfl_xor(nit, 32));
+                const uint32_t maxit = __builtin_amdgcn_readfirstlane(nit);
+                const uint4* base = reinterpret_cast<const uint4*>(P.frames + fb);
+                uint32_t acc = 0;
+                for (uint32_t it = 0; it < maxit; it++) {
+                    const uint32_t b0 = it * kCoopSpan + l16;
+                    uint4 d[kCoopU];
+#pragma unroll
+                    for (uint32_t u = 0; u < kCoopU; u++) {
+                        const uint32_t b = b0 + 16 * u;
+                        d[u] = b < nb ? base[b] : make_uint4(0, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kCoopU; u++) acc = block_sum(d[u], acc);
+                }
+                acc += (uint32_t)__shfl_xor(acc, 1);
+                acc += (uint32_t)__shfl_xor(acc, 2);
+                acc += (uint32_t)__shfl_xor(acc, 4);
+                acc += (uint32_t)__shfl_xor(acc, 8);
+                if (has && l16 == 0) s_csum[wv][j] = acc;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (nblk) L.lsum += s_csum[wv][lane];
+        }
+    }
+
+    // ---------------- Phase C: checksum verdicts, options, demux, results ----------------
+    uint32_t fid = DK_FLOW_NONE;
+    if (L.v == kPendTcp || L.v == kPendUdp) {
+        const bool tcp = L.v == kPendTcp;
+        if (L.need) {
+            uint32_t s = L.lsum;
+            if (L.E > 64 && (L.E & 15u) && fast) s = block_sum_masked(tail.x, tail.y, tail.z, tail.w, 0, (int)(L.E & 15u), s);
+            s -= bswap16(L.stored);  // the stored field is in the summed region; the reference sums it as zero
+            const uint32_t seg = L.E - L.S;
+            const uint32_t lip = P.local_ip;
+            // pseudo-header: src, local (tcp/peer.rs:223-228, udp/peer.rs:134), protocol, segment length (BE words)
+            const uint32_t pseudo = bswap16(L.src & 0xFFFFu) + bswap16(L.src >> 16) + bswap16(lip & 0xFFFFu) +
+                                    bswap16(lip >> 16) + (tcp ? 6u : 17u) + seg;
+            const uint32_t c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
+            if (c != L.stored) L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
+        }
+        if (L.v == kPendTcp && L.hlen > 20) {
+            const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20);
+            if (e) L.v = e;
+        }
+        const uint32_t sport = L.ports & 0xFFFFu, dport = L.ports >> 16;
+        if (L.v == kPendTcp) {
+            // SocketId::Active(local=(local_ip, dport), remote=(src, sport)), then Passive(local) (tcp/peer.rs:241-251)
+            fid = probe(P, DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, dport | (sport << 16));
+            if (fid == DK_FLOW_NONE) fid = probe(P, DK_FLOW_TCP_PASSIVE, P.local_ip, 0u, dport);
+            L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
+        } else if (L.v == kPendUdp) {
+            // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
+            fid = probe(P, DK_FLOW_UDP, P.local_ip, 0u, dport);
+            if (fid == DK_FLOW_NONE) fid = probe(P, DK_FLOW_UDP, 0u, 0u, dport);
+            L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
+        }
+    }
+
+    const uint32_t v = L.v;
+    if (live) {
+        const bool full = v == DK_V_OK_TCP || v == DK_V_TCP_NOSOCK || v == DK_V_OK_UDP || v == DK_V_UDP_NOSOCK;
+        const bool is_tcp = v == DK_V_OK_TCP || v == DK_V_TCP_NOSOCK;
+        uint32_t meta = v, src = 0, dst = 0, ports = 0, pay = 0, seq = 0, ack = 0, win = 0;
+        if (full) {
+            meta |= is_tcp ? ((6u << 8) | ((L.b1213 >> 8) << 16) | ((L.b1213 & 0xFFu) << 24)) : (17u << 8);
+            src = L.src;
+            dst = L.dst;
+            ports = L.ports;
+            const uint32_t poff = L.S + L.hlen;
+            pay = poff | ((L.E - poff) << 16);
+            if (is_tcp) { seq = L.seq; ack = L.ack; win = L.winurg; }
+        }
+        P.res.meta[i] = meta;
+        P.res.src_ip[i] = src;
+        P.res.dst_ip[i] = dst;
+        P.res.ports[i] = ports;
+        P.res.payload[i] = pay;
+        P.res.flow_id[i] = fid;
+        if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
+        if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
+        if (P.res.tcp_win) P.res.tcp_win[i] = win;
+        if (P.res.flow_counts && (v == DK_V_OK_TCP || v == DK_V_OK_UDP))
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
+    }
+
+    // Verdict histogram: one LDS add per distinct verdict per wave, one global add per bin per workgroup.
+    if (P.res.verdict_counts) {
+        __syncthreads();
+        uint64_t todo = __ballot(live);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
+            const uint64_t m = __ballot(live && v == v0);
+            if (lane == leader) atomicAdd(&s_vh[v0], (uint32_t)__popcll(m));
+            todo &= ~m;
+        }
+        __syncthreads();
+        if (tid < DK_V_COUNT && s_vh[tid])
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// TX checksum fill: lane per frame, byte-granular sums (the TX path is not the benchmark).
+// Mirrors Ipv4Header::serialize_and_attach (ipv4/header.rs:229-266), TcpHeader::serialize_and_attach
+// (tcp/header.rs:397-404) and UdpHeader::serialize_and_attach (udp/header.rs:119-124) with offload off.
+// ---------------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void dk_tx_checksum_kernel(uint8_t* frames, uint64_t frames_bytes,
+                                                                const uint32_t* off, const uint16_t* lens,
+                                                                uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = off[i], len = lens[i];
+    if ((uint64_t)o + len > frames_bytes || len < 34) return;
+    uint8_t* f = frames + o;
+    const MemAcc M{f};
+    if (M.be16(12) != 0x0800u) return;
+    const uint32_t hs = (f[14] & 15u) * 4;
+    const uint32_t tot = M.be16(16);
+    if (hs < 20 || 14 + tot > len || tot < hs) return;
+    f[24] = 0;
+    f[25] = 0;
+    const uint32_t hsum = M.le16(14) + M.le16(16) + M.le16(18) + M.le16(20) + M.le16(22) + M.le16(26) + M.le16(28) +
+                          M.le16(30) + M.le16(32);
+    const uint32_t ipc = csum_from_residue(be_residue(hsum));
+    f[24] = (uint8_t)(ipc >> 8);
+    f[25] = (uint8_t)ipc;
+    const uint32_t proto = f[23];
+    const uint32_t S = 14 + hs, E = 14 + tot, seg = tot - hs;
+    uint32_t cs_at;
+    if (proto == 6u) {
+        if (seg < 20) return;
+        const uint32_t doff = (f[S + 12] >> 4) * 4u;
+        if (doff < 20 || doff > seg) return;
+        cs_at = S + 16;
+    } else if (proto == 17u) {
+        if (seg < 8) return;
+        cs_at = S + 6;
+    } else {
+        return;
+    }
+    f[cs_at] = 0;
+    f[cs_at + 1] = 0;
+    const uint32_t s = M.sum_le16(S, E);
+    const uint32_t src = M.u32(26), dst = M.u32(30);
+    const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) + bswap16(dst >> 16) +
+                            proto + seg;
+    const uint32_t c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
+    f[cs_at] = (uint8_t)(c >> 8);
+    f[cs_at + 1] = (uint8_t)c;
+}
+
+}  // namespace
+}  // namespace dk
+
+int dk_launch_rx(const dk::RxParams& p, void* stream) {
+    if (p.n == 0) return 0;
+    const uint32_t grid = (p.n + dk::kBlock - 1) / dk::kBlock;
+    hipLaunchKernelGGL(dk::dk_rx_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : 5;
+}
+
+int dk_launch_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
+                          uint32_t n, void* stream) {
+    if (n == 0) return 0;
+    const uint32_t grid = (n + dk::kBlock - 1) / dk::kBlock;
+    hipLaunchKernelGGL(dk::dk_tx_checksum_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, frames,
+                       frames_bytes, off, len, n);
+    return hipGetLastError() == hipSuccess ? 0 : 5;
+}

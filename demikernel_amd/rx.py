@@ -1,0 +1,220 @@
+"""Host-side mirror of the reference's receive interface, over the C ABI (include/dk_rx.h).
+
+The reference (Rust, src/rust/) receives frames one by one through
+    PhysicalLayer::receive -> SharedLayer2Endpoint::receive -> SharedLayer3Endpoint::receive
+    -> Peer::receive_batch -> TcpPeer::receive / UdpPeer::receive -> socket.receive(...)
+(inetstack/protocols/layer1/mod.rs:27-33 ... layer4/tcp/peer.rs:220-255, layer4/udp/peer.rs:129-168).
+`RxEngine.receive_batch` runs that whole chain for a batch on one MI355X and returns, per frame, what the chain
+decides: the verdict (delivered / diverted / dropped / parse error with the reference's errno), the 4-tuple, the
+payload window (the DemiBuffer after adjust/trim) and the socket (flow id). Errors follow runtime/fail.rs: a call
+failure raises `Fail(errno, cause)`; per-frame failures are verdicts.
+
+torch is used only to own device memory and to name the HIP stream; the ABI takes plain pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import socket
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+from ._native import DK_V_COUNT, FLOW_DTYPE, V, VERDICTS  # noqa: F401  (re-exported)
+
+
+class Fail(Exception):
+    """runtime/fail.rs `Fail { errno, cause }`."""
+
+    def __init__(self, errno: int, cause: str):
+        super().__init__(f"Error {errno}: {cause}")
+        self.errno = errno
+        self.cause = cause
+
+
+def ipv4(addr: str) -> int:
+    """Ipv4Addr -> u32 whose in-memory bytes are the octets (s_addr order), as the ABI takes it."""
+    return int.from_bytes(socket.inet_aton(addr), "little")
+
+
+def ipv4_str(a: int) -> str:
+    return socket.inet_ntoa(int(a).to_bytes(4, "little"))
+
+
+@dataclass
+class Config:
+    """The hot-path subset of the reference YAML config (demikernel/config.rs:20-48, :115, :340-346)."""
+
+    local_ipv4_addr: str
+    tcp_checksum_offload: bool = False
+    udp_checksum_offload: bool = False
+
+
+class SocketId:
+    """Constructors for socket-table entries (runtime/network/socket/mod.rs:22-26; UDP: udp/peer.rs:38)."""
+
+    @staticmethod
+    def Active(local: tuple[str, int], remote: tuple[str, int]) -> tuple:
+        return (N.DK_FLOW_TCP_ACTIVE, ipv4(local[0]), ipv4(remote[0]), local[1], remote[1])
+
+    @staticmethod
+    def Passive(local: tuple[str, int]) -> tuple:
+        return (N.DK_FLOW_TCP_PASSIVE, ipv4(local[0]), 0, local[1], 0)
+
+    @staticmethod
+    def Udp(local: tuple[str, int]) -> tuple:
+        return (N.DK_FLOW_UDP, ipv4(local[0]), 0, local[1], 0)
+
+
+def flow_array(entries) -> np.ndarray:
+    """List of SocketId tuples -> FLOW_DTYPE array (flow id = index)."""
+    a = np.zeros(len(entries), dtype=FLOW_DTYPE)
+    for i, (k, lip, rip, lp, rp) in enumerate(entries):
+        a[i] = (k, lip, rip, lp, rp)
+    return a
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise Fail(rc, what)
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data
+
+
+class FrameBatch:
+    """An HBM-resident batch: packed frame blob + per-frame (u32 offset, u16 length) descriptors."""
+
+    def __init__(self, blob, off, lens, frames_bytes: Optional[int] = None):
+        import torch
+
+        assert blob.dtype == torch.uint8 and blob.is_cuda
+        assert off.dtype == torch.int32 and lens.dtype == torch.int16 and off.numel() == lens.numel()
+        self.blob, self.off, self.len = blob, off, lens
+        self.n = off.numel()
+        self.frames_bytes = blob.numel() if frames_bytes is None else frames_bytes
+
+    @classmethod
+    def from_numpy(cls, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, device: int = 0) -> "FrameBatch":
+        import torch
+
+        dev = torch.device("cuda", device)
+        b = torch.from_numpy(np.ascontiguousarray(blob, dtype=np.uint8)).to(dev)
+        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint32).view(np.int32)).to(dev)
+        ln = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint16).view(np.int16)).to(dev)
+        return cls(b, o, ln)
+
+    def c_struct(self) -> N.DkRxBatch:
+        return N.DkRxBatch(_ptr(self.blob), self.frames_bytes, _ptr(self.off), _ptr(self.len), self.n, 0)
+
+
+class RxResults:
+    """Device (or host) result arrays, struct-of-arrays, int32/int64 storage reinterpreted as the ABI's u32/u64."""
+
+    ARRAYS = ["meta", "src_ip", "dst_ip", "ports", "payload", "flow_id"]
+    TCP_ARRAYS = ["tcp_seq", "tcp_ack", "tcp_win"]
+
+    def __init__(self, n: int, nflows: int, *, device=None, tcp_fields: bool = False, counts: bool = True,
+                 host: bool = False):
+        import torch
+
+        kw = dict(device=device) if not host else dict(pin_memory=torch.cuda.is_available())
+        self.n = n
+        self.t = {}
+        for name in self.ARRAYS + (self.TCP_ARRAYS if tcp_fields else []):
+            self.t[name] = torch.zeros(n, dtype=torch.int32, **kw)
+        if counts:
+            self.t["flow_counts"] = torch.zeros(max(nflows, 1), dtype=torch.int64, **kw)
+            self.t["verdict_counts"] = torch.zeros(DK_V_COUNT, dtype=torch.int64, **kw)
+
+    def c_struct(self) -> N.DkRxResults:
+        return N.DkRxResults(*[_ptr(self.t.get(name)) for name in N.RESULT_FIELDS])
+
+    def zero_counts(self) -> None:
+        for k in ("flow_counts", "verdict_counts"):
+            if k in self.t:
+                self.t[k].zero_()
+
+    def to_numpy(self) -> dict:
+        out = {}
+        for k, v in self.t.items():
+            a = v.cpu().numpy()
+            out[k] = a.view(np.uint64) if a.dtype == np.int64 else a.view(np.uint32)
+        return out
+
+
+class RxEngine:
+    """Batch receive path on one GPU (the drop-in for layer2..layer4 receive + demux, see module docstring)."""
+
+    def __init__(self, config: Config, device: int = 0):
+        self.lib = N.load_library()
+        self.config = config
+        self.device = device
+        cfg = N.DkRxCfg(ipv4(config.local_ipv4_addr), int(config.tcp_checksum_offload),
+                        int(config.udp_checksum_offload), 0, device)
+        h = ctypes.c_void_p()
+        _check(self.lib.dk_rx_ctx_create(ctypes.byref(cfg), ctypes.byref(h)), "dk_rx_ctx_create")
+        self._ctx = h
+        self.nflows = 0
+
+    def close(self) -> None:
+        if self._ctx:
+            self.lib.dk_rx_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_sockets(self, flows: np.ndarray) -> None:
+        flows = np.ascontiguousarray(flows, dtype=FLOW_DTYPE)
+        _check(self.lib.dk_rx_flow_table_set(self._ctx, flows.ctypes.data, len(flows)), "dk_rx_flow_table_set")
+        self.nflows = len(flows)
+
+    def results(self, n: int, *, tcp_fields: bool = False, counts: bool = True) -> RxResults:
+        import torch
+
+        return RxResults(n, self.nflows, device=torch.device("cuda", self.device), tcp_fields=tcp_fields,
+                         counts=counts)
+
+    def receive_batch(self, batch: FrameBatch, results: RxResults, stream=None) -> None:
+        """Asynchronous on `stream` (a torch.cuda.Stream; default: the current stream)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        b, r = batch.c_struct(), results.c_struct()
+        _check(self.lib.dk_rx_process(self._ctx, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(s.cuda_stream)),
+               "dk_rx_process")
+
+    def receive_batch_host(self, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, results: RxResults,
+                           chunk_frames: int = 0) -> None:
+        """Host-resident batch (NIC ring / socket buffer): pipelined H2D -> kernel -> D2H. Synchronous."""
+        b = N.DkRxBatch(blob.ctypes.data, blob.nbytes, off.ctypes.data, lens.ctypes.data, len(off), 0)
+        r = results.c_struct()
+        _check(self.lib.dk_rx_process_host(self._ctx, ctypes.byref(b), ctypes.byref(r), chunk_frames),
+               "dk_rx_process_host")
+
+    def tx_checksum(self, batch: FrameBatch, stream=None) -> None:
+        """Fill IPv4/TCP/UDP checksums in place (serialize_and_attach with tx offload off)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(self.lib.dk_tx_checksum(_ptr(batch.blob), batch.frames_bytes, _ptr(batch.off), _ptr(batch.len),
+                                       batch.n, ctypes.c_void_p(s.cuda_stream)), "dk_tx_checksum")
+
+
+def verdict_errno(v: int) -> int:
+    return N.load_library().dk_rx_verdict_errno(v)
+
+
+def raise_for_verdict(v: int) -> None:
+    """Turn an error verdict back into the reference's Fail (errno from the reference line it mirrors)."""
+    if v in (V["OK_TCP"], V["OK_UDP"]):
+        return
+    raise Fail(verdict_errno(v), VERDICTS[v])
