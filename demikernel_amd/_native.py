@@ -13,6 +13,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libdk_rx.so")
+# Tuning builds only (tools/variants.sh): load an alternative build of the same sources.
+LIB_PATH = os.environ.get("DK_RX_LIB_VARIANT", LIB_PATH)
 
 DK_FLOW_NONE = 0xFFFFFFFF
 DK_FLOW_TCP_ACTIVE, DK_FLOW_TCP_PASSIVE, DK_FLOW_UDP = 1, 2, 3
@@ -71,6 +73,11 @@ FUNCTIONS = [
     ("dk_rx_device_count", c_int, []),
 ]
 
+# include/dk_diag.h (diagnostics, not the receive ABI)
+DIAG_FUNCTIONS = [
+    ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
+]
+
 _lib = None
 
 
@@ -89,7 +96,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
-    for name, restype, argtypes in FUNCTIONS:
+    for name, restype, argtypes in FUNCTIONS + DIAG_FUNCTIONS:
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes

@@ -1,0 +1,75 @@
+// diag.hip — on-box HBM read-bandwidth probe (include/dk_diag.h). Not part of the receive path: bench.py uses it to
+// report the measured streaming-read ceiling next to the 8 TB/s spec (SURVEY.md §8(d) "Roofline").
+#include <hip/hip_runtime.h>
+
+#include "../../include/dk_diag.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kUnroll = 8;
+
+__device__ __forceinline__ uint4 ld(const uint4* p, bool nt) {
+    if (nt) {
+        uint4 v;
+        v.x = __builtin_nontemporal_load(&p->x);
+        v.y = __builtin_nontemporal_load(&p->y);
+        v.z = __builtin_nontemporal_load(&p->z);
+        v.w = __builtin_nontemporal_load(&p->w);
+        return v;
+    }
+    return *p;
+}
+
+// mode 0: grid-stride, the 8 loads of a lane one grid-stride apart.
+// mode 1: each wave streams a contiguous 8 KiB piece per step (lane-contiguous 16 B, 8 x 1 KiB in flight).
+// mode 2: as mode 1 with nontemporal loads.
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void read_probe(const uint4* __restrict__ p, uint64_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    if (kMode == 0) {
+        const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+        uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        for (; i + (kUnroll - 1) * stride < n16; i += kUnroll * stride) {
+            uint4 v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) v[u] = p[i + u * stride];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
+        }
+        for (; i < n16; i += stride) {
+            const uint4 v = p[i];
+            acc ^= v.x + v.y + v.z + v.w;
+        }
+    } else {
+        const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+        const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        const uint32_t lane = threadIdx.x & 63;
+        const uint64_t piece = 64 * kUnroll;  // 16-byte words per wave step
+        for (uint64_t base = w * piece; base < n16; base += nwaves * piece) {
+            uint4 v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) {
+                const uint64_t i = base + u * 64 + lane;
+                v[u] = i < n16 ? ld(p + i, kMode == 2) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
+        }
+    }
+    acc = __reduce_add_sync(~0ull, acc);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
+}
+
+}  // namespace
+
+extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode,
+                                  void* stream) {
+    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 2) return 22;
+    const uint4* p = (const uint4*)buf;
+    const hipStream_t s = (hipStream_t)stream;
+    if (mode == 0) hipLaunchKernelGGL(read_probe<0>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 1) hipLaunchKernelGGL(read_probe<1>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 2) hipLaunchKernelGGL(read_probe<2>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    return hipGetLastError() == hipSuccess ? 0 : 5;
+}

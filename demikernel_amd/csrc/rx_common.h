@@ -38,6 +38,13 @@ DK_HD uint32_t flow_hash(uint32_t kind, uint32_t lip, uint32_t rip, uint32_t por
     return h;
 }
 
+// Per-flow counting strategy (chosen per launch by the host).
+constexpr uint32_t kFlowNone = 0;    // no flow_counts requested
+constexpr uint32_t kFlowLds = 1;     // per-workgroup packed-u16 LDS histogram + scratch rows + reduce kernel
+constexpr uint32_t kFlowGlobal = 2;  // per-frame u64 global atomics (tables too large for LDS)
+constexpr uint32_t kMaxLdsFlowWords = 16384;  // 64 KiB of LDS -> up to 32768 flows on the LDS path
+constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
+
 // Kernel parameters (passed by value).
 struct RxParams {
     const uint8_t* frames;
@@ -51,12 +58,16 @@ struct RxParams {
     const uint32_t* table;  // slots as 4 x u32
     uint32_t table_mask;
     uint32_t nflows;
+    uint32_t flow_mode;      // kFlow*
+    uint32_t flow_words;     // kFlowLds: ceil(nflows / 2)
+    uint32_t* flow_scratch;  // kFlowLds: [grid][flow_words]
     dk_rx_results res;
 };
 
 }  // namespace dk
 
 // Launchers implemented in rx_kernels.hip (internal symbols, not part of the C ABI).
-int dk_launch_rx(const dk::RxParams& p, void* stream);
+int dk_rx_resident_blocks(uint32_t dyn_lds_bytes);  // occupancy of dk_rx_kernel per CU (0 on error)
+int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
 int dk_launch_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
                           uint32_t n, void* stream);

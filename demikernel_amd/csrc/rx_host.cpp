@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -19,6 +21,11 @@ constexpr int kPipeStreams = 3;
 constexpr uint32_t kDefaultChunkFrames = 1u << 16;
 constexpr uint64_t kMaxChunkBytes = 256ull << 20;
 
+struct FlowScratch {  // per-workgroup flow-count rows for the kFlowLds path (one per concurrent launch)
+    uint32_t* p = nullptr;
+    size_t words = 0;
+};
+
 struct Stage {  // device staging for one pipeline stream
     hipStream_t stream = nullptr;
     uint8_t* frames = nullptr;
@@ -27,6 +34,7 @@ struct Stage {  // device staging for one pipeline stream
     uint16_t* desc_len = nullptr;
     uint32_t* res = nullptr;  // 9 result arrays of chunk_cap entries
     uint32_t cap = 0;
+    FlowScratch scratch;
 };
 
 }  // namespace
@@ -41,6 +49,10 @@ struct dk_rx_ctx {
     uint64_t* d_flow_counts = nullptr;
     uint32_t d_flow_cap = 0;
     uint64_t* d_verdict_counts = nullptr;
+    FlowScratch scratch;      // for dk_rx_process (device-resident path)
+    uint32_t cu_count = 0;
+    uint32_t occ_dyn = ~0u;   // occupancy cache: dynamic LDS bytes -> resident blocks per CU
+    uint32_t occ_blocks = 0;
 };
 
 namespace {
@@ -75,7 +87,64 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
     return 0;
 }
 
+int ensure_scratch(FlowScratch& f, size_t words) {
+    if (f.words >= words) return 0;
+    if (f.p) (void)hipFree(f.p);
+    f.p = nullptr;
+    f.words = 0;
+    if (hipMalloc(&f.p, words * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+    f.words = words;
+    return 0;
+}
+
+void free_scratch(FlowScratch& f) {
+    if (f.p) (void)hipFree(f.p);
+    f = FlowScratch{};
+}
+
+// Choose the flow-count mode and the persistent grid, then launch (main kernel + flow reduce).
+int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
+    if (p.n == 0) return 0;
+    const uint32_t ntiles = (p.n + 255) / 256;
+    p.flow_mode = dk::kFlowNone;
+    p.flow_words = 0;
+    p.flow_scratch = nullptr;
+    uint32_t dyn = 0;
+    if (p.res.flow_counts && c->nflows) {
+        const uint32_t words = (c->nflows + 1) / 2;
+        if (words <= dk::kMaxLdsFlowWords) {
+            p.flow_mode = dk::kFlowLds;
+            p.flow_words = words;
+            dyn = words * 4;
+        } else {
+            p.flow_mode = dk::kFlowGlobal;
+        }
+    }
+    if (c->occ_dyn != dyn) {
+        c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn), 1);
+        c->occ_dyn = dyn;
+    }
+    // Resident workgroups per CU (measured, DESIGN.md "Tuning log"): large frames stream best with 2 (fewer
+    // concurrent frame streams per CU), small frames are issue-bound and want 4. The host only knows the blob size
+    // per frame, which is what the choice keys on.
+    const uint64_t bytes_per_frame = p.frames_bytes / p.n;
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, bytes_per_frame >= 1024 ? 2u : 4u);
+    if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
+    uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
+    if (p.flow_mode == dk::kFlowLds) {
+        grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
+        int rc = ensure_scratch(fs, (size_t)grid * p.flow_words);
+        if (rc) return rc;
+        p.flow_scratch = fs.p;
+    }
+    if (getenv("DK_RX_DEBUG"))
+        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u\n", p.n, ntiles, grid,
+                c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words);
+    return dk_launch_rx(p, grid, stream);
+}
+
 void free_stage(Stage& s) {
+    free_scratch(s.scratch);
     if (s.frames) (void)hipFree(s.frames);
     if (s.desc_off) (void)hipFree(s.desc_off);
     if (s.desc_len) (void)hipFree(s.desc_len);
@@ -136,6 +205,10 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     DeviceGuard g(cfg->device);
     dk_rx_ctx* c = new dk_rx_ctx();
     c->cfg = *cfg;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    c->cu_count = (uint32_t)cus;
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4, 0u);
     int rc = upload_table(c, slots, dk::kMinTableSlots - 1);
@@ -154,6 +227,7 @@ void dk_rx_ctx_destroy(dk_rx_ctx* c) {
     for (Stage& s : c->stages) free_stage(s);
     if (c->d_flow_counts) (void)hipFree(c->d_flow_counts);
     if (c->d_verdict_counts) (void)hipFree(c->d_verdict_counts);
+    free_scratch(c->scratch);
     delete c;
 }
 
@@ -205,7 +279,7 @@ int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, vo
     p.len = b->len;
     p.n = b->n;
     p.res = *r;
-    return dk_launch_rx(p, stream);
+    return launch_batch(c, p, c->scratch, stream);
 }
 
 int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, uint32_t chunk_frames) {
@@ -296,7 +370,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         p.res.tcp_win = r->tcp_win ? R + 8 * (size_t)st.cap : nullptr;
         p.res.flow_counts = r->flow_counts ? c->d_flow_counts : nullptr;
         p.res.verdict_counts = r->verdict_counts ? c->d_verdict_counts : nullptr;
-        rc = dk_launch_rx(p, st.stream);
+        rc = launch_batch(c, p, st.scratch, st.stream);
         if (rc) break;
         uint32_t* outs[9] = {r->meta, r->src_ip, r->dst_ip, r->ports, r->payload, r->flow_id,
                              r->tcp_seq, r->tcp_ack, r->tcp_win};

@@ -35,9 +35,19 @@ namespace {
 constexpr uint32_t kNone = 0xFFu;      // not yet decided
 constexpr uint32_t kPendTcp = 0xF0u;   // TCP header parsed; awaiting T4/T5/demux
 constexpr uint32_t kPendUdp = 0xF1u;   // UDP header parsed; awaiting U3/demux
+// Tuning knobs (compile-time; defaults are the measured best, see DESIGN.md "Tuning log").
+#ifndef DK_COOP_U
+#define DK_COOP_U 6
+#endif
+#ifndef DK_NT_LOADS
+#define DK_NT_LOADS 1
+#endif
+#ifndef DK_MIN_WAVES
+#define DK_MIN_WAVES 1
+#endif
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr uint32_t kCoopU = 6;         // dwordx4 loads per lane per phase-B round
+constexpr uint32_t kCoopU = DK_COOP_U; // dwordx4 loads per lane per phase-B round
 constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave covers per round
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -66,6 +76,20 @@ __device__ __forceinline__ uint32_t block_sum_masked(uint32_t a, uint32_t b, uin
     acc = hsum2(b & bytes_mask(clamp4(lo - 4), clamp4(hi - 4)), acc);
     acc = hsum2(c & bytes_mask(clamp4(lo - 8), clamp4(hi - 8)), acc);
     return hsum2(d & bytes_mask(clamp4(lo - 12), clamp4(hi - 12)), acc);
+}
+
+// Streaming 16-byte load of once-read frame bytes (nontemporal by default: +3-4 % on C2/C4).
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+#if DK_NT_LOADS
+    uint4 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    v.z = __builtin_nontemporal_load(&p->z);
+    v.w = __builtin_nontemporal_load(&p->w);
+    return v;
+#else
+    return *p;
+#endif
 }
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
@@ -243,17 +267,11 @@ __device__ __forceinline__ uint32_t probe(const RxParams& P, uint32_t kind, uint
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
-__global__ __launch_bounds__(kBlock) void dk_rx_kernel(RxParams P) {
-    __shared__ uint32_t s_list[kWaves][64];   // phase B: coop frame lanes, in rank order
-    __shared__ uint32_t s_csum[kWaves][64];   // phase B: coop sums by owner lane
-    __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = lane_id();
-    const uint32_t wv = tid >> 6;
-    const uint32_t i = blockIdx.x * kBlock + tid;
+// One frame per lane, 256 frames per workgroup tile: phases A, B, C and the result stores. Every lane of the
+// workgroup calls it (phase B is wave-cooperative). Returns the verdict and the flow id (DK_FLOW_NONE if none).
+__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t lane, uint32_t (*s_list)[64],
+                                        uint32_t (*s_csum)[64], uint32_t wv, uint32_t& v_out, uint32_t& fid_out) {
     const bool live = i < P.n;
-    if (tid < DK_V_COUNT) s_vh[tid] = 0;
 
     // ---------------- Phase A: descriptor, header window, parse ----------------
     uint32_t off = 0, len = 0;
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void dk_rx_kernel(RxParams P) {
 #pragma unroll
                     for (uint32_t u = 0; u < kCoopU; u++) {
                         const uint32_t b = b0 + 16 * u;
-                        d[u] = b < nb ? base[b] : make_uint4(0, 0, 0, 0);
+                        d[u] = b < nb ? ld_stream(base + b) : make_uint4(0, 0, 0, 0);
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < kCoopU; u++) acc = block_sum(d[u], acc);
@@ -423,25 +441,81 @@ __global__ __launch_bounds__(kBlock) void dk_rx_kernel(RxParams P) {
         if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
         if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
         if (P.res.tcp_win) P.res.tcp_win[i] = win;
-        if (P.res.flow_counts && (v == DK_V_OK_TCP || v == DK_V_OK_UDP))
-            atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
+    }
+    v_out = v;
+    fid_out = fid;
+}
+
+// Persistent kernel: workgroup b processes tiles b, b + G, b + 2G, ... (G = resident workgroups, host-chosen), so
+// per-workgroup state lives across tiles: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
+// histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
+// wraps). At exit the histogram row is written with plain stores to flow_scratch[b][*] and dk_flow_reduce_kernel adds
+// the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
+__global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P) {
+    __shared__ uint32_t s_list[kWaves][64];   // phase B: coop frame lanes, in rank order
+    __shared__ uint32_t s_csum[kWaves][64];   // phase B: coop sums by owner lane
+    __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6;
+    const bool lds_flows = P.flow_mode == kFlowLds;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
+    __syncthreads();
+
+    const uint32_t ntiles = (P.n + kBlock - 1) / kBlock;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t i = t * kBlock + tid;
+        uint32_t v, fid;
+        rx_tile(P, i, lane, s_list, s_csum, wv, v, fid);
+        const bool live = i < P.n;
+        if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
+            if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
+            else if (P.flow_mode == kFlowGlobal)
+                atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
+        }
+        if (P.res.verdict_counts) {  // one LDS add per distinct verdict per wave
+            uint64_t todo = __ballot(live);
+            while (todo) {
+                const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+                const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
+                const uint64_t m = __ballot(live && v == v0);
+                if (lane == leader) atomicAdd(&s_vh[v0], (uint32_t)__popcll(m));
+                todo &= ~m;
+            }
+        }
     }
 
-    // Verdict histogram: one LDS add per distinct verdict per wave, one global add per bin per workgroup.
-    if (P.res.verdict_counts) {
-        __syncthreads();
-        uint64_t todo = __ballot(live);
-        while (todo) {
-            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
-            const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
-            const uint64_t m = __ballot(live && v == v0);
-            if (lane == leader) atomicAdd(&s_vh[v0], (uint32_t)__popcll(m));
-            todo &= ~m;
-        }
-        __syncthreads();
-        if (tid < DK_V_COUNT && s_vh[tid])
-            atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
+    __syncthreads();
+    if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
+    if (lds_flows) {
+        uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.flow_words;
+        for (uint32_t k = tid; k < P.flow_words; k += kBlock) row[k] = s_flow[k];
     }
+}
+
+// Adds the per-workgroup packed-u16 rows of flow_scratch[rows][words] into flow_counts[nflows] (u64). Block (x, y)
+// sums rows [y * kReduceRows, ...) of 256 consecutive words (coalesced row reads, loads independent) and adds the two
+// 64-bit partials with device-scope atomics; (rows / kReduceRows) * nflows adds in all, contiguous per wave.
+constexpr uint32_t kReduceRows = 32;
+__global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* scratch, uint32_t rows,
+                                                                uint32_t words, uint32_t nflows, uint64_t* counts) {
+    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
+    if (w >= words) return;
+    const uint32_t r0 = blockIdx.y * kReduceRows, r1 = min(rows, r0 + kReduceRows);
+    uint64_t lo = 0, hi = 0;
+#pragma unroll 8
+    for (uint32_t r = r0; r < r1; r++) {
+        const uint32_t x = scratch[(size_t)r * words + w];
+        lo += x & 0xFFFFu;
+        hi += x >> 16;
+    }
+    if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2 * w), (unsigned long long)lo);
+    if (hi && 2 * w + 1 < nflows) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2 * w + 1), (unsigned long long)hi);
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
@@ -497,11 +571,25 @@ __global__ __launch_bounds__(kBlock) void dk_tx_checksum_kernel(uint8_t* frames,
 }  // namespace
 }  // namespace dk
 
-int dk_launch_rx(const dk::RxParams& p, void* stream) {
-    if (p.n == 0) return 0;
-    const uint32_t grid = (p.n + dk::kBlock - 1) / dk::kBlock;
-    hipLaunchKernelGGL(dk::dk_rx_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, p);
-    return hipGetLastError() == hipSuccess ? 0 : 5;
+int dk_rx_resident_blocks(uint32_t dyn_lds_bytes) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_kernel, dk::kBlock, dyn_lds_bytes) != hipSuccess)
+        return 0;
+    return blocks;
+}
+
+int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
+    if (p.n == 0 || grid == 0) return 0;
+    const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
+    hipLaunchKernelGGL(dk::dk_rx_kernel, dim3(grid), dim3(dk::kBlock), dyn, (hipStream_t)stream, p);
+    if (hipGetLastError() != hipSuccess) return 5;
+    if (p.flow_mode == dk::kFlowLds) {
+        const dim3 g2((p.flow_words + dk::kBlock - 1) / dk::kBlock, (grid + dk::kReduceRows - 1) / dk::kReduceRows);
+        hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, (hipStream_t)stream,
+                           p.flow_scratch, grid, p.flow_words, p.nflows, p.res.flow_counts);
+        if (hipGetLastError() != hipSuccess) return 5;
+    }
+    return 0;
 }
 
 int dk_launch_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Kernel-level timing for tuning: dk_rx kernel on a workload vs the on-box streaming-read probe over the same blob.
+
+    python tools/kbench.py [--workload c2_tcp1500] [--iters 50] [--probe]
+Prints one JSON line per measurement. Also the command profiled by rocprofv3 (profiles/README.md).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def time_events(fn, iters, warm=3):
+    import torch
+
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c2_tcp1500")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--no-rx", action="store_true")
+    ap.add_argument("--no-counts", action="store_true", help="pass NULL flow/verdict counters (cost attribution)")
+    args = ap.parse_args()
+
+    import torch
+
+    import bench
+    from demikernel_amd import Config, RxEngine, synth
+    from demikernel_amd import _native as N
+
+    eng = RxEngine(Config(synth.BOB_IPV4))
+    batch, flows, tr = bench.make_batch(eng, args.workload, 0, synth.SEED)
+    res = eng.results(batch.n, counts=not args.no_counts)
+    fb = int(tr.frame_len.astype(np.int64).sum())
+    if not args.no_rx:
+        t = time_events(lambda: eng.receive_batch(batch, res), args.iters)
+        algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES)
+        print(json.dumps({"kernel": "dk_rx", "workload": args.workload, "counts": not args.no_counts,
+                          "ms": round(t * 1e3, 4),
+                          "frame_GBps": round(fb / t / 1e9, 1), "algo_GBps": round(algo / t / 1e9, 1),
+                          "mpkt_s": round(batch.n / t / 1e6, 1)}), flush=True)
+    if args.probe:
+        lib = N.load_library()
+        nbytes = batch.blob.numel() // 16 * 16
+        for mode in (0, 1, 2):
+            for grid in (1024, 2048, 4096, 8192, 16384):
+                scratch = torch.zeros(grid, dtype=torch.int32, device="cuda")
+                s = torch.cuda.current_stream().cuda_stream
+
+                def run():
+                    lib.dk_diag_read_probe(ctypes.c_void_p(batch.blob.data_ptr()), nbytes,
+                                           ctypes.c_void_p(scratch.data_ptr()), grid, mode, ctypes.c_void_p(s))
+
+                t = time_events(run, args.iters)
+                print(json.dumps({"kernel": "read_probe", "mode": mode, "grid": grid, "bytes": nbytes,
+                                  "ms": round(t * 1e3, 4), "GBps": round(nbytes / t / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
