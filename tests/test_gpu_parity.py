@@ -6,6 +6,7 @@ import pytest
 
 import frames as F
 from demikernel_amd import Config, FrameBatch, RxEngine, V, VERDICTS, ipv4, synth
+from demikernel_amd._native import FLOW_DTYPE
 from oracle.oracle import OraclePeer
 
 pytestmark = pytest.mark.gpu
@@ -239,3 +240,18 @@ def test_full_size_c2_properties(torch_cuda):
     exp = run_oracle(blob, off[sample], lens[sample], flows)
     for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id"):
         assert np.array_equal(got[k][sample], exp[k]), k
+
+
+@pytest.mark.parametrize("name", ["verdict_corpus", "mixed_batch"])
+def test_golden_fixtures(torch_cuda, name):
+    """The committed fixtures (tests/golden, made by make_golden.py) reproduce bit for bit on the GPU."""
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"), allow_pickle=False)
+    flows = g["flows"].view(FLOW_DTYPE)
+    got = run_gpu(g["blob"], g["off"].astype(np.uint32), g["len"].astype(np.uint16), flows)
+    for k, v in got.items():
+        e = g["res_" + k][: len(v)]
+        assert np.array_equal(v, e), k
+    if name == "verdict_corpus":
+        assert np.array_equal(got["meta"] & 0xFF, g["expected_verdict"])
