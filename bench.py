@@ -39,14 +39,22 @@ def dist_env():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")), ws
 
 
-def make_batch(eng, name, rank, seed_base):
+def make_batch(eng, name, rank, seed_base, world=1):
+    """This rank's packet shard of the global batch (world x frames-per-GPU frames, weak scaling): the frame-size
+    sequence is global and seeded, the shard boundaries are byte-balanced (demikernel_amd.shard), and each rank
+    synthesises only its own frames on its own GPU."""
     from demikernel_amd import synth
+    from demikernel_amd.shard import byte_balanced_shards
 
     _, n, ip_len, kind, nflows = WORKLOADS[name]
     flows = synth.make_flows(nflows, kind=kind)
+    total = n * world
+    ip_all = synth.imix_ip_lengths(total, seed_base) if ip_len == "imix" else np.full(total, ip_len, np.uint16)
+    frame_all = np.maximum(ip_all.astype(np.int64) + 14, synth.ETH_MIN_FRAME)
+    a, b = byte_balanced_shards(frame_all, world)[rank]
     seed = seed_base + 7919 * rank
-    lens = synth.imix_ip_lengths(n, seed) if ip_len == "imix" else ip_len
-    tr = synth.traffic(n, lens, flows, seed=seed)
+    n = b - a
+    tr = synth.traffic(n, ip_all[a:b], flows, seed=seed)
     eng.set_sockets(flows)
     batch = synth.build_device(tr, eng, seed=seed)
     synth.corrupt_device(batch, batch.off.cpu().numpy().view(np.uint32), synth.corruption_plan(n, 0.01, tr, seed))
@@ -54,36 +62,48 @@ def make_batch(eng, name, rank, seed_base):
 
 
 def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allreduce=False):
-    """Run warmup + timed steps; returns (wall seconds for `steps`, list of per-launch kernel seconds)."""
+    """Run warmup + timed steps. A step = the receive pass over one batch (+ for N > 1 the all-reduce of this step's
+    per-flow counts). Returns (wall seconds for `steps`, per-launch kernel seconds, per-step collective seconds)."""
     import torch
 
-    def step(k):
+    def step(k, ev=None):
         b = batches[k % len(batches)]
+        if counts_allreduce:
+            res.t["flow_counts"].zero_()
+        if ev:
+            ev[0].record(stream)
         eng.receive_batch(b, res, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        if counts_allreduce:
+            fc = res.t["flow_counts"]
+            if dist.get_backend() == "gloo":  # rehearsal only: gloo reduces a host copy
+                h = fc.cpu()
+                dist.all_reduce(h)
+                fc.copy_(h)
+            else:
+                dist.all_reduce(fc)
+            if ev:
+                ev[2].record(stream)
 
     for k in range(warmup):
         step(k)
-        if counts_allreduce:
-            dist.all_reduce(res.t["flow_counts"])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(steps)]
     t0 = time.perf_counter()
     for k in range(steps):
-        ev[k][0].record(stream)
-        step(k)
-        ev[k][1].record(stream)
-        if counts_allreduce:
-            dist.all_reduce(res.t["flow_counts"])
+        step(k, ev[k])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern = [a.elapsed_time(b) / 1e3 for a, b in ev]
-    return wall, kern
+    kern = [a.elapsed_time(b) / 1e3 for a, b, _ in ev]
+    coll = [b.elapsed_time(c) / 1e3 for _, b, c in ev] if counts_allreduce else []
+    return wall, kern, coll
 
 
 def cpu_baseline(batch, flows, sample_frames, min_seconds, threads=1):
@@ -132,6 +152,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 17)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL on ROCm; gloo only to rehearse on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -141,8 +163,12 @@ def main():
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        local_dev = local_rank % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local_dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -152,19 +178,21 @@ def main():
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
     stream = torch.cuda.current_stream(dev)
     name = args.workload
-    batch, flows, tr = make_batch(eng, name, rank, synth.SEED)
+    batch, flows, tr = make_batch(eng, name, rank, synth.SEED, world)
     batches = [batch]
     if name == "c3_udp64":  # 64 B batches fit in the 256 MB MALL: rotate 8 distinct batches (> 512 MB)
-        batches += [make_batch(eng, name, rank + 1000 * k, synth.SEED)[0] for k in range(1, 8)]
+        batches += [make_batch(eng, name, rank, synth.SEED + 1000 * k, world)[0] for k in range(1, 8)]
     res = eng.results(batch.n)
     frame_bytes = int(tr.frame_len.astype(np.int64).sum())
 
-    wall, kern = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist, counts_allreduce=world > 1)
+    wall, kern, coll = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist,
+                                   counts_allreduce=world > 1)
     if dist is not None:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        cdev = "cuda" if args.backend == "nccl" else "cpu"
+        t = torch.tensor([wall], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-        tb = torch.tensor([frame_bytes, batch.n], dtype=torch.int64, device="cuda")
+        tb = torch.tensor([frame_bytes, batch.n], dtype=torch.int64, device=cdev)
         dist.all_reduce(tb)
         total_bytes, total_frames = int(tb[0]), int(tb[1])
     else:
@@ -198,6 +226,8 @@ def main():
                      "kernel_ms_avg": round(kern_avg * 1e3, 4),
                      "algorithmic_bytes_per_launch": algo},
     }
+    if coll:
+        out["collective_ms_avg"] = round(float(np.mean(coll)) * 1e3, 4)
     if rank == 0 and world == 1 and not args.no_cpu:
         gbs, used, n_s, nb_s, reps = cpu_baseline(batch, flows, args.cpu_sample, args.cpu_seconds)
         out["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s", "cores": used, "kind": "port",
@@ -206,9 +236,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras and name == "c2_tcp1500":
         # secondary: 64 B UDP Mpkt/s (config 3) on rotating batches
         eng3 = RxEngine(Config(synth.BOB_IPV4), device=dev)
-        b3 = [make_batch(eng3, "c3_udp64", 1000 * k, synth.SEED)[0] for k in range(8)]
+        b3 = [make_batch(eng3, "c3_udp64", 0, synth.SEED + 1000 * k)[0] for k in range(8)]
         r3 = eng3.results(b3[0].n)
-        w3, k3 = time_kernel(eng3, b3, r3, 40, 4, stream)
+        w3, k3, _ = time_kernel(eng3, b3, r3, 40, 4, stream)
         n3 = b3[0].n
         out["c3_udp64"] = {"gbps": round(n3 * 64 * 40 / w3 / 1e9, 2), "mpkt_s": round(n3 * 40 / w3 / 1e6, 1),
                            "kernel_ms_avg": round(float(np.mean(k3)) * 1e3, 4)}

@@ -131,6 +131,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
     uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, bytes_per_frame >= 1024 ? 2u : 4u);
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
+    if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
     if (p.flow_mode == dk::kFlowLds) {
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
         int rc = ensure_scratch(fs, (size_t)grid * p.flow_words);

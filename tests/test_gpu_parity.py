@@ -255,3 +255,22 @@ def test_golden_fixtures(torch_cuda, name):
         assert np.array_equal(v, e), k
     if name == "verdict_corpus":
         assert np.array_equal(got["meta"] & 0xFF, g["expected_verdict"])
+
+
+def test_flow_counter_modes_and_wrap_guard(torch_cuda, monkeypatch):
+    """Per-flow counts on both counter paths (LDS histogram up to 32768 flows, global atomics above) and the packed-u16
+    wrap guard: one workgroup asked to count 100k frames of one flow must still count exactly."""
+    for nflows in (32767, 32768, 32769):
+        flows = synth.make_flows(nflows, passive=False)
+        n = 30000
+        tr = synth.traffic(n, 100, flows, seed=nflows)
+        blob, off, lens = synth.build_numpy(tr)
+        got = check(blob, off, lens, flows, ctx=f"nflows={nflows}")
+        assert got["flow_counts"].sum() == n
+    flows = synth.make_flows(1, passive=False)
+    n = 100_000
+    tr = synth.traffic(n, 40, flows, seed=1)
+    blob, off, lens = synth.build_numpy(tr)
+    monkeypatch.setenv("DK_RX_GRID", "1")
+    got = run_gpu(blob, off, lens, flows)
+    assert int(got["flow_counts"][0]) == n and int(got["verdict_counts"][0]) == n

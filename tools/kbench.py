@@ -50,7 +50,7 @@ def main():
     from demikernel_amd import _native as N
 
     eng = RxEngine(Config(synth.BOB_IPV4))
-    batch, flows, tr = bench.make_batch(eng, args.workload, 0, synth.SEED)
+    batch, flows, tr = bench.make_batch(eng, args.workload, 0, synth.SEED, 1)
     res = eng.results(batch.n, counts=not args.no_counts)
     fb = int(tr.frame_len.astype(np.int64).sum())
     if not args.no_rx:
