@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--workload", default="c2_tcp1500")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--probe-one", action="store_true", help="one probe config (mode 1, grid 1024): PMC calibration")
     ap.add_argument("--no-rx", action="store_true")
     ap.add_argument("--no-counts", action="store_true", help="pass NULL flow/verdict counters (cost attribution)")
     args = ap.parse_args()
@@ -57,14 +58,15 @@ def main():
         t = time_events(lambda: eng.receive_batch(batch, res), args.iters)
         algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES)
         print(json.dumps({"kernel": "dk_rx", "workload": args.workload, "counts": not args.no_counts,
+                          "frames": batch.n, "frame_bytes": fb, "algo_bytes": algo, "blob_bytes": batch.blob.numel(),
                           "ms": round(t * 1e3, 4),
                           "frame_GBps": round(fb / t / 1e9, 1), "algo_GBps": round(algo / t / 1e9, 1),
                           "mpkt_s": round(batch.n / t / 1e6, 1)}), flush=True)
-    if args.probe:
+    if args.probe or args.probe_one:
         lib = N.load_library()
         nbytes = batch.blob.numel() // 16 * 16
-        for mode in (0, 1, 2):
-            for grid in (1024, 2048, 4096, 8192, 16384):
+        for mode in ((1,) if args.probe_one else (0, 1, 2)):
+            for grid in ((1024,) if args.probe_one else (1024, 2048, 4096, 8192, 16384)):
                 scratch = torch.zeros(grid, dtype=torch.int32, device="cuda")
                 s = torch.cuda.current_stream().cuda_stream
 

@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 evidence for one round (run on the GPU box from the repo root):
+#   1. kernel trace + stats of the bench command itself (profiles/<tag>_bench_kernel_stats.csv)
+#   2. FETCH_SIZE and WRITE_SIZE in separate --pmc passes over kbench (dk_rx_kernel + the read probe, whose byte count
+#      is known: it calibrates the FETCH_SIZE unit for this access pattern on gfx950)
+# then tools/summarize_profile.py <tag> writes profiles/<tag>_summary.md and profiles/pmc_traffic.json.
+set -o pipefail
+TAG=${1:-r01}
+R=$(pwd)
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d $OUT/bench -o run --output-format csv -- \
+  python3 $R/bench.py --steps 50 --warmup 5 --cpu-seconds 2 --no-extras > $OUT/bench.json 2> $OUT/bench.err || exit 11
+for WL in c2_tcp1500 c3_udp64 c4_imix c5_tcp1500_10k; do
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "dk_rx_kernel|read_probe" -T -d $OUT/fetch_$WL -o run --output-format csv -- \
+    python3 $R/tools/kbench.py --workload $WL --iters 5 --probe-one > $OUT/fetch_$WL.log 2>&1 || exit 12
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "dk_rx_kernel|read_probe" -T -d $OUT/write_$WL -o run --output-format csv -- \
+    python3 $R/tools/kbench.py --workload $WL --iters 5 --probe-one > $OUT/write_$WL.log 2>&1 || exit 13
+done
+cd $R && python3 tools/summarize_profile.py $TAG

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 outputs of tools/profile_bench.sh into profiles/ (committed evidence).
+
+    python tools/summarize_profile.py <tag>
+Writes profiles/<tag>_bench_kernel_stats.csv (verbatim kernel stats of the bench command), profiles/<tag>_pmc.csv
+(per-kernel FETCH_SIZE / WRITE_SIZE averages) and profiles/pmc_traffic.json (per-launch HBM bytes bench.py reports as
+roofline.traffic).
+
+FETCH_SIZE unit on gfx950: the guide's rule (MI355X_MICROARCH.md §HBM) is that FETCH_SIZE reads 1/2 of the bytes of a
+wide coalesced streaming read; we calibrate instead of assuming, with the read probe that runs in the same --pmc pass
+over the same blob: factor = probe bytes / (probe FETCH_SIZE * 1024), applied to dk_rx_kernel's FETCH_SIZE.
+WRITE_SIZE is reported as counted (exact for 16-B streaming stores per the guide; our 4-B-per-lane SoA stores are
+uncalibrated).
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path):
+    agg = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def kbench_info(path):
+    rx, probe = None, None
+    for line in open(path):
+        line = line.strip()
+        if not line.startswith("{"):
+            continue
+        d = json.loads(line)
+        if d.get("kernel") == "dk_rx":
+            rx = d
+        elif d.get("kernel") == "read_probe":
+            probe = d
+    return rx, probe
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "bench", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "bench.json")):
+        shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench_under_rocprof.json"))
+    traffic = {}
+    rows = [["workload", "kernel", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "calib_factor", "hbm_read_bytes",
+             "hbm_write_bytes", "algo_bytes", "traffic_over_algo"]]
+    for wl in ("c2_tcp1500", "c3_udp64", "c4_imix", "c5_tcp1500_10k"):
+        fdir, wdir = os.path.join(src, f"fetch_{wl}"), os.path.join(src, f"write_{wl}")
+        if not os.path.exists(os.path.join(fdir, "run_counter_collection.csv")):
+            continue
+        fc = counters(os.path.join(fdir, "run_counter_collection.csv"))
+        wc = counters(os.path.join(wdir, "run_counter_collection.csv"))
+        rx, probe = kbench_info(os.path.join(src, f"fetch_{wl}.log"))
+        fk = {k[0]: v for k, v in fc.items() if k[1] == "FETCH_SIZE"}
+        wk = {k[0]: v for k, v in wc.items() if k[1] == "WRITE_SIZE"}
+        rxk = next(k for k in fk if "dk_rx_kernel" in k)
+        pk = next(k for k in fk if "read_probe" in k)
+        factor = probe["bytes"] / (fk[pk] * 1024.0)
+        rd = fk[rxk] * 1024.0 * factor
+        wr = wk.get(rxk, 0.0) * 1024.0
+        algo = rx["algo_bytes"]
+        traffic[wl] = {"hbm_bytes_per_launch": int(rd + wr), "hbm_read_bytes": int(rd), "hbm_write_bytes": int(wr),
+                       "fetch_size_kb_raw": fk[rxk], "write_size_kb_raw": wk.get(rxk, 0.0),
+                       "fetch_calibration_factor": round(factor, 4), "algorithmic_bytes_per_launch": algo,
+                       "source": f"profiles/{tag}_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
+        rows.append([wl, "dk_rx_kernel", f"{fk[rxk]:.0f}", f"{wk.get(rxk, 0.0):.0f}", f"{factor:.4f}", f"{rd:.0f}",
+                     f"{wr:.0f}", algo, f"{(rd + wr) / algo:.3f}"])
+        rows.append([wl, "read_probe", f"{fk[pk]:.0f}", f"{wk.get(pk, 0.0):.0f}", "", probe["bytes"], "", "", ""])
+    with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as f:
+        csv.writer(f).writerows(rows)
+    json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
