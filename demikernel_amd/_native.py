@@ -76,6 +76,8 @@ FUNCTIONS = [
 # include/dk_diag.h (diagnostics, not the receive ABI)
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
+    ("dk_diag_path_stats_enable", c_int, [c_void_p, c_int]),
+    ("dk_diag_path_stats_read", c_int, [c_void_p, c_void_p]),
 ]
 
 _lib = None
@@ -97,7 +99,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         pass
     lib = ctypes.CDLL(path)
     for name, restype, argtypes in FUNCTIONS + DIAG_FUNCTIONS:
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if (name, restype, argtypes) in DIAG_FUNCTIONS and path != LIB_PATH:
+                continue  # older tuning builds may predate a diagnostic
+            raise ImportError(f"{path}: missing {name}")
         fn.restype = restype
         fn.argtypes = argtypes
     if path == LIB_PATH:

@@ -61,15 +61,62 @@ __global__ __launch_bounds__(kBlock) void read_probe(const uint4* __restrict__ p
     if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
 }
 
+// mode 3: register loads, 16 x 1 KiB per wave step in flight.
+// mode 4 / 5: LDS-DMA (global_load_lds_dwordx4), nontemporal / default policy, 16 x 1 KiB per wave step into a
+// per-wave 16 KiB LDS slot, read back with ds_read_b128 and summed.
+typedef __attribute__((address_space(3))) void lds_void;
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void read_probe16(const uint4* __restrict__ p, uint64_t n16, uint32_t* out) {
+    __shared__ uint4 slot[kBlock / 64][16][64];
+    constexpr int U = 16;
+    uint32_t acc = 0;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + wv;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t piece = 64 * U;
+    for (uint64_t base = w * piece; base < n16; base += nwaves * piece) {
+        if (kMode == 3) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = base + u * 64 + lane;
+                v[u] = i < n16 ? ld(p + i, true) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = min(base + u * 64 + lane, n16 - 1);
+                __builtin_amdgcn_global_load_lds((const void*)(p + i), (lds_void*)&slot[wv][u][0], 16, 0,
+                                                 kMode == 4 ? 2 : 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint4 v = slot[wv][u][lane];
+                acc ^= v.x + v.y + v.z + v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+    acc = __reduce_add_sync(~0ull, acc);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
+}
+
 }  // namespace
 
 extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode,
                                   void* stream) {
-    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 2) return 22;
+    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 5) return 22;
     const uint4* p = (const uint4*)buf;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == 0) hipLaunchKernelGGL(read_probe<0>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 1) hipLaunchKernelGGL(read_probe<1>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 2) hipLaunchKernelGGL(read_probe<2>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 3) hipLaunchKernelGGL(read_probe16<3>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 4) hipLaunchKernelGGL(read_probe16<4>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 5) hipLaunchKernelGGL(read_probe16<5>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

@@ -3,6 +3,7 @@
 
 #include <stdint.h>
 
+#include "../../include/dk_diag.h"
 #include "../../include/dk_rx.h"
 
 #if defined(__HIPCC__)
@@ -61,6 +62,7 @@ struct RxParams {
     uint32_t flow_mode;      // kFlow*
     uint32_t flow_words;     // kFlowLds: ceil(nflows / 2)
     uint32_t* flow_scratch;  // kFlowLds: [grid][flow_words]
+    unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
     dk_rx_results res;
 };
 

@@ -53,6 +53,7 @@ struct dk_rx_ctx {
     uint32_t cu_count = 0;
     uint32_t occ_dyn = ~0u;   // occupancy cache: dynamic LDS bytes -> resident blocks per CU
     uint32_t occ_blocks = 0;
+    unsigned long long* d_path_stats = nullptr;  // dk_diag path counters (nullptr = off)
 };
 
 namespace {
@@ -124,11 +125,9 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn), 1);
         c->occ_dyn = dyn;
     }
-    // Resident workgroups per CU (measured, DESIGN.md "Tuning log"): large frames stream best with 2 (fewer
-    // concurrent frame streams per CU), small frames are issue-bound and want 4. The host only knows the blob size
-    // per frame, which is what the choice keys on.
-    const uint64_t bytes_per_frame = p.frames_bytes / p.n;
-    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, bytes_per_frame >= 1024 ? 2u : 4u);
+    // Resident workgroups per CU: 4 (16 waves/CU) measured best for every workload once phase B streams whole frames
+    // (DESIGN.md "Tuning log"); fewer when LDS (large socket tables) or registers do not admit 4.
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, 4u);
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
     if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
@@ -177,6 +176,7 @@ int ensure_stage(Stage& s, uint32_t cap, uint64_t bytes) {
 
 dk::RxParams base_params(const dk_rx_ctx* c) {
     dk::RxParams p{};
+    p.path_stats = c->d_path_stats;
     p.local_ip = c->cfg.local_ipv4;
     p.tcp_offload = c->cfg.tcp_rx_checksum_offload ? 1u : 0u;
     p.udp_offload = c->cfg.udp_rx_checksum_offload ? 1u : 0u;
@@ -229,6 +229,7 @@ void dk_rx_ctx_destroy(dk_rx_ctx* c) {
     if (c->d_flow_counts) (void)hipFree(c->d_flow_counts);
     if (c->d_verdict_counts) (void)hipFree(c->d_verdict_counts);
     free_scratch(c->scratch);
+    if (c->d_path_stats) (void)hipFree(c->d_path_stats);
     delete c;
 }
 
@@ -400,6 +401,25 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         for (int k = 0; k < DK_V_COUNT; k++) r->verdict_counts[k] += tmp[k];
     }
     return 0;
+}
+
+int dk_diag_path_stats_enable(dk_rx_ctx* c, int on) {
+    if (!c) return EINVAL;
+    DeviceGuard g(c->cfg.device);
+    if (!on) {
+        if (c->d_path_stats) (void)hipFree(c->d_path_stats);
+        c->d_path_stats = nullptr;
+        return 0;
+    }
+    if (!c->d_path_stats && hipMalloc(&c->d_path_stats, 4 * sizeof(unsigned long long)) != hipSuccess) return ENOMEM;
+    return hipMemset(c->d_path_stats, 0, 4 * sizeof(unsigned long long)) == hipSuccess ? 0 : EIO;
+}
+
+int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
+    if (!c || !out || !c->d_path_stats) return EINVAL;
+    DeviceGuard g(c->cfg.device);
+    if (hipDeviceSynchronize() != hipSuccess) return EIO;
+    return hipMemcpy(out, c->d_path_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : EIO;
 }
 
 int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,

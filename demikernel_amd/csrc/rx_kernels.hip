@@ -8,17 +8,17 @@
 //   UdpHeader::parse_and_strip        (layer4/udp/header.rs:57-94, checksum :140-193)
 //   TcpPeer::receive / UdpPeer::receive demux (layer4/tcp/peer.rs:220-255, layer4/udp/peer.rs:129-168)
 //
-// Work decomposition (one 256-thread workgroup = 4 waves = 256 consecutive frames):
-//   Phase A, lane per frame: load descriptor + the first 64 frame bytes (4 x dwordx4), parse every header field from
-//     registers, run every check that precedes the L4 checksum (Appendix A order), verify the IPv4 header checksum,
-//     sum the L4 bytes that sit in the 64-byte header window, and prefetch the partial tail block.
-//   Phase B, quarter-wave per frame: the full 16-byte blocks of the L4 region past byte 64 are summed by 16 lanes
-//     (6 x dwordx4 in flight per lane, 1.5 KB per quarter per round; 4 frames per wave per round), reduced with
-//     4 lane shuffles and handed to the owning lane through LDS.
-//   Phase C, lane per frame: close the one's-complement sum (pseudo-header, stored field removed), T4/U3 verdicts,
-//     TCP option walk (T5, byte loads: only option-bearing segments), hash-table demux, SoA result stores, counters.
-// Frames whose start is not 16-byte aligned, or whose IPv4 IHL != 5, take a per-lane byte-load path that implements
-// the same checks (phase A "slow"); they skip phase B.
+// Work decomposition (persistent grid; one 256-thread workgroup = 4 waves processes 256-frame tiles):
+//   Phase A, lane per frame: descriptor; frames of <= 64 bytes load straight into registers (4 x dwordx4).
+//   Phase B, quarter-wave per frame: every frame of > 64 bytes is streamed once, whole, by 16 lanes (6 x dwordx4 in
+//     flight per lane, 1.5 KB per quarter per round, 4 frames per wave per round); its blocks are summed, its header
+//     window and last 32 bytes are deposited in LDS for the owning lane, and the quarter's sum is reduced with 4
+//     lane shuffles.
+//   Phase C, lane per frame: parse every header field from registers in Appendix A order (IPv4 header checksum
+//     included), close the L4 one's-complement sum (pseudo-header, stored field removed), T4/U3 verdicts, TCP option
+//     walk (T5, byte loads: only option-bearing segments), hash-table demux, SoA result stores, counters.
+// Frames whose start is not 16-byte aligned, or whose IPv4 IHL != 5, are parsed and summed by a per-lane byte-load
+// path that implements the same checks.
 //
 // Checksum arithmetic: the reference sums big-endian 16-bit words into a u32 seeded with
 // 0xFFFF and folds by repeated subtraction of 0xFFFF. We sum little-endian 16-bit halves of dwords with
@@ -44,6 +44,9 @@ constexpr uint32_t kPendUdp = 0xF1u;   // UDP header parsed; awaiting U3/demux
 #endif
 #ifndef DK_MIN_WAVES
 #define DK_MIN_WAVES 1
+#endif
+#ifndef DK_DESC_PREFETCH
+#define DK_DESC_PREFETCH 1  // load the next tile's descriptors before processing the current one
 #endif
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
@@ -269,96 +272,78 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 
 // One frame per lane, 256 frames per workgroup tile: phases A, B, C and the result stores. Every lane of the
 // workgroup calls it (phase B is wave-cooperative). Returns the verdict and the flow id (DK_FLOW_NONE if none).
-__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t lane, uint32_t (*s_list)[64],
-                                        uint32_t (*s_csum)[64], uint32_t wv, uint32_t& v_out, uint32_t& fid_out) {
+// Per-wave LDS used by one tile. Strides of 5 and 3 uint4 keep the owner-lane ds_read_b128 conflict-free.
+struct WaveLds {
+    uint4 rec[64];         // phase B: per rank {owner lane, frame offset, blocks, 0}
+    uint32_t csum[64];     // phase B: whole-frame LE-half sums by owner lane
+    uint4 hdr[64][5];      // phase B -> C: bytes [0, 64) of each big frame
+    uint4 tail[64][3];     // phase B -> C: the last two 16-byte blocks of each big frame
+};
+
+
+// One frame per lane, 256 frames per workgroup tile. Every lane of the workgroup calls it (phase B is
+// wave-cooperative). Returns the verdict and the flow id (DK_FLOW_NONE if none).
+//   Phase A (lane): descriptor; frames of <= 64 bytes load their bytes straight into registers.
+//   Phase B (quarter-wave per frame, 4 frames per wave per round): frames of > 64 bytes are streamed whole, once, by
+//     16 lanes (kCoopU x dwordx4 in flight each): blocks summed with v_dot2_u32_u16, the header window and the last
+//     32 bytes deposited in LDS for the owner lane, the quarter's sum reduced by 4 shuffles. Reading each frame in one
+//     contiguous pass keeps DRAM rows open (a separate 64-byte header read per frame cost 8 %).
+//   Phase C (lane): parse from registers, checksum = sum(all blocks) - sum[0, S) - sum[E, 16 * nblk) (exact integer
+//     arithmetic), T4/U3, options, demux, results.
+__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t lane, WaveLds& W, uint32_t off,
+                                        uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
     const bool live = i < P.n;
 
-    // ---------------- Phase A: descriptor, header window, parse ----------------
-    uint32_t off = 0, len = 0;
-    if (live) {
-        off = P.off[i];
-        len = P.len[i];
-    }
+    // ---------------- Phase A: descriptor (loaded by the caller); small frames into registers ----------------
     const bool inb = live && (uint64_t)off + len <= P.frames_bytes;
     const uint8_t* f = P.frames + off;
-    const bool aligned = (reinterpret_cast<uintptr_t>(f) & 15) == 0;
+    const bool vec = inb && (reinterpret_cast<uintptr_t>(f) & 15) == 0;  // vector path
+    const bool big = vec && len > 64;                                  // streamed by a quarter-wave
+    const uint32_t nblk = big ? (len + 15) >> 4 : 0;                     // 16-byte blocks covering the frame
 
     RegAcc R;
     {
         const uint4* fp = reinterpret_cast<const uint4*>(f);
-        const bool al = inb && aligned;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             uint4 q = make_uint4(0, 0, 0, 0);
-            if (al && (uint32_t)(16 * k) < len) q = fp[k];
+            if (vec && !big && (uint32_t)(16 * k) < len) q = fp[k];
             R.w[4 * k + 0] = q.x;
             R.w[4 * k + 1] = q.y;
             R.w[4 * k + 2] = q.z;
             R.w[4 * k + 3] = q.w;
         }
     }
-    // Fast path: aligned, whole Ethernet + IPv4 fixed header present, IHL == 5.
-    const bool fast = inb && aligned && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u;
 
-    Lane L;
-    L.v = kNone; L.src = L.dst = L.ports = L.b1213 = L.seq = L.ack = L.winurg = 0;
-    L.S = L.E = L.hlen = L.stored = L.need = L.lsum = 0;
-    uint4 tail = make_uint4(0, 0, 0, 0);
-    uint32_t nblk = 0;  // phase-B blocks of this frame
-
-    if (!live) {
-        L.v = kNone;
-    } else if (!inb) {
-        L.v = DK_V_BAD_DESC;
-    } else if (fast) {
-        parse_headers<true>(R, len, P, L);
-        if (L.need) {
-            const int E = (int)L.E;
-            // bytes [34, min(E, 64)) from the header window: block 2 (bytes 32..47) and block 3 (48..63)
-            uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
-            s = block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
-            L.lsum = s;
-            if (E > 64) {
-                const uint32_t fe = L.E & ~15u;
-                nblk = (fe - 64) >> 4;
-                if (L.E & 15u) tail = *reinterpret_cast<const uint4*>(f + fe);  // prefetch; summed in phase C
-            }
-        }
-    } else {
-        const MemAcc M{f};
-        parse_headers<false>(M, len, P, L);
-        if (L.need) L.lsum = M.sum_le16(L.S, L.E);
-    }
-
-    // ---------------- Phase B: quarter-wave sums of the full 16-byte blocks in [64, E & ~15) ----------------
+    // ---------------- Phase B: whole-frame quarter-wave streams ----------------
+    uint32_t fsum = 0;  // big frames: LE-half sum over blocks [0, nblk)
     {
-        const uint64_t cm = __ballot(nblk != 0);
+        const uint64_t cm = __ballot(big);
         const uint32_t ncoop = (uint32_t)__popcll(cm);
         if (ncoop) {
-            if (nblk) {
+            if (big) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-                s_list[wv][rank] = lane;
+                W.rec[rank] = make_uint4(lane, off, nblk, 0);  // per-rank frame record: one ds_read_b128 per round
+            }
+            // Wave-uniform iterations per round (1 unless a frame exceeds kCoopSpan blocks, i.e. > 1536 bytes).
+            uint32_t maxit = 1;
+            if (__ballot(nblk > kCoopSpan)) {
+                uint32_t mx = nblk;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+                maxit = __builtin_amdgcn_readfirstlane((mx + kCoopSpan - 1) / kCoopSpan);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t q = lane >> 4, l16 = lane & 15;
-            const uint32_t cbase = off + 64;
             for (uint32_t r = 0; r * 4 < ncoop; r++) {
                 const uint32_t k = r * 4 + q;
                 const bool has = k < ncoop;
-                const uint32_t j = has ? s_list[wv][k] : 0u;
-                // Both shuffles run with every lane active: ds_bpermute reads 0 from a source lane that is
-                // exec-masked off, and the owner lane j may sit in a quarter with no frame this round.
-                const uint32_t fb = __shfl(cbase, (int)j);
-                const uint32_t nb_j = __shfl(nblk, (int)j);
-                const uint32_t nb = has ? nb_j : 0u;
-                uint32_t nit = (nb + kCoopSpan - 1) / kCoopSpan;
-                nit = max(nit, (uint32_t)__shfl_xor(nit, 16));
-                nit = max(nit, (uint32_t)__shfl_xor(nit, 32));
-                const uint32_t maxit = __builtin_amdgcn_readfirstlane(nit);
-                const uint4* base = reinterpret_cast<const uint4*>(P.frames + fb);
+                const uint4 rec = has ? W.rec[k] : make_uint4(0, 0, 0, 0);
+                const uint32_t j = rec.x, nb = rec.z;
+                const uint4* base = reinterpret_cast<const uint4*>(P.frames + rec.y);
                 uint32_t acc = 0;
                 for (uint32_t it = 0; it < maxit; it++) {
                     const uint32_t b0 = it * kCoopSpan + l16;
@@ -369,29 +354,83 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t 
                         d[u] = b < nb ? ld_stream(base + b) : make_uint4(0, 0, 0, 0);
                     }
 #pragma unroll
-                    for (uint32_t u = 0; u < kCoopU; u++) acc = block_sum(d[u], acc);
+                    for (uint32_t u = 0; u < kCoopU; u++) {
+                        const uint32_t b = b0 + 16 * u;
+                        acc = block_sum(d[u], acc);
+                        if (has && b < 4) W.hdr[j][b] = d[u];                // big frame: 4 < nb
+                        if (b < nb && b + 2 >= nb) W.tail[j][b + 2 - nb] = d[u];
+                    }
                 }
-                acc += (uint32_t)__shfl_xor(acc, 1);
-                acc += (uint32_t)__shfl_xor(acc, 2);
-                acc += (uint32_t)__shfl_xor(acc, 4);
-                acc += (uint32_t)__shfl_xor(acc, 8);
-                if (has && l16 == 0) s_csum[wv][j] = acc;
+                // Quarter = DPP row of 16 lanes: inclusive row scan by row_shr 1/2/4/8; lane 15 holds the sum.
+                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xF, 0xF, false);
+                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x112, 0xF, 0xF, false);
+                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x114, 0xF, 0xF, false);
+                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x118, 0xF, 0xF, false);
+                if (has && l16 == 15) W.csum[j] = acc;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (nblk) L.lsum += s_csum[wv][lane];
+            if (big) {
+                fsum = W.csum[lane];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 h = W.hdr[lane][k];
+                    R.w[4 * k + 0] = h.x;
+                    R.w[4 * k + 1] = h.y;
+                    R.w[4 * k + 2] = h.z;
+                    R.w[4 * k + 3] = h.w;
+                }
+            }
         }
     }
 
-    // ---------------- Phase C: checksum verdicts, options, demux, results ----------------
+    // ---------------- Phase C: parse, checksum, options, demux, results ----------------
+    // Fast parse: 16-byte aligned, whole Ethernet + IPv4 fixed header present, IHL == 5 (S == 34).
+    const bool fast = vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u;
+    bool resum = false;  // path-stats: streamed frame whose segment is re-summed in-lane
+    Lane L;
+    L.v = kNone; L.src = L.dst = L.ports = L.b1213 = L.seq = L.ack = L.winurg = 0;
+    L.S = L.E = L.hlen = L.stored = L.need = L.lsum = 0;
+    if (!live) {
+        L.v = kNone;
+    } else if (!inb) {
+        L.v = DK_V_BAD_DESC;
+    } else if (fast) {
+        parse_headers<true>(R, len, P, L);
+        if (L.need) {
+            const int E = (int)L.E;
+            if (!big) {
+                // [34, E) inside the register window: block 2 (bytes 32..47) and block 3 (48..63)
+                uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
+                L.lsum = block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
+            } else if ((int)(16 * nblk) - E <= 32) {
+                // sum[S, E) = sum(all blocks) - sum[0, 34) - sum[E, 16 * nblk); the last two blocks are in LDS
+                uint32_t pre = block_sum(make_uint4(R.w[0], R.w[1], R.w[2], R.w[3]), 0);
+                pre = block_sum(make_uint4(R.w[4], R.w[5], R.w[6], R.w[7]), pre);
+                pre += R.w[8] & 0xFFFFu;
+                const int t0 = (int)(16 * nblk) - 32;
+                const uint4 a = W.tail[lane][0], c = W.tail[lane][1];
+                uint32_t post = block_sum_masked(a.x, a.y, a.z, a.w, E - t0, 16, 0);
+                post = block_sum_masked(c.x, c.y, c.z, c.w, E - t0 - 16, 16, post);
+                L.lsum = fsum - pre - post;
+            } else {
+                // IPv4 total_length far below the frame length: sum the segment directly (rare)
+                L.lsum = MemAcc{f}.sum_le16(L.S, L.E);
+                resum = true;
+            }
+        }
+    } else {
+        const MemAcc M{f};
+        parse_headers<false>(M, len, P, L);
+        if (L.need) L.lsum = M.sum_le16(L.S, L.E);
+    }
+
     uint32_t fid = DK_FLOW_NONE;
     if (L.v == kPendTcp || L.v == kPendUdp) {
         const bool tcp = L.v == kPendTcp;
         if (L.need) {
-            uint32_t s = L.lsum;
-            if (L.E > 64 && (L.E & 15u) && fast) s = block_sum_masked(tail.x, tail.y, tail.z, tail.w, 0, (int)(L.E & 15u), s);
-            s -= bswap16(L.stored);  // the stored field is in the summed region; the reference sums it as zero
+            const uint32_t s = L.lsum - bswap16(L.stored);  // the reference sums the stored field as zero
             const uint32_t seg = L.E - L.S;
             const uint32_t lip = P.local_ip;
             // pseudo-header: src, local (tcp/peer.rs:223-228, udp/peer.rs:134), protocol, segment length (BE words)
@@ -442,6 +481,14 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t 
         if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
         if (P.res.tcp_win) P.res.tcp_win[i] = win;
     }
+    if (P.path_stats) {  // diagnostics (dk_diag.h): one atomic per path per wave
+        const uint32_t path = !fast ? 3u : resum ? 2u : big ? 1u : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint64_t m = __ballot(live && inb && path == k);
+            if (m && lane == 0) atomicAdd(P.path_stats + k, (unsigned long long)__popcll(m));
+        }
+    }
     v_out = v;
     fid_out = fid;
 }
@@ -452,8 +499,7 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t 
 // wraps). At exit the histogram row is written with plain stores to flow_scratch[b][*] and dk_flow_reduce_kernel adds
 // the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
 __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P) {
-    __shared__ uint32_t s_list[kWaves][64];   // phase B: coop frame lanes, in rank order
-    __shared__ uint32_t s_csum[kWaves][64];   // phase B: coop sums by owner lane
+    __shared__ WaveLds s_wave[kWaves];        // per-wave phase B/C exchange
     __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
@@ -467,10 +513,35 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P)
     __syncthreads();
 
     const uint32_t ntiles = (P.n + kBlock - 1) / kBlock;
+    uint32_t noff = 0, nlen = 0;  // descriptors of this workgroup's next tile
+    {
+        const uint32_t i0 = blockIdx.x * kBlock + tid;
+        if (i0 < P.n) {
+            noff = P.off[i0];
+            nlen = P.len[i0];
+        }
+    }
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t i = t * kBlock + tid;
+        const uint32_t off = noff, len = nlen;
+#if DK_DESC_PREFETCH
+        const uint32_t i2 = i + gridDim.x * kBlock;
+        if (t + gridDim.x < ntiles && i2 < P.n) {
+            noff = P.off[i2];
+            nlen = P.len[i2];
+        }
+#endif
         uint32_t v, fid;
-        rx_tile(P, i, lane, s_list, s_csum, wv, v, fid);
+        rx_tile(P, i, lane, s_wave[wv], off, len, v, fid);
+#if !DK_DESC_PREFETCH
+        {
+            const uint32_t i2 = i + gridDim.x * kBlock;
+            if (t + gridDim.x < ntiles && i2 < P.n) {
+                noff = P.off[i2];
+                nlen = P.len[i2];
+            }
+        }
+#endif
         const bool live = i < P.n;
         if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
             if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));

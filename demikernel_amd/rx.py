@@ -150,8 +150,8 @@ class RxResults:
 class RxEngine:
     """Batch receive path on one GPU (the drop-in for layer2..layer4 receive + demux, see module docstring)."""
 
-    def __init__(self, config: Config, device: int = 0):
-        self.lib = N.load_library()
+    def __init__(self, config: Config, device: int = 0, lib_path: Optional[str] = None):
+        self.lib = N.load_library() if lib_path is None else N.load_library(lib_path)
         self.config = config
         self.device = device
         cfg = N.DkRxCfg(ipv4(config.local_ipv4_addr), int(config.tcp_checksum_offload),
@@ -199,6 +199,15 @@ class RxEngine:
         r = results.c_struct()
         _check(self.lib.dk_rx_process_host(self._ctx, ctypes.byref(b), ctypes.byref(r), chunk_frames),
                "dk_rx_process_host")
+
+    def path_stats(self, enable: Optional[bool] = None) -> Optional[np.ndarray]:
+        """Diagnostics (dk_diag.h): enable/disable per-path frame counters, or read them ([4] u64)."""
+        if enable is not None:
+            _check(self.lib.dk_diag_path_stats_enable(self._ctx, int(enable)), "dk_diag_path_stats_enable")
+            return None
+        out = np.zeros(4, np.uint64)
+        _check(self.lib.dk_diag_path_stats_read(self._ctx, out.ctypes.data), "dk_diag_path_stats_read")
+        return out
 
     def tx_checksum(self, batch: FrameBatch, stream=None) -> None:
         """Fill IPv4/TCP/UDP checksums in place (serialize_and_attach with tx offload off)."""

@@ -12,9 +12,18 @@ extern "C" {
 
 /* Streaming read of `bytes` (multiple of 16) of device memory at `buf`; `scratch` = device u32[grid] (zeroed by the
  * caller). Used to measure the achievable HBM read bandwidth on the running box. Async on `stream`.
- * mode 0: grid-stride loads; 1: contiguous 8 KiB per wave step; 2: as 1 with nontemporal loads.
+ * mode 0: grid-stride loads; 1: contiguous 8 KiB per wave step; 2: as 1 with nontemporal loads; 3: 16 KiB per wave
+ * step, nontemporal; 4/5: 16 KiB per wave step by LDS-DMA (global_load_lds), nontemporal / default policy.
  * Returns 0, EINVAL or EIO. */
 int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode, void* stream);
+
+/* Per-path frame counters of a receive context (off by default). Paths: [0] vector path, frame <= 64 B in registers;
+ * [1] vector path, frame streamed by a quarter-wave; [2] streamed but the L4 segment re-summed in-lane (IPv4
+ * total_length far below the frame length); [3] per-lane byte-load path (unaligned frame, IHL != 5, or a frame too
+ * short for the fixed headers). Enabling costs one atomic per wave per tile. */
+struct dk_rx_ctx;
+int dk_diag_path_stats_enable(struct dk_rx_ctx* ctx, int on);       /* 0, EINVAL or ENOMEM; on: counters reset */
+int dk_diag_path_stats_read(struct dk_rx_ctx* ctx, uint64_t out[4]); /* synchronous; 0 or EINVAL */
 
 #ifdef __cplusplus
 }

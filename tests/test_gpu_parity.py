@@ -274,3 +274,27 @@ def test_flow_counter_modes_and_wrap_guard(torch_cuda, monkeypatch):
     monkeypatch.setenv("DK_RX_GRID", "1")
     got = run_gpu(blob, off, lens, flows)
     assert int(got["flow_counts"][0]) == n and int(got["verdict_counts"][0]) == n
+
+
+@pytest.mark.parametrize("mix", ["tcp1500", "udp64", "imix"])
+def test_aligned_traffic_stays_on_vector_path(torch_cuda, mix):
+    """Performance guard (dk_diag path counters): well-formed 64-byte-slot traffic never falls back to the byte-load
+    path; frames <= 64 B stay in registers, larger ones are streamed by quarter-waves."""
+    import torch
+
+    n = 20000
+    flows = synth.make_flows(256, kind="udp" if mix == "udp64" else "tcp")
+    ip_len = {"tcp1500": 1486, "udp64": 50, "imix": synth.imix_ip_lengths(n)}[mix]
+    tr = synth.traffic(n, ip_len, flows, seed=2)
+    blob, off, lens = synth.build_numpy(tr)
+    eng = RxEngine(Config(LOCAL))
+    eng.set_sockets(flows)
+    eng.path_stats(True)
+    b = FrameBatch.from_numpy(blob, off, lens)
+    r = eng.results(n)
+    eng.receive_batch(b, r)
+    torch.cuda.synchronize()
+    st = eng.path_stats()
+    small = int((lens <= 64).sum())
+    assert st.tolist() == [small, n - small, 0, 0], st
+    assert (r.to_numpy()["meta"] & 0xFF <= 1).all()

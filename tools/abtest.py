@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of several libdk_rx.so builds in ONE process on the same batch (tuning tool).
+
+    python tools/abtest.py --workload c2_tcp1500 --grids 2,3,4 build/variants/*.so
+Each (variant, grid) is timed `--iters` launches per repetition, repetitions interleaved; prints the median ms.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--workload", default="c2_tcp1500")
+    ap.add_argument("--grids", default="2,3,4")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=7)
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    from demikernel_amd import Config, RxEngine, synth
+
+    base = RxEngine(Config(synth.BOB_IPV4))
+    batch, flows, tr = bench.make_batch(base, args.workload, 0, synth.SEED, 1)
+    engines = {}
+    for v in args.variants:
+        e = RxEngine(Config(synth.BOB_IPV4), lib_path=os.path.abspath(v))
+        e.set_sockets(flows)
+        engines[os.path.basename(v)[:-3]] = (e, e.results(batch.n))
+    fb = int(tr.frame_len.astype(np.int64).sum())
+    algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES)
+    grids = [int(g) for g in args.grids.split(",")]
+    times = {(k, g): [] for k in engines for g in grids}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rep in range(args.reps):
+        for g in grids:
+            os.environ["DK_RX_GRID_PER_CU"] = str(g)
+            for k, (e, r) in engines.items():
+                e.receive_batch(batch, r)
+                ev0.record()
+                for _ in range(args.iters):
+                    e.receive_batch(batch, r)
+                ev1.record()
+                torch.cuda.synchronize()
+                times[(k, g)].append(ev0.elapsed_time(ev1) / args.iters)
+    for (k, g), ts in sorted(times.items(), key=lambda x: (x[0][1], x[0][0])):
+        ms = float(np.median(ts))
+        print(json.dumps({"variant": k, "grid_per_cu": g, "workload": args.workload, "ms": round(ms, 4),
+                          "algo_GBps": round(algo / ms / 1e6, 1), "spread": round((max(ts) - min(ts)) / ms, 3)}))
+
+
+if __name__ == "__main__":
+    main()
