@@ -63,6 +63,7 @@ struct RxParams {
     uint32_t flow_words;     // kFlowLds: ceil(nflows / 2)
     uint32_t* flow_scratch;  // kFlowLds: [grid][flow_words]
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
+    uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave
     dk_rx_results res;
 };
 

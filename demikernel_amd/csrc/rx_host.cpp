@@ -125,9 +125,13 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn), 1);
         c->occ_dyn = dyn;
     }
-    // Resident workgroups per CU: 4 (16 waves/CU) measured best for every workload once phase B streams whole frames
-    // (DESIGN.md "Tuning log"); fewer when LDS (large socket tables) or registers do not admit 4.
-    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, 4u);
+    // Schedule and resident workgroups per CU (measured, DESIGN.md "Tuning log"): large frames (>= 1 KiB of blob per
+    // frame) stream best with one contiguous share per wave and 3 workgroups/CU; small and mixed frames with
+    // round-robin tiles and 4/CU. Never more than the occupancy admits (large socket tables take LDS).
+    const uint64_t bytes_per_frame = p.frames_bytes / p.n;
+    p.sched = bytes_per_frame >= 1024 ? 1u : 0u;
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.sched ? 3u : 4u);
+    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)atoi(e) ? 1u : 0u;
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
     if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
@@ -138,8 +142,8 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         p.flow_scratch = fs.p;
     }
     if (getenv("DK_RX_DEBUG"))
-        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u\n", p.n, ntiles, grid,
-                c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words);
+        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u\n", p.n, ntiles,
+                grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched);
     return dk_launch_rx(p, grid, stream);
 }
 

@@ -45,13 +45,14 @@ constexpr uint32_t kPendUdp = 0xF1u;   // UDP header parsed; awaiting U3/demux
 #ifndef DK_MIN_WAVES
 #define DK_MIN_WAVES 1
 #endif
-#ifndef DK_DESC_PREFETCH
-#define DK_DESC_PREFETCH 1  // load the next tile's descriptors before processing the current one
-#endif
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kCoopU = DK_COOP_U; // dwordx4 loads per lane per phase-B round
 constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave covers per round
+#ifndef DK_ROUNDS_PER_STEP
+#define DK_ROUNDS_PER_STEP 2
+#endif
+constexpr uint32_t kRoundsPerStep = DK_ROUNDS_PER_STEP;  // phase-B rounds whose loads are in flight together
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
@@ -273,6 +274,13 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // One frame per lane, 256 frames per workgroup tile: phases A, B, C and the result stores. Every lane of the
 // workgroup calls it (phase B is wave-cooperative). Returns the verdict and the flow id (DK_FLOW_NONE if none).
 // Per-wave LDS used by one tile. Strides of 5 and 3 uint4 keep the owner-lane ds_read_b128 conflict-free.
+// One quarter-wave's frame in a phase-B step.
+struct CoopSlot {
+    const uint4* base;
+    uint32_t nb, j, acc;
+    bool has;
+};
+
 struct WaveLds {
     uint4 rec[64];         // phase B: per rank {owner lane, frame offset, blocks, 0}
     uint32_t csum[64];     // phase B: whole-frame LE-half sums by owner lane
@@ -290,9 +298,8 @@ struct WaveLds {
 //     contiguous pass keeps DRAM rows open (a separate 64-byte header read per frame cost 8 %).
 //   Phase C (lane): parse from registers, checksum = sum(all blocks) - sum[0, S) - sum[E, 16 * nblk) (exact integer
 //     arithmetic), T4/U3, options, demux, results.
-__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t lane, WaveLds& W, uint32_t off,
-                                        uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
-    const bool live = i < P.n;
+__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
+                                        uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
 
     // ---------------- Phase A: descriptor (loaded by the caller); small frames into registers ----------------
     const bool inb = live && (uint64_t)off + len <= P.frames_bytes;
@@ -338,35 +345,50 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t q = lane >> 4, l16 = lane & 15;
-            for (uint32_t r = 0; r * 4 < ncoop; r++) {
-                const uint32_t k = r * 4 + q;
-                const bool has = k < ncoop;
-                const uint4 rec = has ? W.rec[k] : make_uint4(0, 0, 0, 0);
-                const uint32_t j = rec.x, nb = rec.z;
-                const uint4* base = reinterpret_cast<const uint4*>(P.frames + rec.y);
-                uint32_t acc = 0;
+            for (uint32_t r = 0; r * 4 < ncoop; r += kRoundsPerStep) {
+                // kRoundsPerStep rounds per step: their loads are all in flight together (kRoundsPerStep * 4
+                // consecutive frames per wave, one contiguous region of the blob).
+                CoopSlot sl[kRoundsPerStep];
+#pragma unroll
+                for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+                    const uint32_t k = (r + h) * 4 + q;
+                    sl[h].has = k < ncoop;
+                    const uint4 rec = sl[h].has ? W.rec[k] : make_uint4(0, 0, 0, 0);
+                    sl[h].j = rec.x;
+                    sl[h].nb = rec.z;
+                    sl[h].base = reinterpret_cast<const uint4*>(P.frames + rec.y);
+                    sl[h].acc = 0;
+                }
                 for (uint32_t it = 0; it < maxit; it++) {
                     const uint32_t b0 = it * kCoopSpan + l16;
-                    uint4 d[kCoopU];
+                    uint4 d[kRoundsPerStep][kCoopU];
 #pragma unroll
-                    for (uint32_t u = 0; u < kCoopU; u++) {
-                        const uint32_t b = b0 + 16 * u;
-                        d[u] = b < nb ? ld_stream(base + b) : make_uint4(0, 0, 0, 0);
-                    }
+                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
 #pragma unroll
-                    for (uint32_t u = 0; u < kCoopU; u++) {
-                        const uint32_t b = b0 + 16 * u;
-                        acc = block_sum(d[u], acc);
-                        if (has && b < 4) W.hdr[j][b] = d[u];                // big frame: 4 < nb
-                        if (b < nb && b + 2 >= nb) W.tail[j][b + 2 - nb] = d[u];
-                    }
+                        for (uint32_t u = 0; u < kCoopU; u++) {
+                            const uint32_t b = b0 + 16 * u;
+                            d[h][u] = b < sl[h].nb ? ld_stream(sl[h].base + b) : make_uint4(0, 0, 0, 0);
+                        }
+#pragma unroll
+                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
+#pragma unroll
+                        for (uint32_t u = 0; u < kCoopU; u++) {
+                            const uint32_t b = b0 + 16 * u;
+                            sl[h].acc = block_sum(d[h][u], sl[h].acc);
+                            if (sl[h].has && b < 4) W.hdr[sl[h].j][b] = d[h][u];  // big frame: 4 < nb
+                            if (b < sl[h].nb && b + 2 >= sl[h].nb) W.tail[sl[h].j][b + 2 - sl[h].nb] = d[h][u];
+                        }
                 }
-                // Quarter = DPP row of 16 lanes: inclusive row scan by row_shr 1/2/4/8; lane 15 holds the sum.
-                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xF, 0xF, false);
-                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x112, 0xF, 0xF, false);
-                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x114, 0xF, 0xF, false);
-                acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x118, 0xF, 0xF, false);
-                if (has && l16 == 15) W.csum[j] = acc;
+#pragma unroll
+                for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+                    // Quarter = DPP row of 16 lanes: inclusive row scan by row_shr 1/2/4/8; lane 15 holds the sum.
+                    uint32_t acc = sl[h].acc;
+                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xF, 0xF, false);
+                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x112, 0xF, 0xF, false);
+                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x114, 0xF, 0xF, false);
+                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x118, 0xF, 0xF, false);
+                    if (sl[h].has && l16 == 15) W.csum[sl[h].j] = acc;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -493,8 +515,8 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, uint32_t 
     fid_out = fid;
 }
 
-// Persistent kernel: workgroup b processes tiles b, b + G, b + 2G, ... (G = resident workgroups, host-chosen), so
-// per-workgroup state lives across tiles: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
+// Persistent kernel: G resident workgroups (host-chosen); each wave walks its own equal, contiguous share of the batch
+// in 64-frame chunks, so per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
 // wraps). At exit the histogram row is written with plain stores to flow_scratch[b][*] and dk_flow_reduce_kernel adds
 // the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
@@ -512,37 +534,37 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     __syncthreads();
 
-    const uint32_t ntiles = (P.n + kBlock - 1) / kBlock;
-    uint32_t noff = 0, nlen = 0;  // descriptors of this workgroup's next tile
-    {
-        const uint32_t i0 = blockIdx.x * kBlock + tid;
-        if (i0 < P.n) {
-            noff = P.off[i0];
-            nlen = P.len[i0];
-        }
+    // Schedule (host-chosen per launch, measured in DESIGN.md "Tuning log"):
+    //   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame) and walks it in 64-frame chunks
+    //            (no tile quantization; best for large frames);
+    //   sched 0: round-robin 256-frame tiles, wave wv of workgroup b takes frames [t * 256 + 64 wv, +64) of tiles
+    //            t = b, b + G, ... (the grid sweeps one contiguous window of the blob; best for small/mixed frames).
+    uint32_t f0, f1, cstep;
+    if (P.sched == 1) {
+        const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
+        f0 = (uint32_t)(((uint64_t)P.n * gw) / nw);
+        f1 = (uint32_t)(((uint64_t)P.n * (gw + 1)) / nw);
+        cstep = 64;
+    } else {
+        f0 = blockIdx.x * kBlock + wv * 64;
+        f1 = P.n;
+        cstep = gridDim.x * kBlock;
     }
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t i = t * kBlock + tid;
+    uint32_t noff = 0, nlen = 0;  // descriptors of this wave's next chunk
+    if (f0 + lane < f1) {
+        noff = P.off[f0 + lane];
+        nlen = P.len[f0 + lane];
+    }
+    for (uint32_t c = f0; c < f1; c += cstep) {
+        const uint32_t i = c + lane;
+        const bool live = i < f1;
         const uint32_t off = noff, len = nlen;
-#if DK_DESC_PREFETCH
-        const uint32_t i2 = i + gridDim.x * kBlock;
-        if (t + gridDim.x < ntiles && i2 < P.n) {
-            noff = P.off[i2];
-            nlen = P.len[i2];
+        if (i + cstep < f1) {  // prefetch the next chunk's descriptors
+            noff = P.off[i + cstep];
+            nlen = P.len[i + cstep];
         }
-#endif
         uint32_t v, fid;
-        rx_tile(P, i, lane, s_wave[wv], off, len, v, fid);
-#if !DK_DESC_PREFETCH
-        {
-            const uint32_t i2 = i + gridDim.x * kBlock;
-            if (t + gridDim.x < ntiles && i2 < P.n) {
-                noff = P.off[i2];
-                nlen = P.len[i2];
-            }
-        }
-#endif
-        const bool live = i < P.n;
+        rx_tile(P, i, live, lane, s_wave[wv], off, len, v, fid);
         if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
             if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
             else if (P.flow_mode == kFlowGlobal)
