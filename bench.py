@@ -63,46 +63,73 @@ def make_batch(eng, name, rank, seed_base, world=1):
 
 def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allreduce=False):
     """Run warmup + timed steps. A step = the receive pass over one batch (+ for N > 1 the all-reduce of this step's
-    per-flow counts). Returns (wall seconds for `steps`, per-launch kernel seconds, per-step collective seconds)."""
+    per-flow counts). For N > 1 the counters are double-buffered and the all-reduce is issued asynchronously (RCCL runs
+    on its own stream), so step k's reduction overlaps step k+1's kernel.
+    Returns (wall seconds for `steps`, per-launch kernel seconds, per-step collective seconds measured unoverlapped)."""
     import torch
+
+    gloo = dist is not None and dist.get_backend() == "gloo"
+    bufs = [res.t["flow_counts"], torch.zeros_like(res.t["flow_counts"])] if counts_allreduce else []
+    pending = [None, None]
+
+    def reduce(buf, async_op):
+        if gloo:  # rehearsal only: gloo reduces a host copy, synchronously
+            h = buf.cpu()
+            dist.all_reduce(h)
+            buf.copy_(h)
+            return None
+        return dist.all_reduce(buf, async_op=async_op)
 
     def step(k, ev=None):
         b = batches[k % len(batches)]
         if counts_allreduce:
-            res.t["flow_counts"].zero_()
+            slot = k % 2
+            if pending[slot] is not None:
+                pending[slot].wait()  # stream dependency: the buffer's previous all-reduce has finished
+                pending[slot] = None
+            bufs[slot].zero_()
+            res.t["flow_counts"] = bufs[slot]
         if ev:
             ev[0].record(stream)
         eng.receive_batch(b, res, stream=stream)
         if ev:
             ev[1].record(stream)
         if counts_allreduce:
-            fc = res.t["flow_counts"]
-            if dist.get_backend() == "gloo":  # rehearsal only: gloo reduces a host copy
-                h = fc.cpu()
-                dist.all_reduce(h)
-                fc.copy_(h)
-            else:
-                dist.all_reduce(fc)
-            if ev:
-                ev[2].record(stream)
+            pending[k % 2] = reduce(bufs[k % 2], True)
+
+    def drain():
+        for slot in (0, 1):
+            if pending[slot] is not None:
+                pending[slot].wait()
+                pending[slot] = None
 
     for k in range(warmup):
         step(k)
+    drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(steps)]
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(steps)]
     t0 = time.perf_counter()
     for k in range(steps):
         step(k, ev[k])
+    drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern = [a.elapsed_time(b) / 1e3 for a, b, _ in ev]
-    coll = [b.elapsed_time(c) / 1e3 for _, b, c in ev] if counts_allreduce else []
+    kern = [a.elapsed_time(b) / 1e3 for a, b in ev]
+    coll = []
+    if counts_allreduce:  # the collective alone, unoverlapped, for the report
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            reduce(bufs[0], False)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            coll.append(e0.elapsed_time(e1) / 1e3)
     return wall, kern, coll
 
 
@@ -153,6 +180,25 @@ def host_path_rate(eng, batch, flows, nframes, reps=3):
         rates.append(nbytes / (time.perf_counter() - t) / 1e9)
     return {"gbps": round(max(rates), 2), "frames": n, "bytes": nbytes, "reps": reps,
             "pipeline": "3 streams, 65536-frame chunks, pinned host memory (dk_rx_process_host)"}
+
+
+def tx_rate(eng, batch, frame_bytes, stream, iters=20):
+    """dk_tx_checksum kernel time over an HBM-resident batch: frame bytes read, 2 checksum fields written per frame."""
+    import torch
+
+    for _ in range(3):
+        eng.tx_checksum(batch, stream=stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        eng.tx_checksum(batch, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    algo = frame_bytes + batch.n * (DESC_BYTES + 4)
+    return {"gbps": round(frame_bytes / t / 1e9, 1), "kernel_ms_avg": round(t * 1e3, 4),
+            "roofline_achieved_gbps": round(algo / t / 1e9, 1), "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_launch": algo}
 
 
 def load_traffic_profile(workload):
@@ -245,7 +291,8 @@ def main():
         "data": "synthetic (seeded frames generated on device; 1% corrupted tail)",
         "config": {"workload": WORKLOADS[name][0], "name": name, "frames_per_gpu": batch.n,
                    "global_frames": total_frames, "parallelism": f"packet-shard x{world}",
-                   "collective": "all_reduce(flow_counts, u64) per step" if world > 1 else "none"},
+                   "collective": ("all_reduce(flow_counts, u64) per step, async, double-buffered (overlaps the next "
+                                  "step's kernel)") if world > 1 else "none"},
         "mpkt_s": round(total_frames * args.steps / wall / 1e6, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -258,7 +305,15 @@ def main():
         gbs, used, n_s, nb_s, reps = cpu_baseline(batch, flows, args.cpu_sample, args.cpu_seconds)
         out["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s", "cores": used, "kind": "port",
                                "sample": f"first {n_s} frames of the same batch ({nb_s / 1e6:.0f} MB), "
-                                         f"{reps} reps over >= {args.cpu_seconds:.0f} s, median"}
+                                         f"{reps} reps over >= {args.cpu_seconds:.0f} s, median; oracle/dk_oracle.cpp "
+                                         f"(C++ restatement of the Rust path, clang -O3, 1 thread as the reference's "
+                                         f"single-threaded LibOS)"}
+        if not args.no_extras:
+            # the same restatement on all host cores of this box's share (OpenMP packet shards), as a scaled figure
+            threads = min(os.cpu_count() or 1, 16)
+            gbs_mt, used_mt, _, _, _ = cpu_baseline(batch, flows, args.cpu_sample, max(args.cpu_seconds / 2, 1.0),
+                                                    threads=threads)
+            out["cpu_baseline_all_cores"] = {"value": round(gbs_mt, 3), "unit": "GB/s", "cores": used_mt}
     if rank == 0 and world == 1 and not args.no_extras and name == "c2_tcp1500":
         # secondary: 64 B UDP Mpkt/s (config 3) on rotating batches
         eng3 = RxEngine(Config(synth.BOB_IPV4), device=dev)
@@ -272,6 +327,8 @@ def main():
         # host-resident path (NIC ring / socket buffer in pinned host memory): H2D frames + descriptors, kernel,
         # D2H results, pipelined on 3 streams (dk_rx_process_host). Reported beside `value`, never as `value`.
         out["host_path"] = host_path_rate(eng, batch, flows, args.host_frames)
+        # TX checksum fill (dk_tx_checksum) over the same batch (rewrites its checksum fields)
+        out["tx_checksum"] = tx_rate(eng, batch, frame_bytes, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -25,6 +25,7 @@ VERDICTS = [
     "IP_HDR_TRUNC", "IP_TOTLEN_SMALL", "IP_TOTLEN_BIG", "IP_EVIL", "IP_MF", "IP_FRAGOFF", "IP_TTL", "IP_PROTO",
     "IP_CSUM_FFFF", "IP_CSUM", "IP_DST", "IP_SRC", "TCP_SHORT", "TCP_DOFF_TRUNC", "TCP_DOFF_SMALL", "TCP_CSUM",
     "TCP_OPT", "TCP_OPT_EIO", "TCP_NOSOCK", "UDP_SHORT", "UDP_LEN", "UDP_CSUM", "UDP_NOSOCK", "BAD_DESC",
+    "ARP_SHORT", "ARP_UNSUP", "ICMP_SHORT", "ICMP_CSUM", "ICMP_TYPE",
 ]
 V = {name: i for i, name in enumerate(VERDICTS)}
 DK_V_COUNT = len(VERDICTS)

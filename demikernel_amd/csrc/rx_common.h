@@ -67,10 +67,20 @@ struct RxParams {
     dk_rx_results res;
 };
 
+// TX checksum fill (dk_tx_checksum): the same chunk streaming as the receive kernel, in-place checksum writes.
+struct TxParams {
+    uint8_t* frames;
+    uint64_t frames_bytes;
+    const uint32_t* off;
+    const uint16_t* len;
+    uint32_t n;
+    uint32_t sched;  // as RxParams::sched
+};
+
 }  // namespace dk
 
 // Launchers implemented in rx_kernels.hip (internal symbols, not part of the C ABI).
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes);  // occupancy of dk_rx_kernel per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
-int dk_launch_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
-                          uint32_t n, void* stream);
+int dk_tx_resident_blocks();  // occupancy of dk_tx_kernel per CU (0 on error)
+int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream);

@@ -429,7 +429,24 @@ int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
 int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
                    void* stream) {
     if (n && (!frames || !off || !len)) return EINVAL;
-    return dk_launch_tx_checksum(frames, frames_bytes, off, len, n, stream);
+    if (n == 0) return 0;
+    // Persistent grid on the current device, same schedule rule as the receive kernel (launch_batch).
+    static thread_local int dev_cached = -1;
+    static thread_local uint32_t cus = 0, occ = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return ENODEV;
+    if (dev != dev_cached) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            return ENODEV;
+        cus = (uint32_t)c;
+        occ = (uint32_t)std::max(dk_tx_resident_blocks(), 1);
+        dev_cached = dev;
+    }
+    dk::TxParams p{frames, frames_bytes, off, len, n, frames_bytes / n >= 1024 ? 1u : 0u};
+    const uint32_t per_cu = std::min<uint32_t>(occ, p.sched ? 3u : 4u);
+    const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
+    return dk_launch_tx(p, grid, stream);
 }
 
 const char* dk_rx_verdict_name(int v) {
@@ -439,13 +456,15 @@ const char* dk_rx_verdict_name(int v) {
         "IP_TOTLEN_BIG",  "IP_EVIL",       "IP_MF",        "IP_FRAGOFF",     "IP_TTL",        "IP_PROTO",
         "IP_CSUM_FFFF",   "IP_CSUM",       "IP_DST",       "IP_SRC",         "TCP_SHORT",     "TCP_DOFF_TRUNC",
         "TCP_DOFF_SMALL", "TCP_CSUM",      "TCP_OPT",      "TCP_OPT_EIO",    "TCP_NOSOCK",    "UDP_SHORT",
-        "UDP_LEN",        "UDP_CSUM",      "UDP_NOSOCK",   "BAD_DESC"};
+        "UDP_LEN",        "UDP_CSUM",      "UDP_NOSOCK",   "BAD_DESC",       "ARP_SHORT",     "ARP_UNSUP",
+        "ICMP_SHORT",     "ICMP_CSUM",     "ICMP_TYPE"};
     return (v >= 0 && v < DK_V_COUNT) ? names[v] : "UNKNOWN";
 }
 
 int dk_rx_verdict_errno(int v) {
     switch (v) {
         case DK_V_ETH_TYPE: case DK_V_IP_VERSION: case DK_V_IP_MF: case DK_V_IP_FRAGOFF: case DK_V_IP_PROTO:
+        case DK_V_ARP_UNSUP:
             return 95;  // ENOTSUP
         case DK_V_TCP_OPT_EIO:
             return 5;   // EIO
@@ -455,7 +474,7 @@ int dk_rx_verdict_errno(int v) {
         case DK_V_IP_TOTLEN_SMALL: case DK_V_IP_TOTLEN_BIG: case DK_V_IP_EVIL: case DK_V_IP_TTL:
         case DK_V_IP_CSUM_FFFF: case DK_V_IP_CSUM: case DK_V_TCP_SHORT: case DK_V_TCP_DOFF_TRUNC:
         case DK_V_TCP_DOFF_SMALL: case DK_V_TCP_CSUM: case DK_V_TCP_OPT: case DK_V_UDP_SHORT: case DK_V_UDP_LEN:
-        case DK_V_UDP_CSUM:
+        case DK_V_UDP_CSUM: case DK_V_ARP_SHORT: case DK_V_ICMP_SHORT: case DK_V_ICMP_CSUM: case DK_V_ICMP_TYPE:
             return 74;  // EBADMSG
         default:
             return 0;

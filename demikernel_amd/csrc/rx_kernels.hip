@@ -35,6 +35,9 @@ namespace {
 constexpr uint32_t kNone = 0xFFu;      // not yet decided
 constexpr uint32_t kPendTcp = 0xF0u;   // TCP header parsed; awaiting T4/T5/demux
 constexpr uint32_t kPendUdp = 0xF1u;   // UDP header parsed; awaiting U3/demux
+constexpr uint32_t kPendIcmp = 0xF2u;  // ICMPv4 message >= 8 bytes; awaiting its checksum and type checks
+// ICMPv4 type bytes Icmpv4Type2::parse accepts (icmpv4/protocol.rs:37-56): 0, 3, 4, 5, 8 .. 14.
+constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | (0x7Fu << 8);
 // Tuning knobs (compile-time; defaults are the measured best, see DESIGN.md "Tuning log").
 #ifndef DK_COOP_U
 #define DK_COOP_U 6
@@ -147,7 +150,7 @@ struct Lane {
     uint32_t v;       // verdict or kPend*
     uint32_t src, dst;
     uint32_t ports;   // src_port | dst_port << 16
-    uint32_t b1213;   // tcp byte 12 | byte 13 << 8
+    uint32_t mhi;     // result meta bits 8..31 (protocol and protocol bytes, dk_rx.h)
     uint32_t seq, ack, winurg;
     uint32_t S, E;    // L4 region [S, E), frame-relative
     uint32_t hlen;    // TCP data offset / 8 for UDP
@@ -156,15 +159,29 @@ struct Lane {
     uint32_t lsum;    // LE-half sum of the part of [S, E) summed in-lane
 };
 
-// Everything up to (not including) the L4 checksum, in Appendix A order. kFast: IHL == 5 asserted by the caller,
-// so S == 34 is a compile-time constant and every field offset folds to a register extract.
-template <bool kFast, class A>
+// Everything up to (not including) the L4 checksum, in Appendix A order (slow path: any alignment, any IHL, bytes
+// read from global memory; the fast path is parse_fast below).
+template <class A>
 __device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const RxParams& P, Lane& L) {
     L.v = kNone;
     if (len < 14) { L.v = DK_V_ETH_SHORT; return; }                          // E1
     const uint32_t et = a.be16(12);
     if (et != 0x0806u && et != 0x0800u && et != 0x86ddu) { L.v = DK_V_ETH_TYPE; return; }  // E2
-    if (et == 0x0806u) { L.v = DK_V_ARP; return; }
+    if (et == 0x0806u) {  // ArpHeader::parse_and_consume (arp/header.rs:80-111, :161-166)
+        if (len - 14 < 28) { L.v = DK_V_ARP_SHORT; return; }
+        const uint32_t op = a.be16(20);
+        if (a.be16(14) != 1u || a.be16(16) != 0x0800u || a.b8(18) != 6u || a.b8(19) != 4u || (op != 1u && op != 2u)) {
+            L.v = DK_V_ARP_UNSUP;
+            return;
+        }
+        L.v = DK_V_ARP;
+        L.mhi = op << 8;
+        L.src = a.u32(28);
+        L.dst = a.u32(38);
+        L.S = 14;
+        L.E = len;
+        return;
+    }
     if (et == 0x86ddu) { L.v = DK_V_IPV6; return; }
     const uint32_t iplen = len - 14;
     if (iplen < 20) { L.v = DK_V_IP_SHORT; return; }                         // I1
@@ -192,13 +209,21 @@ __device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const Rx
     const uint32_t src = a.u32(26), dst = a.u32(30);
     if (dst != P.local_ip && dst != 0xFFFFFFFFu) { L.v = DK_V_IP_DST; return; }       // F1
     if (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) { L.v = DK_V_IP_SRC; return; }  // F2
-    if (proto == 1u) { L.v = DK_V_ICMP; return; }
-    const uint32_t S = kFast ? 34u : 14u + hs;
+    const uint32_t S = 14u + hs;
     const uint32_t seg = tot - hs;
     L.src = src;
     L.dst = dst;
     L.S = S;
     L.E = 14 + tot;
+    if (proto == 1u) {  // Icmpv4Header::parse_and_strip (icmpv4/header.rs:47-66)
+        if (seg < 8) { L.v = DK_V_ICMP_SHORT; return; }
+        L.ports = a.be16(S + 4) | (a.be16(S + 6) << 16);
+        L.mhi = 1u | (a.b8(S) << 8) | (a.b8(S + 1) << 16);
+        L.hlen = 8;
+        L.need = 1;
+        L.v = kPendIcmp;
+        return;
+    }
     if (proto == 6u) {
         if (seg < 20) { L.v = DK_V_TCP_SHORT; return; }                      // T1
         const uint32_t b12 = a.b8(S + 12);
@@ -208,7 +233,7 @@ __device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const Rx
         L.ports = a.be16(S) | (a.be16(S + 2) << 16);
         L.seq = a.be32(S + 4);
         L.ack = a.be32(S + 8);
-        L.b1213 = b12 | (a.b8(S + 13) << 8);
+        L.mhi = 6u | (a.b8(S + 13) << 8) | (b12 << 16);
         L.winurg = a.be16(S + 14) | (a.be16(S + 18) << 16);
         L.stored = a.be16(S + 16);
         L.hlen = doff;
@@ -220,9 +245,70 @@ __device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const Rx
         L.ports = a.be16(S) | (a.be16(S + 2) << 16);
         L.stored = a.be16(S + 6);
         L.hlen = 8;
+        L.mhi = 17u;
         L.need = (!P.udp_offload && L.stored != 0) ? 1u : 0u;                // U3 precondition (udp/header.rs:78-82)
         L.v = kPendUdp;
     }
+}
+
+// parse_headers<true> restated without branches for the register window (IHL == 5, len >= 34, every offset < 64):
+// each check is one compare + select, applied last-to-first so the first failing check in Appendix A order wins. The
+// early-return form made the compiler re-materialise every zeroed Lane field on each of its ~25 exits, i.e. ~12
+// v_mov per check per wave on the path every valid frame takes. I3/I4 (hs < 20, iplen < hs) cannot fire here.
+__device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const RxParams& P, Lane& L) {
+    const uint32_t et = a.be16(12);
+    const uint32_t iplen = len - 14;
+    const uint32_t b14 = a.b8(14);
+    const uint32_t tot = a.be16(16);
+    const uint32_t frag = a.be16(20);
+    const uint32_t proto = a.b8(23);
+    const uint32_t ipcs = a.be16(24);
+    const uint32_t hsum = a.le16(14) + a.le16(16) + a.le16(18) + a.le16(20) + a.le16(22) + a.le16(26) + a.le16(28) +
+                          a.le16(30) + a.le16(32);
+    const uint32_t src = a.u32(26), dst = a.u32(30);
+    const uint32_t seg = tot - 20;
+    const uint32_t b12 = a.b8(46);
+    const uint32_t doff = (b12 >> 4) * 4;
+    const bool tcp = proto == 6u;
+    const uint32_t stored = tcp ? a.be16(50) : a.be16(40);
+
+    uint32_t v4 = tcp ? (seg < 20 ? (uint32_t)DK_V_TCP_SHORT                                  // T1
+                         : seg < doff ? (uint32_t)DK_V_TCP_DOFF_TRUNC                         // T2
+                         : doff < 20 ? (uint32_t)DK_V_TCP_DOFF_SMALL : kPendTcp)              // T3
+                      : (seg < 8 ? (uint32_t)DK_V_UDP_SHORT                                   // U1
+                         : a.be16(38) != seg ? (uint32_t)DK_V_UDP_LEN : kPendUdp);            // U2
+    const bool icmp = proto == 1u;
+    uint32_t v = icmp ? (seg < 8 ? (uint32_t)DK_V_ICMP_SHORT : kPendIcmp) : v4;
+    v = (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) ? (uint32_t)DK_V_IP_SRC : v;   // F2
+    v = (dst != P.local_ip && dst != 0xFFFFFFFFu) ? (uint32_t)DK_V_IP_DST : v;                   // F1
+    v = csum_from_residue(be_residue(hsum)) != ipcs ? (uint32_t)DK_V_IP_CSUM : v;                // I13
+    v = ipcs == 0xFFFFu ? (uint32_t)DK_V_IP_CSUM_FFFF : v;                                       // I12
+    v = (proto != 1u && proto != 6u && proto != 17u) ? (uint32_t)DK_V_IP_PROTO : v;              // I11
+    v = a.b8(22) == 0 ? (uint32_t)DK_V_IP_TTL : v;                                               // I10
+    v = (frag & 0x1FFFu) ? (uint32_t)DK_V_IP_FRAGOFF : v;                                        // I9
+    v = (frag & 0x2000u) ? (uint32_t)DK_V_IP_MF : v;                                             // I8
+    v = (frag & 0x8000u) ? (uint32_t)DK_V_IP_EVIL : v;                                           // I7
+    v = tot > iplen ? (uint32_t)DK_V_IP_TOTLEN_BIG : v;                                          // I6
+    v = tot < 20 ? (uint32_t)DK_V_IP_TOTLEN_SMALL : v;                                           // I5
+    v = (b14 >> 4) != 4 ? (uint32_t)DK_V_IP_VERSION : v;                                         // I2
+    v = et == 0x86ddu ? (uint32_t)DK_V_IPV6 : v;
+    v = et == 0x0806u ? (uint32_t)DK_V_ARP : v;
+    v = (et != 0x0806u && et != 0x0800u && et != 0x86ddu) ? (uint32_t)DK_V_ETH_TYPE : v;        // E2
+
+    const bool pend = v == kPendTcp || v == kPendUdp || v == kPendIcmp;
+    L.v = v;
+    L.src = src;
+    L.dst = dst;
+    L.S = 34;
+    L.E = 14 + tot;
+    L.ports = icmp ? a.be16(38) | (a.be16(40) << 16) : a.be16(34) | (a.be16(36) << 16);
+    L.seq = a.be32(38);
+    L.ack = a.be32(42);
+    L.mhi = tcp ? 6u | (a.b8(47) << 8) | (b12 << 16) : icmp ? 1u | (a.b8(34) << 8) | (a.b8(35) << 16) : 17u;
+    L.winurg = a.be16(48) | (a.be16(52) << 16);
+    L.stored = stored;
+    L.hlen = tcp ? doff : 8u;
+    L.need = pend && (tcp ? !P.tcp_offload : icmp ? true : (!P.udp_offload && stored != 0)) ? 1u : 0u;  // U3 :78-82
 }
 
 // TCP option walk (tcp/header.rs:215-302), over the option bytes in global memory. Returns 0 (ok), DK_V_TCP_OPT
@@ -281,34 +367,50 @@ struct CoopSlot {
     bool has;
 };
 
+#ifndef DK_LDSDMA
+#define DK_LDSDMA 0  // phase B via global_load_lds_dwordx4 (LDS-DMA) into per-wave slots instead of register loads
+#endif
+#ifndef DK_COMPACT_LDS
+#define DK_COMPACT_LDS DK_LDSDMA  // strides 4/2 (2-way conflicts on 6 reads per chunk) to leave LDS for DMA slots
+#endif
+constexpr uint32_t kHdrStride = DK_COMPACT_LDS ? 4 : 5, kTailStride = DK_COMPACT_LDS ? 2 : 3;
 struct WaveLds {
-    uint4 rec[64];         // phase B: per rank {owner lane, frame offset, blocks, 0}
+    uint2 rec[64];         // phase B: per rank {owner lane | blocks << 8, frame offset}
     uint32_t csum[64];     // phase B: whole-frame LE-half sums by owner lane
-    uint4 hdr[64][5];      // phase B -> C: bytes [0, 64) of each big frame
-    uint4 tail[64][3];     // phase B -> C: the last two 16-byte blocks of each big frame
+    uint4 hdr[64][kHdrStride];    // phase B -> C: bytes [0, 64) of each big frame
+    uint4 tail[64][kTailStride];  // phase B -> C: the last two 16-byte blocks of each big frame
+#if DK_LDSDMA
+    uint4 dma[kRoundsPerStep][kCoopU][64];  // LDS-DMA landing slots: lane L's 16 bytes at [h][u][L]
+#endif
 };
+typedef __attribute__((address_space(3))) void lds_void;
 
 
-// One frame per lane, 256 frames per workgroup tile. Every lane of the workgroup calls it (phase B is
-// wave-cooperative). Returns the verdict and the flow id (DK_FLOW_NONE if none).
+// The bytes of one 64-frame chunk (phases A and B), shared by the RX and TX kernels. Every lane of the wave calls it
+// (phase B is wave-cooperative).
 //   Phase A (lane): descriptor; frames of <= 64 bytes load their bytes straight into registers.
 //   Phase B (quarter-wave per frame, 4 frames per wave per round): frames of > 64 bytes are streamed whole, once, by
 //     16 lanes (kCoopU x dwordx4 in flight each): blocks summed with v_dot2_u32_u16, the header window and the last
-//     32 bytes deposited in LDS for the owner lane, the quarter's sum reduced by 4 shuffles. Reading each frame in one
-//     contiguous pass keeps DRAM rows open (a separate 64-byte header read per frame cost 8 %).
-//   Phase C (lane): parse from registers, checksum = sum(all blocks) - sum[0, S) - sum[E, 16 * nblk) (exact integer
-//     arithmetic), T4/U3, options, demux, results.
-__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
-                                        uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
-
+//     32 bytes deposited in LDS for the owner lane, the quarter's sum reduced by a DPP row scan. Reading each frame in
+//     one contiguous pass keeps DRAM rows open (a separate 64-byte header read per frame cost 8 %).
+// On return the owner lane holds bytes [0, 64) in C.R and, for big frames, the whole-frame sum in C.fsum and the last
+// two blocks in W.tail[lane].
+struct Chunk {
+    RegAcc R;       // frame bytes [0, 64) (zero beyond the frame for small frames)
+    uint32_t fsum;  // big frames: LE-half sum over blocks [0, nblk)
+    uint32_t nblk;  // big frames: 16-byte blocks covering the frame
+    bool inb, vec, big;  // descriptor in bounds; 16-byte aligned (vector path); streamed by a quarter-wave
+};
+__device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t lane,
+                                             WaveLds& W, uint32_t off, uint32_t len, Chunk& C) {
     // ---------------- Phase A: descriptor (loaded by the caller); small frames into registers ----------------
-    const bool inb = live && (uint64_t)off + len <= P.frames_bytes;
-    const uint8_t* f = P.frames + off;
+    const bool inb = live && (uint64_t)off + len <= frames_bytes;
+    const uint8_t* f = frames + off;
     const bool vec = inb && (reinterpret_cast<uintptr_t>(f) & 15) == 0;  // vector path
     const bool big = vec && len > 64;                                  // streamed by a quarter-wave
     const uint32_t nblk = big ? (len + 15) >> 4 : 0;                     // 16-byte blocks covering the frame
 
-    RegAcc R;
+    RegAcc& R = C.R;
     {
         const uint4* fp = reinterpret_cast<const uint4*>(f);
 #pragma unroll
@@ -323,7 +425,8 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
     }
 
     // ---------------- Phase B: whole-frame quarter-wave streams ----------------
-    uint32_t fsum = 0;  // big frames: LE-half sum over blocks [0, nblk)
+    uint32_t& fsum = C.fsum;  // big frames: LE-half sum over blocks [0, nblk)
+    fsum = 0;
     {
         const uint64_t cm = __ballot(big);
         const uint32_t ncoop = (uint32_t)__popcll(cm);
@@ -331,7 +434,7 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
             if (big) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-                W.rec[rank] = make_uint4(lane, off, nblk, 0);  // per-rank frame record: one ds_read_b128 per round
+                W.rec[rank] = make_uint2(lane | (nblk << 8), off);  // per-rank frame record: one ds_read_b64 per round
             }
             // Wave-uniform iterations per round (1 unless a frame exceeds kCoopSpan blocks, i.e. > 1536 bytes).
             uint32_t maxit = 1;
@@ -353,15 +456,35 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
                 for (uint32_t h = 0; h < kRoundsPerStep; h++) {
                     const uint32_t k = (r + h) * 4 + q;
                     sl[h].has = k < ncoop;
-                    const uint4 rec = sl[h].has ? W.rec[k] : make_uint4(0, 0, 0, 0);
-                    sl[h].j = rec.x;
-                    sl[h].nb = rec.z;
-                    sl[h].base = reinterpret_cast<const uint4*>(P.frames + rec.y);
+                    const uint2 rec = sl[h].has ? W.rec[k] : make_uint2(0, 0);
+                    sl[h].j = rec.x & 0xFFu;
+                    sl[h].nb = rec.x >> 8;
+                    sl[h].base = reinterpret_cast<const uint4*>(frames + rec.y);
                     sl[h].acc = 0;
                 }
                 for (uint32_t it = 0; it < maxit; it++) {
                     const uint32_t b0 = it * kCoopSpan + l16;
                     uint4 d[kRoundsPerStep][kCoopU];
+#if DK_LDSDMA
+#pragma unroll
+                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
+#pragma unroll
+                        for (uint32_t u = 0; u < kCoopU; u++) {
+                            const uint32_t b = b0 + 16 * u;
+                            if (b < sl[h].nb)
+                                __builtin_amdgcn_global_load_lds(static_cast<const void*>(sl[h].base + b),
+                                                                 (lds_void*)(&W.dma[h][u][0]), 16, 0,
+                                                                 DK_NT_LOADS ? 2 : 0);
+                        }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
+#pragma unroll
+                        for (uint32_t u = 0; u < kCoopU; u++) {
+                            const uint32_t b = b0 + 16 * u;
+                            d[h][u] = b < sl[h].nb ? W.dma[h][u][lane] : make_uint4(0, 0, 0, 0);
+                        }
+#else
 #pragma unroll
                     for (uint32_t h = 0; h < kRoundsPerStep; h++)
 #pragma unroll
@@ -369,6 +492,7 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
                             const uint32_t b = b0 + 16 * u;
                             d[h][u] = b < sl[h].nb ? ld_stream(sl[h].base + b) : make_uint4(0, 0, 0, 0);
                         }
+#endif
 #pragma unroll
                     for (uint32_t h = 0; h < kRoundsPerStep; h++)
 #pragma unroll
@@ -378,6 +502,9 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
                             if (sl[h].has && b < 4) W.hdr[sl[h].j][b] = d[h][u];  // big frame: 4 < nb
                             if (b < sl[h].nb && b + 2 >= sl[h].nb) W.tail[sl[h].j][b + 2 - sl[h].nb] = d[h][u];
                         }
+#if DK_LDSDMA
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads retired before the next DMA
+#endif
                 }
 #pragma unroll
                 for (uint32_t h = 0; h < kRoundsPerStep; h++) {
@@ -406,50 +533,78 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
             }
         }
     }
+    C.inb = inb;
+    C.vec = vec;
+    C.big = big;
+    C.nblk = nblk;
+}
+
+// LE-half sum of frame bytes [34, E) on the fast path (IHL == 5), from what stream_chunk left: the register window
+// for small frames; for big frames sum(all blocks) - sum[0, 34) - sum[E, 16 * nblk), the last two blocks being in
+// LDS; a direct byte sum when IPv4 total_length ends more than 32 bytes before the last block (rare; sets resum).
+__device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& W, uint32_t lane, const uint8_t* f,
+                                                 int E, bool& resum) {
+    const RegAcc& R = C.R;
+    if (!C.big) {
+        // [34, E) inside the register window: block 2 (bytes 32..47) and block 3 (48..63)
+        const uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
+        return block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
+    }
+    if ((int)(16 * C.nblk) - E <= 32) {
+        uint32_t pre = block_sum(make_uint4(R.w[0], R.w[1], R.w[2], R.w[3]), 0);
+        pre = block_sum(make_uint4(R.w[4], R.w[5], R.w[6], R.w[7]), pre);
+        pre += R.w[8] & 0xFFFFu;
+        const int t0 = (int)(16 * C.nblk) - 32;
+        const uint4 a = W.tail[lane][0], c = W.tail[lane][1];
+        uint32_t post = block_sum_masked(a.x, a.y, a.z, a.w, E - t0, 16, 0);
+        post = block_sum_masked(c.x, c.y, c.z, c.w, E - t0 - 16, 16, post);
+        return C.fsum - pre - post;
+    }
+    resum = true;
+    return MemAcc{f}.sum_le16(34, (uint32_t)E);
+}
+
+// One frame per lane, 64 frames per wave chunk. Returns the verdict and the flow id (DK_FLOW_NONE if none).
+//   Phases A, B: stream_chunk.
+//   Phase C (lane): parse from registers, checksum = sum(all blocks) - sum[0, S) - sum[E, 16 * nblk) (exact integer
+//     arithmetic), T4/U3, options, demux, results.
+__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
+                                        uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
+    Chunk C;
+    stream_chunk(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+    const RegAcc& R = C.R;
+    const bool inb = C.inb, vec = C.vec, big = C.big;
+    const uint8_t* f = P.frames + off;
 
     // ---------------- Phase C: parse, checksum, options, demux, results ----------------
     // Fast parse: 16-byte aligned, whole Ethernet + IPv4 fixed header present, IHL == 5 (S == 34).
-    const bool fast = vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u;
+    // ARP (ethertype bytes 08 06) is parsed by the byte path (low volume).
+    const bool fast = vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u && (R.w[3] & 0xFFFFu) != 0x0608u;
     bool resum = false;  // path-stats: streamed frame whose segment is re-summed in-lane
     Lane L;
-    L.v = kNone; L.src = L.dst = L.ports = L.b1213 = L.seq = L.ack = L.winurg = 0;
+    L.v = kNone; L.src = L.dst = L.ports = L.mhi = L.seq = L.ack = L.winurg = 0;
     L.S = L.E = L.hlen = L.stored = L.need = L.lsum = 0;
     if (!live) {
         L.v = kNone;
     } else if (!inb) {
         L.v = DK_V_BAD_DESC;
     } else if (fast) {
-        parse_headers<true>(R, len, P, L);
-        if (L.need) {
-            const int E = (int)L.E;
-            if (!big) {
-                // [34, E) inside the register window: block 2 (bytes 32..47) and block 3 (48..63)
-                uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
-                L.lsum = block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
-            } else if ((int)(16 * nblk) - E <= 32) {
-                // sum[S, E) = sum(all blocks) - sum[0, 34) - sum[E, 16 * nblk); the last two blocks are in LDS
-                uint32_t pre = block_sum(make_uint4(R.w[0], R.w[1], R.w[2], R.w[3]), 0);
-                pre = block_sum(make_uint4(R.w[4], R.w[5], R.w[6], R.w[7]), pre);
-                pre += R.w[8] & 0xFFFFu;
-                const int t0 = (int)(16 * nblk) - 32;
-                const uint4 a = W.tail[lane][0], c = W.tail[lane][1];
-                uint32_t post = block_sum_masked(a.x, a.y, a.z, a.w, E - t0, 16, 0);
-                post = block_sum_masked(c.x, c.y, c.z, c.w, E - t0 - 16, 16, post);
-                L.lsum = fsum - pre - post;
-            } else {
-                // IPv4 total_length far below the frame length: sum the segment directly (rare)
-                L.lsum = MemAcc{f}.sum_le16(L.S, L.E);
-                resum = true;
-            }
-        }
+        parse_fast(R, len, P, L);
+        if (L.need) L.lsum = seg_sum_fast(C, W, lane, f, (int)L.E, resum);
     } else {
         const MemAcc M{f};
-        parse_headers<false>(M, len, P, L);
+        parse_headers(M, len, P, L);
         if (L.need) L.lsum = M.sum_le16(L.S, L.E);
     }
 
     uint32_t fid = DK_FLOW_NONE;
-    if (L.v == kPendTcp || L.v == kPendUdp) {
+    if (L.v == kPendIcmp) {
+        // compute_checksum over header + body must fold to 0, i.e. the BE word sum is 0 mod 0xFFFF; the LE-half sum
+        // is 0 mod 0xFFFF exactly then (sum_BE == 256 * sum_LE, 256 invertible mod 0xFFFF) (icmpv4/header.rs:55-57)
+        const uint32_t type = (L.mhi >> 8) & 0xFFu;
+        L.v = mod_ffff(L.lsum) != 0 ? (uint32_t)DK_V_ICMP_CSUM
+              : (type < 15 && ((kIcmpTypes >> type) & 1u)) ? (uint32_t)DK_V_ICMP : (uint32_t)DK_V_ICMP_TYPE;
+    } else if (L.v == kPendTcp || L.v == kPendUdp) {
         const bool tcp = L.v == kPendTcp;
         if (L.need) {
             const uint32_t s = L.lsum - bswap16(L.stored);  // the reference sums the stored field as zero
@@ -481,11 +636,12 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
 
     const uint32_t v = L.v;
     if (live) {
-        const bool full = v == DK_V_OK_TCP || v == DK_V_TCP_NOSOCK || v == DK_V_OK_UDP || v == DK_V_UDP_NOSOCK;
+        // fields for delivered / no-socket TCP and UDP and for parsed ARP and ICMPv4 (codes 0..3, dk_rx.h)
+        const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;
         const bool is_tcp = v == DK_V_OK_TCP || v == DK_V_TCP_NOSOCK;
         uint32_t meta = v, src = 0, dst = 0, ports = 0, pay = 0, seq = 0, ack = 0, win = 0;
         if (full) {
-            meta |= is_tcp ? ((6u << 8) | ((L.b1213 >> 8) << 16) | ((L.b1213 & 0xFFu) << 24)) : (17u << 8);
+            meta |= L.mhi << 8;
             src = L.src;
             dst = L.dst;
             ports = L.ports;
@@ -515,8 +671,31 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
     fid_out = fid;
 }
 
-// Persistent kernel: G resident workgroups (host-chosen); each wave walks its own equal, contiguous share of the batch
-// in 64-frame chunks, so per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
+// Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"):
+//   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame) and walks it in 64-frame chunks
+//            (no tile quantization; best for large frames);
+//   sched 0: round-robin 256-frame tiles, wave wv of workgroup b takes frames [t * 256 + 64 wv, +64) of tiles
+//            t = b, b + G, ... (the grid sweeps one contiguous window of the blob; best for small/mixed frames).
+struct WaveRange {
+    uint32_t f0, f1, step;  // chunks start at f0, f0 + step, ... below f1
+};
+__device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint32_t wv) {
+    WaveRange r;
+    if (sched == 1) {
+        const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
+        r.f0 = (uint32_t)(((uint64_t)n * gw) / nw);
+        r.f1 = (uint32_t)(((uint64_t)n * (gw + 1)) / nw);
+        r.step = 64;
+    } else {
+        r.f0 = blockIdx.x * kBlock + wv * 64;
+        r.f1 = n;
+        r.step = gridDim.x * kBlock;
+    }
+    return r;
+}
+
+// Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
+// per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
 // wraps). At exit the histogram row is written with plain stores to flow_scratch[b][*] and dk_flow_reduce_kernel adds
 // the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
@@ -534,22 +713,8 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     __syncthreads();
 
-    // Schedule (host-chosen per launch, measured in DESIGN.md "Tuning log"):
-    //   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame) and walks it in 64-frame chunks
-    //            (no tile quantization; best for large frames);
-    //   sched 0: round-robin 256-frame tiles, wave wv of workgroup b takes frames [t * 256 + 64 wv, +64) of tiles
-    //            t = b, b + G, ... (the grid sweeps one contiguous window of the blob; best for small/mixed frames).
-    uint32_t f0, f1, cstep;
-    if (P.sched == 1) {
-        const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
-        f0 = (uint32_t)(((uint64_t)P.n * gw) / nw);
-        f1 = (uint32_t)(((uint64_t)P.n * (gw + 1)) / nw);
-        cstep = 64;
-    } else {
-        f0 = blockIdx.x * kBlock + wv * 64;
-        f1 = P.n;
-        cstep = gridDim.x * kBlock;
-    }
+    const WaveRange r = wave_range(P.sched, P.n, wv);
+    const uint32_t f0 = r.f0, f1 = r.f1, cstep = r.step;
     uint32_t noff = 0, nlen = 0;  // descriptors of this wave's next chunk
     if (f0 + lane < f1) {
         noff = P.off[f0 + lane];
@@ -612,25 +777,25 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
-// TX checksum fill: lane per frame, byte-granular sums (the TX path is not the benchmark).
-// Mirrors Ipv4Header::serialize_and_attach (ipv4/header.rs:229-266), TcpHeader::serialize_and_attach
-// (tcp/header.rs:397-404) and UdpHeader::serialize_and_attach (udp/header.rs:119-124) with offload off.
+// TX checksum fill: Ipv4Header::serialize_and_attach (ipv4/header.rs:229-266),
+// TcpHeader::serialize_and_attach (tcp/header.rs:397-404) and UdpHeader::serialize_and_attach (udp/header.rs:119-124)
+// with offload off, over already-built frames: the IPv4 header checksum (first 20 bytes) and the TCP/UDP checksum
+// with the frame's own src/dst in the pseudo-header are written in place. Frames that are not Ethernet/IPv4 with a
+// consistent total_length are left untouched; TCP with a bad data offset / UDP shorter than 8 keep only the IPv4 fill
+// (oracle dko_tx_fill_checksums). Frames must not overlap.
 // ---------------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void dk_tx_checksum_kernel(uint8_t* frames, uint64_t frames_bytes,
-                                                                const uint32_t* off, const uint16_t* lens,
-                                                                uint32_t n) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t o = off[i], len = lens[i];
-    if ((uint64_t)o + len > frames_bytes || len < 34) return;
-    uint8_t* f = frames + o;
+__device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {  // p is 2-byte aligned on the fast path
+    *reinterpret_cast<uint16_t*>(p) = (uint16_t)bswap16(v);
+}
+
+// Byte path (misaligned frames, IHL != 5): lane per frame.
+__device__ __noinline__ void tx_slow(uint8_t* f, uint32_t len) {
+    if (len < 34) return;
     const MemAcc M{f};
     if (M.be16(12) != 0x0800u) return;
     const uint32_t hs = (f[14] & 15u) * 4;
     const uint32_t tot = M.be16(16);
     if (hs < 20 || 14 + tot > len || tot < hs) return;
-    f[24] = 0;
-    f[25] = 0;
     const uint32_t hsum = M.le16(14) + M.le16(16) + M.le16(18) + M.le16(20) + M.le16(22) + M.le16(26) + M.le16(28) +
                           M.le16(30) + M.le16(32);
     const uint32_t ipc = csum_from_residue(be_residue(hsum));
@@ -650,15 +815,67 @@ __global__ __launch_bounds__(kBlock) void dk_tx_checksum_kernel(uint8_t* frames,
     } else {
         return;
     }
-    f[cs_at] = 0;
-    f[cs_at + 1] = 0;
-    const uint32_t s = M.sum_le16(S, E);
+    const uint32_t s = M.sum_le16(S, E) - M.le16(cs_at);  // the field is summed as zero
     const uint32_t src = M.u32(26), dst = M.u32(30);
     const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) + bswap16(dst >> 16) +
                             proto + seg;
     const uint32_t c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
     f[cs_at] = (uint8_t)(c >> 8);
     f[cs_at + 1] = (uint8_t)c;
+}
+
+__device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t lane, WaveLds& W, uint32_t off,
+                                        uint32_t len) {
+    Chunk C;
+    stream_chunk(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+    if (!C.inb) return;
+    uint8_t* f = P.frames + off;
+    const RegAcc& R = C.R;
+    if (!(C.vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u)) {
+        tx_slow(f, len);
+        return;
+    }
+    const uint32_t tot = R.be16(16);
+    if (R.be16(12) != 0x0800u || 14 + tot > len || tot < 20) return;
+    const uint32_t hsum = R.le16(14) + R.le16(16) + R.le16(18) + R.le16(20) + R.le16(22) + R.le16(26) + R.le16(28) +
+                          R.le16(30) + R.le16(32);
+    store_be16(f + 24, csum_from_residue(be_residue(hsum)));
+    const uint32_t proto = R.b8(23), seg = tot - 20;
+    const bool tcp = proto == 6u;
+    if (tcp) {
+        const uint32_t doff = (R.b8(46) >> 4) * 4u;
+        if (seg < 20 || doff < 20 || doff > seg) return;
+    } else if (proto != 17u || seg < 8) {
+        return;
+    }
+    bool resum = false;
+    const uint32_t s = seg_sum_fast(C, W, lane, f, (int)(14 + tot), resum) - (tcp ? R.le16(50) : R.le16(40));
+    const uint32_t src = R.u32(26), dst = R.u32(30);
+    const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) + bswap16(dst >> 16) +
+                            proto + seg;
+    store_be16(f + (tcp ? 50 : 40), csum_from_residue(mod_ffff(be_residue(s) + pseudo)));
+}
+
+// Persistent, same schedule as dk_rx_kernel.
+__global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P) {
+    __shared__ WaveLds s_wave[kWaves];
+    const uint32_t lane = lane_id();
+    const uint32_t wv = threadIdx.x >> 6;
+    const WaveRange r = wave_range(P.sched, P.n, wv);
+    uint32_t noff = 0, nlen = 0;
+    if (r.f0 + lane < r.f1) {
+        noff = P.off[r.f0 + lane];
+        nlen = P.len[r.f0 + lane];
+    }
+    for (uint32_t c = r.f0; c < r.f1; c += r.step) {
+        const uint32_t i = c + lane;
+        const uint32_t off = noff, len = nlen;
+        if (i + r.step < r.f1) {
+            noff = P.off[i + r.step];
+            nlen = P.len[i + r.step];
+        }
+        tx_tile(P, i < r.f1, lane, s_wave[wv], off, len);
+    }
 }
 
 }  // namespace
@@ -685,11 +902,14 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     return 0;
 }
 
-int dk_launch_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
-                          uint32_t n, void* stream) {
-    if (n == 0) return 0;
-    const uint32_t grid = (n + dk::kBlock - 1) / dk::kBlock;
-    hipLaunchKernelGGL(dk::dk_tx_checksum_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, frames,
-                       frames_bytes, off, len, n);
+int dk_tx_resident_blocks() {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_tx_kernel, dk::kBlock, 0) != hipSuccess) return 0;
+    return blocks;
+}
+
+int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream) {
+    if (p.n == 0 || grid == 0) return 0;
+    hipLaunchKernelGGL(dk::dk_tx_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DK_RX_ABI_VERSION 1u
+#define DK_RX_ABI_VERSION 2u
 
 /* Frames whose offset is a multiple of this take the vectorised path; any other offset is still processed
  * (bit-exact), by a per-lane byte-load path. */
@@ -56,8 +56,9 @@ extern "C" {
 enum dk_verdict {
     DK_V_OK_TCP = 0,          /* delivered: socket.receive (tcp/peer.rs:254)                                  */
     DK_V_OK_UDP = 1,          /* delivered: socket.receive (udp/peer.rs:167)                                  */
-    DK_V_ARP = 2,             /* diverted to ARP peer (layer3/mod.rs:75-78)                                   */
-    DK_V_ICMP = 3,            /* diverted to ICMPv4 peer (layer3/mod.rs:109-112)                              */
+    DK_V_ARP = 2,             /* diverted to ARP peer (layer3/mod.rs:75-78); its PDU parses (arp/header.rs:80-111) */
+    DK_V_ICMP = 3,            /* diverted to ICMPv4 peer (layer3/mod.rs:109-112); header parses
+                                 (icmpv4/header.rs:47-66)                                                       */
     DK_V_IPV6 = 4,            /* dropped, IPv6 unsupported (layer3/mod.rs:116)                                */
     DK_V_ETH_SHORT = 5,       /* E1  len < 14 (ethernet2/header.rs:51-53)                        EBADMSG      */
     DK_V_ETH_TYPE = 6,        /* E2  unknown ethertype (ethernet2/protocol.rs:35-41)             ENOTSUP      */
@@ -88,7 +89,14 @@ enum dk_verdict {
     DK_V_UDP_CSUM = 31,       /* U3  checksum mismatch (:78-88)                                  EBADMSG      */
     DK_V_UDP_NOSOCK = 32,     /* no (local_ip,port) and no (0.0.0.0,port) (udp/peer.rs:147-165) dropped       */
     DK_V_BAD_DESC = 33,       /* descriptor outside the frame blob (this ABI, not the reference)  EINVAL       */
-    DK_V_COUNT = 34
+    /* Diverted frames whose control-plane parse fails. The reference hands these to the ARP /
+     * ICMPv4 peer, whose background loop drops them with a warning (arp/peer.rs:140-147, icmpv4/peer.rs:114-121). */
+    DK_V_ARP_SHORT = 34,      /* ARP PDU < 28 B (arp/header.rs:81-83)                            EBADMSG      */
+    DK_V_ARP_UNSUP = 35,      /* HTYPE/PTYPE/HLEN/PLEN/operation unsupported (:85-100, :161-166) ENOTSUP      */
+    DK_V_ICMP_SHORT = 36,     /* ICMPv4 message < 8 B (icmpv4/header.rs:48-50)                   EBADMSG      */
+    DK_V_ICMP_CSUM = 37,      /* ICMPv4 checksum mismatch (:55-57, protocols/mod.rs:47-71)       EBADMSG      */
+    DK_V_ICMP_TYPE = 38,      /* type byte not a known Icmpv4Type2 (icmpv4/protocol.rs:35-58)    EBADMSG      */
+    DK_V_COUNT = 39
 };
 
 /* ---------------------------------------------------------------------------------------------------------------
@@ -129,11 +137,18 @@ typedef struct dk_rx_batch {
 /* Per-frame results, struct-of-arrays, one element per frame. Required arrays: meta, src_ip, dst_ip, ports,
  * payload, flow_id. Optional (NULL = not written): tcp_seq, tcp_ack, tcp_win, flow_counts, verdict_counts.
  *
+ *  TCP / UDP (DK_V_OK_*, DK_V_*_NOSOCK):
  *  meta     = verdict | ip_protocol << 8 | tcp byte 13 (CWR..FIN) << 16 | tcp byte 12 (data offset, NS) << 24
  *  ports    = src_port | dst_port << 16
  *  payload  = payload_off | payload_len << 16     (payload_off counted from the frame start)
  *  tcp_win  = window | urgent_pointer << 16
- * Fields are filled for DK_V_OK_* and DK_V_*_NOSOCK; for every other verdict they are 0 (flow_id DK_FLOW_NONE).
+ *  ICMPv4 (DK_V_ICMP): meta = verdict | 1 << 8 | type << 16 | code << 24; src_ip / dst_ip from the IPv4 header;
+ *           ports = rest-of-header words: id | seq_num << 16 (echo request / reply); payload = the message after
+ *           the 8-byte header (what Icmpv4Header::parse_and_strip leaves).
+ *  ARP (DK_V_ARP): meta = verdict | operation << 16; src_ip = sender protocol address, dst_ip = target protocol
+ *           address; payload = 14 | (len - 14) << 16 (the buffer ArpPeer::receive takes). The sender / target
+ *           hardware addresses are frame bytes [22, 28) and [32, 38).
+ * For every other verdict the fields are 0 (flow_id DK_FLOW_NONE).
  * flow_counts[flow_id] and verdict_counts[verdict] are incremented (they accumulate across calls). */
 typedef struct dk_rx_results {
     uint32_t* meta;

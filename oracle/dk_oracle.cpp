@@ -322,6 +322,59 @@ int udp_parse_and_strip(uint32_t src_ipv4_addr, uint32_t dst_ipv4_addr, Buf& buf
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
+// Diverted control-plane frames: the parse the ARP / ICMPv4 peers run on what layer 3 hands
+// them (arp/peer.rs:140-147, icmpv4/peer.rs:114-121).
+// ---------------------------------------------------------------------------------------------------------------------
+// protocols/mod.rs:47-64 compute_generic_checksum: BE words, odd tail [b, 0], state seeded with 0xFFFF unless given.
+uint32_t compute_generic_checksum(const uint8_t* buf, size_t len, const uint32_t* start) {
+    uint32_t state = start ? *start : 0xFFFF;
+    size_t i = 0;
+    for (; i + 2 <= len; i += 2) state += be16(buf + i);
+    if (i < len) state += (uint32_t)buf[i] << 8;
+    return state;
+}
+
+struct Icmpv4Header { uint8_t type, code; uint16_t id, seq; };
+
+// icmpv4/header.rs:47-66 parse_and_strip; Icmpv4Type2::parse (icmpv4/protocol.rs:35-58).
+int icmpv4_parse_and_strip(Buf& buf, Icmpv4Header* out) {
+    if (buf.len < 8) return DK_V_ICMP_SHORT;                            // :48-50
+    const uint8_t* hdr = buf.p;
+    // compute_checksum (:88-93): generic sum of the 8-byte header (checksum field included) then of the body
+    uint32_t state = compute_generic_checksum(hdr, 8, nullptr);
+    state = compute_generic_checksum(hdr + 8, buf.len - 8, &state);
+    if (fold16(state) != 0) return DK_V_ICMP_CSUM;                      // :55-57
+    switch (hdr[0]) {                                                   // protocol.rs:37-56
+        case 0: case 3: case 4: case 5: case 8: case 9: case 10: case 11: case 12: case 13: case 14: break;
+        default: return DK_V_ICMP_TYPE;                                 // "invalid type byte"
+    }
+    out->type = hdr[0];
+    out->code = hdr[1];
+    out->id = be16(hdr + 4);
+    out->seq = be16(hdr + 6);
+    buf.adjust(8);                                                      // :61
+    return -1;
+}
+
+struct ArpHeader { uint16_t op; uint32_t sender_ip, target_ip; };
+
+// arp/header.rs:80-111 parse_and_consume; ArpOperation::try_from (:161-166).
+int arp_parse_and_consume(const Buf& buf, ArpHeader* out) {
+    if (buf.len < 28) return DK_V_ARP_SHORT;                            // :81-83
+    const uint8_t* b = buf.p;
+    if (be16(b) != 1) return DK_V_ARP_UNSUP;                            // HTYPE Ethernet2 (:85-88)
+    if (be16(b + 2) != 0x0800) return DK_V_ARP_UNSUP;                   // PTYPE IPv4 (:89-92)
+    if (b[4] != 6) return DK_V_ARP_UNSUP;                               // HLEN (:93-96)
+    if (b[5] != 4) return DK_V_ARP_UNSUP;                               // PLEN (:97-100)
+    uint16_t op = be16(b + 6);
+    if (op != 1 && op != 2) return DK_V_ARP_UNSUP;                      // Request / Reply only (:161-166)
+    out->op = op;
+    out->sender_ip = octets_u32(b + 14);
+    out->target_ip = octets_u32(b + 24);
+    return -1;
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
 // Demux tables: HashMap<SocketId, SharedTcpSocket> (tcp/peer.rs) and HashMap<SocketAddrV4, SharedUdpSocket>
 // (udp/peer.rs:38). The hash function is irrelevant to results; lookup order is what matters.
 // ---------------------------------------------------------------------------------------------------------------------
@@ -364,14 +417,31 @@ void receive_one(const dko_peer& peer, const uint8_t* frame, size_t len, uint32_
     int v = eth_parse_and_strip(buf, &et);
     if (v >= 0) { *meta = (uint32_t)v; return; }
     // dst MAC mismatch is warn-only (layer2/mod.rs:69-75): no verdict.
-    if (et == ARP) { *meta = DK_V_ARP; return; }                   // layer3/mod.rs:75-78
+    if (et == ARP) {                                                // layer3/mod.rs:75-78 -> arp/peer.rs:140
+        ArpHeader ah;
+        v = arp_parse_and_consume(buf, &ah);
+        if (v >= 0) { *meta = (uint32_t)v; return; }
+        *meta = DK_V_ARP | (uint32_t)ah.op << 16;
+        *src = ah.sender_ip; *dst = ah.target_ip;
+        *payload = (uint32_t)buf.off | (uint32_t)buf.len << 16;
+        return;
+    }
     if (et == IPV6) { *meta = DK_V_IPV6; return; }                 // layer3/mod.rs:116
     Ipv4Header ip;
     v = ipv4_parse_and_strip(buf, &ip);
     if (v >= 0) { *meta = (uint32_t)v; return; }
     if (ip.dst != peer.local_ipv4 && !is_broadcast(ip.dst)) { *meta = DK_V_IP_DST; return; }   // :91-95
     if (is_broadcast(ip.src) || is_multicast(ip.src) || is_unspecified(ip.src)) { *meta = DK_V_IP_SRC; return; }
-    if (ip.protocol == 0x01) { *meta = DK_V_ICMP; return; }        // :109-112
+    if (ip.protocol == 0x01) {                                     // :109-112 -> icmpv4/peer.rs:114
+        Icmpv4Header ih;
+        v = icmpv4_parse_and_strip(buf, &ih);
+        if (v >= 0) { *meta = (uint32_t)v; return; }
+        *meta = DK_V_ICMP | 0x01u << 8 | (uint32_t)ih.type << 16 | (uint32_t)ih.code << 24;
+        *src = ip.src; *dst = ip.dst;
+        *ports = (uint32_t)ih.id | (uint32_t)ih.seq << 16;
+        *payload = (uint32_t)buf.off | (uint32_t)buf.len << 16;
+        return;
+    }
     if (ip.protocol == 0x06) {
         // TcpPeer::receive (tcp/peer.rs:220-255): parse_and_strip(&src_ipv4_addr, &self.local_ipv4_addr, ...)
         TcpHeader th;

@@ -14,6 +14,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libdk_oracle.so")
 
+DK_V_COUNT = 39  # enum dk_verdict in include/dk_rx.h (tests/test_oracle.py checks it)
 FLOW_DTYPE = np.dtype([("kind", "<u4"), ("local_ip", "<u4"), ("remote_ip", "<u4"),
                        ("local_port", "<u2"), ("remote_port", "<u2")])
 
@@ -95,7 +96,7 @@ class OraclePeer:
         out = {k: np.zeros(n, np.uint32) for k in
                ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win")}
         out["flow_counts"] = np.zeros(max(self.nflows, 1), np.uint64)
-        out["verdict_counts"] = np.zeros(34, np.uint64)
+        out["verdict_counts"] = np.zeros(DK_V_COUNT, np.uint64)
         fb = blob.nbytes if frames_bytes is None else frames_bytes
         self._L.dko_process(self._p, blob.ctypes.data if blob.size else None, fb, off.ctypes.data,
                             lens.ctypes.data, n,

@@ -109,6 +109,27 @@ def udp_frame(payload=b"", src=ALICE_IPV4, dst=BOB_IPV4, sport=40000, dport=5000
     return frame(seg, 17, src, dst, pad=pad, **ip_kw)
 
 
+def icmp_message(type_=8, code=0, ident=0x1234, seq=1, payload=b"", checksum=None) -> bytes:
+    """Icmpv4Header::serialize_and_attach (icmpv4/header.rs:71-84): type, code, checksum, rest-of-header (id, seq)."""
+    m = bytes([type_, code, 0, 0]) + struct.pack("!HH", ident, seq) + payload
+    if checksum is None:
+        checksum = rfc1071(m)
+    return m[:2] + struct.pack("!H", checksum) + m[4:]
+
+
+def icmp_frame(type_=8, code=0, ident=0x1234, seq=1, payload=b"", checksum=None, src=ALICE_IPV4, dst=BOB_IPV4,
+               **kw) -> bytes:
+    return frame(icmp_message(type_, code, ident, seq, payload, checksum), 1, src, dst, **kw)
+
+
+def arp_frame(op=1, sha=ALICE_MAC, spa=ALICE_IPV4, tha=(0,) * 6, tpa=BOB_IPV4, htype=1, ptype=0x0800, hlen=6, plen=4,
+              pad=0) -> bytes:
+    """ArpHeader::create_and_serialize (arp/header.rs:117-135) behind an Ethernet header, as build_arp_query
+    (arp/tests.rs:199-213) builds a query."""
+    pdu = struct.pack("!HHBBH", htype, ptype, hlen, plen, op) + bytes(sha) + ip_bytes(spa) + bytes(tha) + ip_bytes(tpa)
+    return eth_header(0x0806, dst=(0xFF,) * 6) + pdu + b"\0" * pad
+
+
 def pack(frames: list[bytes], align: int = 64, misalign: list[int] | None = None):
     """Pack frames into a blob with aligned slots (+ optional per-frame misalignment). Returns numpy arrays."""
     import numpy as np
@@ -178,7 +199,18 @@ def verdict_corpus(seed: int = 7):
     add("eth_short", eth_header()[:13], "ETH_SHORT")
     add("eth_empty", b"", "ETH_SHORT")
     add("eth_type", eth_header(0x1234) + bytes(40), "ETH_TYPE")
-    add("arp", eth_header(0x0806) + bytes(28), "ARP")
+    add("arp_zero_pdu", eth_header(0x0806) + bytes(28), "ARP_UNSUP")
+    add("arp_request", arp_frame(), "ARP")
+    add("arp_reply", arp_frame(op=2, sha=BOB_MAC, spa=BOB_IPV4, tha=ALICE_MAC, tpa=ALICE_IPV4), "ARP")
+    add("arp_padded", arp_frame(pad=18), "ARP")
+    add("arp_short", arp_frame()[:14 + 27], "ARP_SHORT")
+    add("arp_empty", eth_header(0x0806), "ARP_SHORT")
+    add("arp_htype", arp_frame(htype=6), "ARP_UNSUP")
+    add("arp_ptype", arp_frame(ptype=0x86DD), "ARP_UNSUP")
+    add("arp_hlen", arp_frame(hlen=8), "ARP_UNSUP")
+    add("arp_plen", arp_frame(plen=16), "ARP_UNSUP")
+    add("arp_op", arp_frame(op=3), "ARP_UNSUP")
+    add("arp_op0", arp_frame(op=0), "ARP_UNSUP")
     add("ipv6", eth_header(0x86DD) + bytes(40), "IPV6")
     add("ip_short", eth_header() + bytes(19), "IP_SHORT")
     add("ip_version", frame(tcp_segment(), version=6), "IP_VERSION")
@@ -197,7 +229,22 @@ def verdict_corpus(seed: int = 7):
     add("ip_src_bcast", tcp_frame(pl, src="255.255.255.255"), "IP_SRC")
     add("ip_src_mcast", tcp_frame(pl, src="224.0.0.1"), "IP_SRC")
     add("ip_src_zero", tcp_frame(pl, src="0.0.0.0"), "IP_SRC")
-    add("icmp", frame(bytes([8, 0, 0, 0]) + bytes(4), proto=1), "ICMP")
+    add("icmp_zero_csum", frame(bytes([8, 0, 0, 0]) + bytes(4), proto=1), "ICMP_CSUM")
+    add("icmp_echo_request", icmp_frame(payload=pl[:56]), "ICMP")
+    add("icmp_echo_reply", icmp_frame(0, ident=7, seq=65535, payload=pl[:56]), "ICMP")
+    add("icmp_dest_unreach", icmp_frame(3, code=1, ident=0, seq=0, payload=pl[:28]), "ICMP")
+    add("icmp_odd_payload", icmp_frame(payload=pl[:33]), "ICMP")
+    add("icmp_header_only", icmp_frame(13), "ICMP")
+    add("icmp_big", icmp_frame(payload=pl * 10), "ICMP")
+    add("icmp_eth_pad", icmp_frame(payload=pl[:4], pad=10), "ICMP")
+    add("icmp_ip_options", icmp_frame(payload=pl[:20], ip_options=bytes([1, 1, 1, 0])), "ICMP")
+    add("icmp_short", frame(icmp_message()[:7], proto=1), "ICMP_SHORT")
+    add("icmp_empty", frame(b"", proto=1), "ICMP_SHORT")
+    add("icmp_csum", icmp_frame(payload=pl[:56], checksum=0x1111), "ICMP_CSUM")
+    add("icmp_type_6", icmp_frame(6), "ICMP_TYPE")
+    add("icmp_type_15", icmp_frame(15, payload=pl[:9]), "ICMP_TYPE")
+    add("icmp_type_255", icmp_frame(255), "ICMP_TYPE")
+    add("icmp_dst_not_local", icmp_frame(dst="192.168.1.3"), "IP_DST")
     add("ip_options_ok", tcp_frame(pl, ip_options=bytes([1, 1, 1, 0])), "OK_TCP")
     f = bytearray(tcp_frame(pl, ip_options=bytes([1, 1, 1, 0])))
     f[34:38] = bytes([7, 7, 7, 7])  # IPv4 options are not checksummed (ipv4/header.rs:289-296, quirk 1)

@@ -64,7 +64,7 @@ def test_struct_layout_matches_ctypes(tmp_path):
 
 def test_verdict_tables():
     lib = N.load_library()
-    assert lib.dk_rx_abi_version() == 1
+    assert lib.dk_rx_abi_version() == 2
     for i, name in enumerate(N.VERDICTS):
         assert lib.dk_rx_verdict_name(i).decode() == name
     assert lib.dk_rx_verdict_name(N.DK_V_COUNT).decode() == "UNKNOWN"
@@ -72,9 +72,10 @@ def test_verdict_tables():
     expect = {name: 0 for name in N.VERDICTS}
     for name in ("ETH_SHORT", "IP_SHORT", "IP_IHL_SMALL", "IP_HDR_TRUNC", "IP_TOTLEN_SMALL", "IP_TOTLEN_BIG",
                  "IP_EVIL", "IP_TTL", "IP_CSUM_FFFF", "IP_CSUM", "TCP_SHORT", "TCP_DOFF_TRUNC", "TCP_DOFF_SMALL",
-                 "TCP_CSUM", "TCP_OPT", "UDP_SHORT", "UDP_LEN", "UDP_CSUM"):
+                 "TCP_CSUM", "TCP_OPT", "UDP_SHORT", "UDP_LEN", "UDP_CSUM", "ARP_SHORT", "ICMP_SHORT", "ICMP_CSUM",
+                 "ICMP_TYPE"):
         expect[name] = EBADMSG
-    for name in ("ETH_TYPE", "IP_VERSION", "IP_MF", "IP_FRAGOFF", "IP_PROTO"):
+    for name in ("ETH_TYPE", "IP_VERSION", "IP_MF", "IP_FRAGOFF", "IP_PROTO", "ARP_UNSUP"):
         expect[name] = ENOTSUP
     expect["TCP_OPT_EIO"] = EIO
     expect["BAD_DESC"] = EINVAL

@@ -173,28 +173,81 @@ def test_duplicate_and_large_flow_tables(torch_cuda):
     assert (got["flow_id"][tr.flow < 5000] >= len(flows)).all()
 
 
-def test_tx_checksum_matches_oracle(torch_cuda):
+def tx_check(blob, off, lens, ctx=""):
+    """dk_tx_checksum on the GPU vs the oracle's serialize_and_attach restatement, frame by frame, whole blob."""
     import torch
 
+    from oracle import oracle as O
+
+    blob = blob.copy()
+    rng = np.random.default_rng(len(off))
+    for o, L in zip(off, lens):  # scramble the checksum fields so a skipped write cannot pass
+        if L >= 34:
+            S = 14 + (blob[o + 14] & 15) * 4
+            for k in (24, 25, S + 6, S + 7, S + 16, S + 17):
+                if k < L:
+                    blob[o + k] = rng.integers(0, 256)
+    eng = RxEngine(Config(LOCAL))
+    b = FrameBatch.from_numpy(blob, off, lens)
+    eng.tx_checksum(b)
+    torch.cuda.synchronize()
+    got = b.blob.cpu().numpy()
+    exp = blob.copy()
+    for o, L in zip(off, lens):
+        fr = bytearray(exp[o:o + L].tobytes())
+        O.tx_fill_checksums(fr)
+        exp[o:o + L] = np.frombuffer(bytes(fr), np.uint8)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{ctx}: {bad.size} bytes differ, first at blob offset {bad[:8]}"
+
+
+def test_tx_checksum_matches_oracle(torch_cuda):
     flows = synth.make_flows(64)
     n = 5000
     tr = synth.traffic(n, np.random.default_rng(8).integers(28, 3000, n).astype(np.uint16), flows)
     blob, off, lens = synth.build_numpy(tr, checksums=False)
     frames = [blob[o:o + L].tobytes() for o, L in zip(off, lens)]
     blob2, off2, lens2 = F.pack(frames, misalign=[0, 2, 1, 0])
-    eng = RxEngine(Config(LOCAL))
-    b = FrameBatch.from_numpy(blob2, off2, lens2)
-    eng.tx_checksum(b)
-    torch.cuda.synchronize()
-    got = b.blob.cpu().numpy()
-    from oracle import oracle as O
+    tx_check(blob2, off2, lens2, "random lengths")
 
-    exp = blob2.copy()
-    for o, L in zip(off2, lens2):
-        fr = bytearray(exp[o:o + L].tobytes())
-        O.tx_fill_checksums(fr)
-        exp[o:o + L] = np.frombuffer(bytes(fr), np.uint8)
-    assert np.array_equal(got, exp)
+
+def test_tx_checksum_malformed_and_options(torch_cuda):
+    """Every corpus / fuzz / option frame (non-IPv4, bad lengths, bad data offsets, IHL > 5, short UDP): the TX fill
+    touches exactly what serialize_and_attach's restatement touches, at every alignment class."""
+    rng = np.random.default_rng(77)
+    base = [c[1] for c in F.verdict_corpus()]
+    pl = bytes(range(200))
+    for ihl_opts in (b"", bytes([1, 1, 1, 0]), bytes(40)):
+        for opts, _ in F.tcp_opt_cases():
+            base.append(F.tcp_frame(pl[: len(base) % 150], options=opts, ip_options=ihl_opts))
+    frames = list(base)
+    for k in range(3000):
+        f = bytearray(base[k % len(base)])
+        for _ in range(rng.integers(1, 4)):
+            if len(f):
+                p = int(rng.integers(0, min(len(f), 60)))
+                f[p] = int(rng.integers(0, 256))
+        frames.append(bytes(f))
+    for misalign in (None, [0, 2, 4, 6], [1, 3]):
+        blob, off, lens = F.pack(frames, misalign=misalign)
+        tx_check(blob, off, lens, f"malformed misalign={misalign}")
+
+
+def test_tx_checksum_large_frames_schedule(torch_cuda):
+    """>= 1 KiB per frame (contiguous-share schedule, quarter-wave streams): TCP and UDP up to jumbo sizes, odd
+    lengths, and Ethernet padding far beyond total_length (segment re-summed from memory)."""
+    rng = np.random.default_rng(5)
+    frames = []
+    for k in range(12000):
+        size = int(rng.integers(1000, 9000)) if k % 5 else 1446
+        pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        pad = int(rng.integers(40, 700)) if k % 17 == 0 else 0
+        if k % 3 == 0:
+            frames.append(F.udp_frame(pay[: size - 200], pad=pad))
+        else:
+            frames.append(F.tcp_frame(pay, pad=pad))
+    blob, off, lens = F.pack(frames)
+    tx_check(blob, off, lens, "large")
 
 
 def test_host_pipeline_matches_device_path(torch_cuda):

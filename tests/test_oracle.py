@@ -229,3 +229,28 @@ def test_sanitized_build(tmp_path):
     p = O.OraclePeer(ipv4(BOB_IPV4))
     p.set_flows(flows)
     assert np.array_equal(meta, p.process(blob, off, lens)["meta"])
+
+
+def test_control_plane_fields():
+    """ARP / ICMPv4 result records, expectations derived by hand from the builders: ICMP type /
+    code / rest-of-header words and the stripped message window; ARP operation and protocol addresses."""
+    from demikernel_amd import _native as N
+
+    assert O.DK_V_COUNT == N.DK_V_COUNT
+    pl = bytes(range(40))
+    frames = [F.icmp_frame(0, code=0, ident=0xBEEF, seq=0x0102, payload=pl, pad=6),
+              F.icmp_frame(3, code=4, ident=0, seq=0, payload=pl[:5], ip_options=bytes(8)),
+              F.arp_frame(op=2, sha=F.BOB_MAC, spa=F.BOB_IPV4, tha=F.ALICE_MAC, tpa=F.ALICE_IPV4, pad=18)]
+    blob, off, lens = F.pack(frames)
+    p = O.OraclePeer(ipv4(BOB_IPV4))
+    r = p.process(blob, off, lens)
+    m = r["meta"]
+    assert VERDICTS[m[0] & 0xFF] == "ICMP" and (m[0] >> 8) & 0xFF == 1 and (m[0] >> 16) & 0xFF == 0
+    assert r["ports"][0] == 0xBEEF | 0x0102 << 16
+    assert r["payload"][0] == (34 + 8) | len(pl) << 16  # Ethernet padding trimmed by the IPv4 parse
+    assert r["src_ip"][0] == ipv4(F.ALICE_IPV4) and r["dst_ip"][0] == ipv4(BOB_IPV4)
+    assert VERDICTS[m[1] & 0xFF] == "ICMP" and (m[1] >> 16) & 0xFF == 3 and m[1] >> 24 == 4
+    assert r["payload"][1] == (34 + 8 + 8) | 5 << 16
+    assert VERDICTS[m[2] & 0xFF] == "ARP" and (m[2] >> 8) & 0xFF == 0 and m[2] >> 16 == 2
+    assert r["src_ip"][2] == ipv4(BOB_IPV4) and r["dst_ip"][2] == ipv4(F.ALICE_IPV4)
+    assert r["payload"][2] == 14 | (28 + 18) << 16 and r["flow_id"][2] == 0xFFFFFFFF
