@@ -11,6 +11,7 @@ per-flow packet counts (the only collective on this path). Weak scaling: every r
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -80,7 +81,7 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allr
             return None
         return dist.all_reduce(buf, async_op=async_op)
 
-    def step(k, ev=None):
+    def step(k):
         b = batches[k % len(batches)]
         if counts_allreduce:
             slot = k % 2
@@ -89,11 +90,7 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allr
                 pending[slot] = None
             bufs[slot].zero_()
             res.t["flow_counts"] = bufs[slot]
-        if ev:
-            ev[0].record(stream)
         eng.receive_batch(b, res, stream=stream)
-        if ev:
-            ev[1].record(stream)
         if counts_allreduce:
             pending[k % 2] = reduce(bufs[k % 2], True)
 
@@ -110,17 +107,22 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allr
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(steps)]
+    # HIP events bracket the timed region only (an event pair around every launch adds a marker + cache writeback per
+    # step and perturbs the kernel it measures): per-launch time = region / steps, i.e. dk_rx_kernel plus the small
+    # dk_flow_reduce_kernel and launch gaps (rocprofv3 kernel stats in profiles/ split the two kernels).
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
     for k in range(steps):
-        step(k, ev[k])
+        step(k)
+    e1.record(stream)
     drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern = [a.elapsed_time(b) / 1e3 for a, b in ev]
+    kern = [e0.elapsed_time(e1) / 1e3 / steps]
     coll = []
     if counts_allreduce:  # the collective alone, unoverlapped, for the report
         for _ in range(5):
@@ -199,6 +201,39 @@ def tx_rate(eng, batch, frame_bytes, stream, iters=20):
     return {"gbps": round(frame_bytes / t / 1e9, 1), "kernel_ms_avg": round(t * 1e3, 4),
             "roofline_achieved_gbps": round(algo / t / 1e9, 1), "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_launch": algo}
+
+
+def read_ceiling(batch, stream, iters=10):
+    """On-box streaming-read ceiling: dk_diag_read_probe over the same frame blob, register loads
+    (mode 3) and LDS-DMA (mode 4), 4 and 8 waves per CU; best GB/s and the configuration that reached it."""
+    import torch
+
+    from demikernel_amd import _native as N
+
+    lib = N.load_library()
+    nbytes = batch.blob.numel() // 16 * 16
+    cus = torch.cuda.get_device_properties(batch.blob.device).multi_processor_count
+    best = (0.0, "")
+    for mode in (3, 4):
+        for per_cu in (4, 8):
+            grid = per_cu * cus // 4  # 256-thread workgroups: 4 waves each
+            scratch = torch.zeros(grid, dtype=torch.int32, device=batch.blob.device)
+            call = lambda: lib.dk_diag_read_probe(ctypes.c_void_p(batch.blob.data_ptr()), nbytes,  # noqa: E731
+                                                  ctypes.c_void_p(scratch.data_ptr()), grid, mode,
+                                                  ctypes.c_void_p(stream.cuda_stream))
+            for _ in range(3):
+                call()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                call()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            gbs = nbytes / (e0.elapsed_time(e1) / 1e3 / iters) / 1e9
+            if gbs > best[0]:
+                best = (gbs, f"dk_diag_read_probe mode {mode} ({'LDS-DMA' if mode == 4 else 'register'} loads), "
+                             f"{per_cu} waves/CU, {nbytes / 1e9:.2f} GB")
+    return best
 
 
 def load_traffic_profile(workload):
@@ -299,6 +334,10 @@ def main():
                      "kernel_ms_avg": round(kern_avg * 1e3, 4),
                      "algorithmic_bytes_per_launch": algo},
     }
+    if not args.no_extras:
+        ceil_gbs, ceil_cfg = read_ceiling(batch, stream)
+        out["roofline"]["measured_read_ceiling"] = {"value": round(ceil_gbs, 1), "unit": "GB/s", "probe": ceil_cfg,
+                                                    "frac": round(achieved / ceil_gbs, 4)}
     if coll:
         out["collective_ms_avg"] = round(float(np.mean(coll)) * 1e3, 4)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -329,6 +368,7 @@ def main():
         out["host_path"] = host_path_rate(eng, batch, flows, args.host_frames)
         # TX checksum fill (dk_tx_checksum) over the same batch (rewrites its checksum fields)
         out["tx_checksum"] = tx_rate(eng, batch, frame_bytes, stream)
+        out["tx_checksum"]["traffic"] = load_traffic_profile(name + "_tx")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

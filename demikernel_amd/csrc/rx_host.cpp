@@ -444,7 +444,8 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
         dev_cached = dev;
     }
     dk::TxParams p{frames, frames_bytes, off, len, n, frames_bytes / n >= 1024 ? 1u : 0u};
-    const uint32_t per_cu = std::min<uint32_t>(occ, p.sched ? 3u : 4u);
+    uint32_t per_cu = std::min<uint32_t>(occ, p.sched ? 3u : 4u);
+    if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);  // tuning
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
     return dk_launch_tx(p, grid, stream);
 }

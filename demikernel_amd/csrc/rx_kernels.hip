@@ -784,8 +784,32 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
 // consistent total_length are left untouched; TCP with a bad data offset / UDP shorter than 8 keep only the IPv4 fill
 // (oracle dko_tx_fill_checksums). Frames must not overlap.
 // ---------------------------------------------------------------------------------------------------------------------
+#ifndef DK_TX_STORE
+#define DK_TX_STORE 0  // 0: 16-bit stores; 1: nontemporal 16-bit; 2: the 16-byte block holding the field; 3: bytes [0, 64)
+#endif
 __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {  // p is 2-byte aligned on the fast path
+#if DK_TX_STORE == 1
+    __builtin_nontemporal_store((uint16_t)bswap16(v), reinterpret_cast<uint16_t*>(p));
+#else
     *reinterpret_cast<uint16_t*>(p) = (uint16_t)bswap16(v);
+#endif
+}
+// Fast-path field write at frame byte k (k even, k < 64, 16-byte aligned frame): DK_TX_STORE 2 rewrites the whole
+// 16-byte block from the register window when the block lies inside the frame (a full-block write needs no
+// read-modify-write below L2), else a 16-bit store.
+template <int k>
+__device__ __forceinline__ void store_field(uint8_t* f, const RegAcc& R, uint32_t len, uint32_t v) {
+#if DK_TX_STORE == 2
+    constexpr int b = k / 16;
+    if ((uint32_t)(16 * b + 16) <= len) {
+        uint32_t d[4] = {R.w[4 * b], R.w[4 * b + 1], R.w[4 * b + 2], R.w[4 * b + 3]};
+        constexpr int j = (k / 4) % 4;
+        d[j] = (k & 2) ? (d[j] & 0xFFFFu) | (bswap16(v) << 16) : (d[j] & 0xFFFF0000u) | bswap16(v);
+        *reinterpret_cast<uint4*>(f + 16 * b) = make_uint4(d[0], d[1], d[2], d[3]);
+        return;
+    }
+#endif
+    store_be16(f + k, v);
 }
 
 // Byte path (misaligned frames, IHL != 5): lane per frame.
@@ -839,21 +863,39 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
     if (R.be16(12) != 0x0800u || 14 + tot > len || tot < 20) return;
     const uint32_t hsum = R.le16(14) + R.le16(16) + R.le16(18) + R.le16(20) + R.le16(22) + R.le16(26) + R.le16(28) +
                           R.le16(30) + R.le16(32);
-    store_be16(f + 24, csum_from_residue(be_residue(hsum)));
+    const uint32_t ipc = csum_from_residue(be_residue(hsum));
     const uint32_t proto = R.b8(23), seg = tot - 20;
     const bool tcp = proto == 6u;
-    if (tcp) {
-        const uint32_t doff = (R.b8(46) >> 4) * 4u;
-        if (seg < 20 || doff < 20 || doff > seg) return;
-    } else if (proto != 17u || seg < 8) {
+    const uint32_t doff = (R.b8(46) >> 4) * 4u;
+    const bool l4 = tcp ? (seg >= 20 && doff >= 20 && doff <= seg) : (proto == 17u && seg >= 8);
+    uint32_t c = 0;
+    if (l4) {
+        bool resum = false;
+        const uint32_t s = seg_sum_fast(C, W, lane, f, (int)(14 + tot), resum) - (tcp ? R.le16(50) : R.le16(40));
+        const uint32_t src = R.u32(26), dst = R.u32(30);
+        const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) +
+                                bswap16(dst >> 16) + proto + seg;
+        c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
+    }
+#if DK_TX_STORE == 3
+    if (len >= 64) {  // rewrite the whole 64-byte header window: full-line writes, no partial-write merge below L2
+        uint32_t d[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k] = R.w[k];
+        d[6] = (d[6] & 0xFFFF0000u) | bswap16(ipc);
+        if (l4 && tcp) d[12] = (d[12] & 0xFFFFu) | (bswap16(c) << 16);
+        if (l4 && !tcp) d[10] = (d[10] & 0xFFFF0000u) | bswap16(c);
+        uint4* q = reinterpret_cast<uint4*>(f);
+#pragma unroll
+        for (int k = 0; k < 4; k++) q[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
         return;
     }
-    bool resum = false;
-    const uint32_t s = seg_sum_fast(C, W, lane, f, (int)(14 + tot), resum) - (tcp ? R.le16(50) : R.le16(40));
-    const uint32_t src = R.u32(26), dst = R.u32(30);
-    const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) + bswap16(dst >> 16) +
-                            proto + seg;
-    store_be16(f + (tcp ? 50 : 40), csum_from_residue(mod_ffff(be_residue(s) + pseudo)));
+#endif
+    store_field<24>(f, R, len, ipc);
+    if (l4) {
+        if (tcp) store_field<50>(f, R, len, c);
+        else store_field<40>(f, R, len, c);
+    }
 }
 
 // Persistent, same schedule as dk_rx_kernel.

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--grids", default="2,3,4")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
     args = ap.parse_args()
     import torch
 
@@ -44,16 +45,17 @@ def main():
         for g in grids:
             os.environ["DK_RX_GRID_PER_CU"] = str(g)
             for k, (e, r) in engines.items():
-                e.receive_batch(batch, r)
+                run = (lambda: e.tx_checksum(batch)) if args.tx else (lambda: e.receive_batch(batch, r))  # noqa: E731
+                run()
                 ev0.record()
                 for _ in range(args.iters):
-                    e.receive_batch(batch, r)
+                    run()
                 ev1.record()
                 torch.cuda.synchronize()
                 times[(k, g)].append(ev0.elapsed_time(ev1) / args.iters)
     for (k, g), ts in sorted(times.items(), key=lambda x: (x[0][1], x[0][0])):
         ms = float(np.median(ts))
-        print(json.dumps({"variant": k, "grid_per_cu": g, "workload": args.workload, "ms": round(ms, 4),
+        print(json.dumps({"variant": k, "grid_per_cu": g, "workload": args.workload, "tx": args.tx, "ms": round(ms, 4),
                           "algo_GBps": round(algo / ms / 1e6, 1), "spread": round((max(ts) - min(ts)) / ms, 3)}))
 
 

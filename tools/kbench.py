@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--probe", action="store_true")
     ap.add_argument("--probe-one", action="store_true", help="one probe config (mode 1, grid 1024): PMC calibration")
     ap.add_argument("--no-rx", action="store_true")
+    ap.add_argument("--tx", action="store_true", help="also time dk_tx_checksum (rewrites the batch's checksums)")
     ap.add_argument("--no-counts", action="store_true", help="pass NULL flow/verdict counters (cost attribution)")
     args = ap.parse_args()
 
@@ -62,6 +63,12 @@ def main():
                           "ms": round(t * 1e3, 4),
                           "frame_GBps": round(fb / t / 1e9, 1), "algo_GBps": round(algo / t / 1e9, 1),
                           "mpkt_s": round(batch.n / t / 1e6, 1)}), flush=True)
+    if args.tx:
+        t = time_events(lambda: eng.tx_checksum(batch), args.iters)
+        algo = fb + batch.n * (bench.DESC_BYTES + 4)
+        print(json.dumps({"kernel": "dk_tx", "workload": args.workload, "frames": batch.n, "frame_bytes": fb,
+                          "algo_bytes": algo, "ms": round(t * 1e3, 4), "frame_GBps": round(fb / t / 1e9, 1),
+                          "algo_GBps": round(algo / t / 1e9, 1)}), flush=True)
     if args.probe or args.probe_one:
         lib = N.load_library()
         nbytes = batch.blob.numel() // 16 * 16

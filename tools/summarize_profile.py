@@ -30,7 +30,7 @@ def counters(path):
 
 
 def kbench_info(path):
-    rx, probe = None, None
+    rx, probe, tx = None, None, None
     for line in open(path):
         line = line.strip()
         if not line.startswith("{"):
@@ -40,7 +40,9 @@ def kbench_info(path):
             rx = d
         elif d.get("kernel") == "read_probe":
             probe = d
-    return rx, probe
+        elif d.get("kernel") == "dk_tx":
+            tx = d
+    return rx, probe, tx
 
 
 def main():
@@ -62,7 +64,7 @@ def main():
             continue
         fc = counters(os.path.join(fdir, "run_counter_collection.csv"))
         wc = counters(os.path.join(wdir, "run_counter_collection.csv"))
-        rx, probe = kbench_info(os.path.join(src, f"fetch_{wl}.log"))
+        rx, probe, tx = kbench_info(os.path.join(src, f"fetch_{wl}.log"))
         fk = {k[0]: v for k, v in fc.items() if k[1] == "FETCH_SIZE"}
         wk = {k[0]: v for k, v in wc.items() if k[1] == "WRITE_SIZE"}
         rxk = next(k for k in fk if "dk_rx_kernel" in k)
@@ -78,6 +80,15 @@ def main():
         rows.append([wl, "dk_rx_kernel", f"{fk[rxk]:.0f}", f"{wk.get(rxk, 0.0):.0f}", f"{factor:.4f}", f"{rd:.0f}",
                      f"{wr:.0f}", algo, f"{(rd + wr) / algo:.3f}"])
         rows.append([wl, "read_probe", f"{fk[pk]:.0f}", f"{wk.get(pk, 0.0):.0f}", "", probe["bytes"], "", "", ""])
+        txk = next((k for k in fk if "dk_tx_kernel" in k), None)
+        if tx and txk:
+            trd, twr = fk[txk] * 1024.0 * factor, wk.get(txk, 0.0) * 1024.0
+            traffic[wl + "_tx"] = {"hbm_bytes_per_launch": int(trd + twr), "hbm_read_bytes": int(trd),
+                                   "hbm_write_bytes": int(twr), "fetch_calibration_factor": round(factor, 4),
+                                   "algorithmic_bytes_per_launch": tx["algo_bytes"],
+                                   "source": f"profiles/{tag}_pmc.csv (dk_tx_kernel)"}
+            rows.append([wl, "dk_tx_kernel", f"{fk[txk]:.0f}", f"{wk.get(txk, 0.0):.0f}", f"{factor:.4f}",
+                         f"{trd:.0f}", f"{twr:.0f}", tx["algo_bytes"], f"{(trd + twr) / tx['algo_bytes']:.3f}"])
     with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as f:
         csv.writer(f).writerows(rows)
     json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
