@@ -785,7 +785,7 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
 // (oracle dko_tx_fill_checksums). Frames must not overlap.
 // ---------------------------------------------------------------------------------------------------------------------
 #ifndef DK_TX_STORE
-#define DK_TX_STORE 0  // 0: 16-bit stores; 1: nontemporal 16-bit; 2: the 16-byte block holding the field; 3: bytes [0, 64)
+#define DK_TX_STORE 3  // 0: 16-bit stores; 1: nontemporal 16-bit; 2: the 16-byte block holding the field; 3: bytes [0, 64)
 #endif
 __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {  // p is 2-byte aligned on the fast path
 #if DK_TX_STORE == 1
