@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libdk_rx.so")
 LIB_PATH = os.environ.get("DK_RX_LIB_VARIANT", LIB_PATH)
 
 DK_FLOW_NONE = 0xFFFFFFFF
+DK_RX_BATCH_ALIGNED16 = 1  # dk_rx_batch.flags
 DK_FLOW_TCP_ACTIVE, DK_FLOW_TCP_PASSIVE, DK_FLOW_UDP = 1, 2, 3
 
 # enum dk_verdict (include/dk_rx.h), SURVEY.md Appendix A.
@@ -48,7 +49,7 @@ class DkFlow(ctypes.Structure):
 
 class DkRxBatch(ctypes.Structure):
     _fields_ = [("frames", c_void_p), ("frames_bytes", c_uint64), ("off", c_void_p), ("len", c_void_p),
-                ("n", c_uint32), ("reserved", c_uint32)]
+                ("n", c_uint32), ("flags", c_uint32)]
 
 
 RESULT_FIELDS = ["meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win",

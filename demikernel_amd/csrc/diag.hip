@@ -64,6 +64,7 @@ __global__ __launch_bounds__(kBlock) void read_probe(const uint4* __restrict__ p
 // mode 3: register loads, 16 x 1 KiB per wave step in flight.
 // mode 4 / 5: LDS-DMA (global_load_lds_dwordx4), nontemporal / default policy, 16 x 1 KiB per wave step into a
 // per-wave 16 KiB LDS slot, read back with ds_read_b128 and summed.
+// mode 6 / 7: as mode 3 with buffer_load_dwordx4 (SGPR resource, 32-bit lane offsets), nontemporal / default.
 typedef __attribute__((address_space(3))) void lds_void;
 template <int kMode>
 __global__ __launch_bounds__(kBlock) void read_probe16(const uint4* __restrict__ p, uint64_t n16, uint32_t* out) {
@@ -82,6 +83,18 @@ __global__ __launch_bounds__(kBlock) void read_probe16(const uint4* __restrict__
             for (int u = 0; u < U; u++) {
                 const uint64_t i = base + u * 64 + lane;
                 v[u] = i < n16 ? ld(p + i, true) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
+        } else if (kMode >= 6) {
+            // buffer_load_dwordx4: SGPR resource + 32-bit per-lane offset (blob < 4 GiB), nt (6) / default (7)
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0xFFFFFFFF, 0x00020000);
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = min(base + u * 64 + lane, n16 - 1);
+                const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, kMode == 6 ? 2 : 0);
+                v[u] = make_uint4(r[0], r[1], r[2], r[3]);
             }
 #pragma unroll
             for (int u = 0; u < U; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
@@ -109,7 +122,8 @@ __global__ __launch_bounds__(kBlock) void read_probe16(const uint4* __restrict__
 
 extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode,
                                   void* stream) {
-    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 5) return 22;
+    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 7) return 22;
+    if (mode >= 6 && bytes > 0xFFFFFFFFull) return 22;  // buffer offsets are 32-bit
     const uint4* p = (const uint4*)buf;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == 0) hipLaunchKernelGGL(read_probe<0>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
@@ -118,5 +132,7 @@ extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scr
     if (mode == 3) hipLaunchKernelGGL(read_probe16<3>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 4) hipLaunchKernelGGL(read_probe16<4>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 5) hipLaunchKernelGGL(read_probe16<5>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 6) hipLaunchKernelGGL(read_probe16<6>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 7) hipLaunchKernelGGL(read_probe16<7>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

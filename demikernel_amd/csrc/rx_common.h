@@ -64,6 +64,7 @@ struct RxParams {
     uint32_t* flow_scratch;  // kFlowLds: [grid][flow_words]
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
     uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave
+    uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path
     dk_rx_results res;
 };
 

@@ -284,6 +284,7 @@ int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, vo
     p.off = b->off;
     p.len = b->len;
     p.n = b->n;
+    p.aligned16 = (b->flags & DK_RX_BATCH_ALIGNED16) ? 1u : 0u;
     p.res = *r;
     return launch_batch(c, p, c->scratch, stream);
 }
@@ -364,6 +365,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         p.off = st.desc_off;
         p.len = st.desc_len;
         p.n = m;
+        p.aligned16 = (b->flags & DK_RX_BATCH_ALIGNED16) ? 1u : 0u;  // the staging keeps every offset mod 16
         uint32_t* R = st.res;
         p.res.meta = R;
         p.res.src_ip = R + (size_t)st.cap;

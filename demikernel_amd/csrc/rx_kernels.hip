@@ -46,7 +46,7 @@ constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | 
 #define DK_NT_LOADS 1
 #endif
 #ifndef DK_MIN_WAVES
-#define DK_MIN_WAVES 1
+#define DK_MIN_WAVES 4  // waves per SIMD the register budget must admit (128 VGPRs)
 #endif
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
@@ -362,26 +362,45 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // Per-wave LDS used by one tile. Strides of 5 and 3 uint4 keep the owner-lane ds_read_b128 conflict-free.
 // One quarter-wave's frame in a phase-B step.
 struct CoopSlot {
-    const uint4* base;
+    uint32_t boff;  // byte offset of the frame's first granule in the blob
     uint32_t nb, j, acc;
     bool has;
 };
 
-#ifndef DK_LDSDMA
-#define DK_LDSDMA 0  // phase B via global_load_lds_dwordx4 (LDS-DMA) into per-wave slots instead of register loads
+#ifndef DK_BUFFER_LOADS
+#define DK_BUFFER_LOADS 1  // frame bytes by buffer_load_dwordx4 (SGPR resource + 32-bit lane offset) vs global_load
 #endif
-#ifndef DK_COMPACT_LDS
-#define DK_COMPACT_LDS DK_LDSDMA  // strides 4/2 (2-way conflicts on 6 reads per chunk) to leave LDS for DMA slots
+// Frame-blob granule loads. buffer_load_dwordx4 with the nontemporal policy streams ~12 % faster than
+// global_load_dwordx4 on gfx950 (dk_diag_read_probe modes 6 vs 3: 6.87 vs 6.09 TB/s on one box) and needs one offset
+// VGPR instead of a 64-bit address; the blob is < 4 GiB (dk_rx.h), so 32-bit offsets cover it.
+struct Blob {
+#if DK_BUFFER_LOADS
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ explicit Blob(const uint8_t* frames)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(frames), 0, 0xFFFFFFFF, 0x00020000)) {}
+    template <bool kNt>
+    __device__ __forceinline__ uint4 ld(uint32_t byte_off) const {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, kNt ? 2 : 0);
+        return make_uint4(r[0], r[1], r[2], r[3]);
+    }
+#else
+    const uint8_t* f;
+    __device__ __forceinline__ explicit Blob(const uint8_t* frames) : f(frames) {}
+    template <bool kNt>
+    __device__ __forceinline__ uint4 ld(uint32_t byte_off) const {
+        const uint4* p = reinterpret_cast<const uint4*>(f + byte_off);
+        return kNt ? ld_stream(p) : *p;
+    }
 #endif
-constexpr uint32_t kHdrStride = DK_COMPACT_LDS ? 4 : 5, kTailStride = DK_COMPACT_LDS ? 2 : 3;
+};
+
+// Strides of 5 and 3 uint4 keep the owner-lane ds_read_b128 conflict-free (compact 4/2 strides: DESIGN.md §8).
+constexpr uint32_t kHdrStride = 5, kTailStride = 3;
 struct WaveLds {
-    uint2 rec[64];         // phase B: per rank {owner lane | blocks << 8, frame offset}
+    uint2 rec[64];         // phase B: per rank {owner lane | blocks << 8, offset of the frame's 16-byte base}
     uint32_t csum[64];     // phase B: whole-frame LE-half sums by owner lane
-    uint4 hdr[64][kHdrStride];    // phase B -> C: bytes [0, 64) of each big frame
+    uint4 hdr[64][kHdrStride];    // phase B -> C: the first 5 blocks of each big frame (bytes [0, 64) + shift)
     uint4 tail[64][kTailStride];  // phase B -> C: the last two 16-byte blocks of each big frame
-#if DK_LDSDMA
-    uint4 dma[kRoundsPerStep][kCoopU][64];  // LDS-DMA landing slots: lane L's 16 bytes at [h][u][L]
-#endif
 };
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -393,30 +412,62 @@ typedef __attribute__((address_space(3))) void lds_void;
 //     16 lanes (kCoopU x dwordx4 in flight each): blocks summed with v_dot2_u32_u16, the header window and the last
 //     32 bytes deposited in LDS for the owner lane, the quarter's sum reduced by a DPP row scan. Reading each frame in
 //     one contiguous pass keeps DRAM rows open (a separate 64-byte header read per frame cost 8 %).
-// On return the owner lane holds bytes [0, 64) in C.R and, for big frames, the whole-frame sum in C.fsum and the last
-// two blocks in W.tail[lane].
+// Any even frame address takes this vector path: blocks are the 16-byte granules from a = f - sh (sh = f mod 16, even,
+// so the frame's 16-bit word grid is the granules' grid), loaded whole (a granule never crosses a page, so reading
+// its bytes outside the frame cannot fault; they are masked or subtracted out of every sum). Odd addresses take the
+// byte path.
+// On return the owner lane holds frame bytes [0, 64) in C.R (realigned when sh != 0) and, for big frames, the LE-half
+// sum of frame bytes [0, 16 * nblk - sh) in C.fsum and the last two granules in W.tail[lane].
 struct Chunk {
-    RegAcc R;       // frame bytes [0, 64) (zero beyond the frame for small frames)
-    uint32_t fsum;  // big frames: LE-half sum over blocks [0, nblk)
-    uint32_t nblk;  // big frames: 16-byte blocks covering the frame
-    bool inb, vec, big;  // descriptor in bounds; 16-byte aligned (vector path); streamed by a quarter-wave
+    RegAcc R;       // frame bytes [0, 64) (bytes past the frame end are not defined)
+    uint32_t fsum;  // big frames: LE-half sum from the frame start to the end of the last granule
+    uint32_t nblk;  // big frames: 16-byte granules covering [a, f + len)
+    uint32_t sh;    // f - a, even
+    bool inb, vec, big;  // descriptor in bounds; even address (vector path); streamed by a quarter-wave
 };
+
+// R.w <- bytes [sh, sh + 64) of the 80 bytes {w[0..15], x[0..3]}, sh even: two dword-shift stages (8, 4 bytes) as
+// masked blends, then a 2-byte funnel shift. Written as bit blends so the compiler keeps the 20 words in registers
+// (a ternary between array elements became a dynamically indexed scratch array).
+__device__ __forceinline__ void realign(uint32_t (&w)[16], const uint32_t (&x)[4], uint32_t sh) {
+    uint32_t u[20];
+#pragma unroll
+    for (int k = 0; k < 16; k++) u[k] = w[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) u[16 + k] = x[k];
+    const uint32_t m8 = 0u - ((sh >> 3) & 1u), m4 = 0u - ((sh >> 2) & 1u);
+#pragma unroll
+    for (int k = 0; k < 18; k++) u[k] = (u[k + 2] & m8) | (u[k] & ~m8);
+#pragma unroll
+    for (int k = 0; k < 17; k++) u[k] = (u[k + 1] & m4) | (u[k] & ~m4);
+    const uint32_t b = sh & 2u;  // funnel-shift byte count: 0 or 2
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = __builtin_amdgcn_alignbyte(u[k + 1], u[k], b);
+}
+
+// kShift = false: only 16-byte aligned frames take the vector path (others the byte path); the receive kernel's
+// instantiation for batches the caller flags DK_RX_BATCH_ALIGNED16, which then needs no realignment code and fewer
+// registers.
+template <bool kShift>
 __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t lane,
                                              WaveLds& W, uint32_t off, uint32_t len, Chunk& C) {
     // ---------------- Phase A: descriptor (loaded by the caller); small frames into registers ----------------
     const bool inb = live && (uint64_t)off + len <= frames_bytes;
     const uint8_t* f = frames + off;
-    const bool vec = inb && (reinterpret_cast<uintptr_t>(f) & 15) == 0;  // vector path
-    const bool big = vec && len > 64;                                  // streamed by a quarter-wave
-    const uint32_t nblk = big ? (len + 15) >> 4 : 0;                     // 16-byte blocks covering the frame
+    const uint32_t fmod = (uint32_t)reinterpret_cast<uintptr_t>(f) & 15u;
+    const uint32_t sh = kShift ? fmod : 0u;
+    const bool vec = inb && (kShift ? (fmod & 1u) == 0 : fmod == 0);  // vector path
+    const uint32_t span = sh + len;                        // bytes from the granule base a = f - sh
+    const bool big = vec && span > 64;                     // streamed by a quarter-wave
+    const uint32_t nblk = big ? (span + 15) >> 4 : 0;      // granules covering [a, f + len)
 
     RegAcc& R = C.R;
+    const Blob B(frames);
     {
-        const uint4* fp = reinterpret_cast<const uint4*>(f);
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             uint4 q = make_uint4(0, 0, 0, 0);
-            if (vec && !big && (uint32_t)(16 * k) < len) q = fp[k];
+            if (vec && !big && (uint32_t)(16 * k) < span) q = B.template ld<false>(off - sh + 16 * k);
             R.w[4 * k + 0] = q.x;
             R.w[4 * k + 1] = q.y;
             R.w[4 * k + 2] = q.z;
@@ -434,7 +485,7 @@ __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t fra
             if (big) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-                W.rec[rank] = make_uint2(lane | (nblk << 8), off);  // per-rank frame record: one ds_read_b64 per round
+                W.rec[rank] = make_uint2(lane | (nblk << 8), off - sh);  // per-rank record: one ds_read_b64 per round
             }
             // Wave-uniform iterations per round (1 unless a frame exceeds kCoopSpan blocks, i.e. > 1536 bytes).
             uint32_t maxit = 1;
@@ -459,52 +510,29 @@ __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t fra
                     const uint2 rec = sl[h].has ? W.rec[k] : make_uint2(0, 0);
                     sl[h].j = rec.x & 0xFFu;
                     sl[h].nb = rec.x >> 8;
-                    sl[h].base = reinterpret_cast<const uint4*>(frames + rec.y);
+                    sl[h].boff = rec.y;
                     sl[h].acc = 0;
                 }
                 for (uint32_t it = 0; it < maxit; it++) {
                     const uint32_t b0 = it * kCoopSpan + l16;
                     uint4 d[kRoundsPerStep][kCoopU];
-#if DK_LDSDMA
 #pragma unroll
                     for (uint32_t h = 0; h < kRoundsPerStep; h++)
 #pragma unroll
                         for (uint32_t u = 0; u < kCoopU; u++) {
                             const uint32_t b = b0 + 16 * u;
-                            if (b < sl[h].nb)
-                                __builtin_amdgcn_global_load_lds(static_cast<const void*>(sl[h].base + b),
-                                                                 (lds_void*)(&W.dma[h][u][0]), 16, 0,
-                                                                 DK_NT_LOADS ? 2 : 0);
+                            d[h][u] = b < sl[h].nb ? B.template ld<DK_NT_LOADS != 0>(sl[h].boff + 16 * b) : make_uint4(0, 0, 0, 0);
                         }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
-#pragma unroll
-                        for (uint32_t u = 0; u < kCoopU; u++) {
-                            const uint32_t b = b0 + 16 * u;
-                            d[h][u] = b < sl[h].nb ? W.dma[h][u][lane] : make_uint4(0, 0, 0, 0);
-                        }
-#else
-#pragma unroll
-                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
-#pragma unroll
-                        for (uint32_t u = 0; u < kCoopU; u++) {
-                            const uint32_t b = b0 + 16 * u;
-                            d[h][u] = b < sl[h].nb ? ld_stream(sl[h].base + b) : make_uint4(0, 0, 0, 0);
-                        }
-#endif
 #pragma unroll
                     for (uint32_t h = 0; h < kRoundsPerStep; h++)
 #pragma unroll
                         for (uint32_t u = 0; u < kCoopU; u++) {
                             const uint32_t b = b0 + 16 * u;
                             sl[h].acc = block_sum(d[h][u], sl[h].acc);
-                            if (sl[h].has && b < 4) W.hdr[sl[h].j][b] = d[h][u];  // big frame: 4 < nb
+                            // header window: 4 granules, a 5th when frames may start off a 16-byte boundary
+                            if (sl[h].has && b < (kShift ? 5u : 4u)) W.hdr[sl[h].j][b] = d[h][u];  // 5 <= nb
                             if (b < sl[h].nb && b + 2 >= sl[h].nb) W.tail[sl[h].j][b + 2 - sl[h].nb] = d[h][u];
                         }
-#if DK_LDSDMA
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads retired before the next DMA
-#endif
                 }
 #pragma unroll
                 for (uint32_t h = 0; h < kRoundsPerStep; h++) {
@@ -533,6 +561,18 @@ __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t fra
             }
         }
     }
+    // Frames not on a 16-byte boundary: drop the granule bytes before the frame from the whole-frame sum and shift
+    // the header window into frame coordinates (skipped when the whole wave is aligned).
+    if (kShift && __ballot(vec && sh != 0)) {
+        uint32_t x[4] = {0, 0, 0, 0};
+        if (big && sh != 0) {
+            const uint4 h = W.hdr[lane][4];
+            x[0] = h.x; x[1] = h.y; x[2] = h.z; x[3] = h.w;
+            fsum -= block_sum_masked(R.w[0], R.w[1], R.w[2], R.w[3], 0, (int)sh, 0);
+        }
+        if (vec && sh != 0) realign(R.w, x, sh);
+    }
+    C.sh = sh;
     C.inb = inb;
     C.vec = vec;
     C.big = big;
@@ -550,11 +590,11 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& 
         const uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
         return block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
     }
-    if ((int)(16 * C.nblk) - E <= 32) {
+    if ((int)(16 * C.nblk - C.sh) - E <= 32) {
         uint32_t pre = block_sum(make_uint4(R.w[0], R.w[1], R.w[2], R.w[3]), 0);
         pre = block_sum(make_uint4(R.w[4], R.w[5], R.w[6], R.w[7]), pre);
         pre += R.w[8] & 0xFFFFu;
-        const int t0 = (int)(16 * C.nblk) - 32;
+        const int t0 = (int)(16 * C.nblk - C.sh) - 32;  // frame offset of the first tail byte
         const uint4 a = W.tail[lane][0], c = W.tail[lane][1];
         uint32_t post = block_sum_masked(a.x, a.y, a.z, a.w, E - t0, 16, 0);
         post = block_sum_masked(c.x, c.y, c.z, c.w, E - t0 - 16, 16, post);
@@ -568,10 +608,17 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& 
 //   Phases A, B: stream_chunk.
 //   Phase C (lane): parse from registers, checksum = sum(all blocks) - sum[0, S) - sum[E, 16 * nblk) (exact integer
 //     arithmetic), T4/U3, options, demux, results.
+template <bool kShift>
 __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
                                         uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
     Chunk C;
-    stream_chunk(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+    stream_chunk<kShift>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+#ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
+    if (live) P.res.meta[i] = C.fsum ^ C.R.w[3] ^ C.R.w[9];
+    v_out = kNone;
+    fid_out = DK_FLOW_NONE;
+    return;
+#endif
     const RegAcc& R = C.R;
     const bool inb = C.inb, vec = C.vec, big = C.big;
     const uint8_t* f = P.frames + off;
@@ -699,7 +746,11 @@ __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
 // wraps). At exit the histogram row is written with plain stores to flow_scratch[b][*] and dk_flow_reduce_kernel adds
 // the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
-__global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P) {
+#ifndef DK_MIN_WAVES_ALIGNED
+#define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
+#endif
+template <bool kShift>
+__global__ __launch_bounds__(kBlock, kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED) void dk_rx_kernel(RxParams P) {
     __shared__ WaveLds s_wave[kWaves];        // per-wave phase B/C exchange
     __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
@@ -729,7 +780,7 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_rx_kernel(RxParams P)
             nlen = P.len[i + cstep];
         }
         uint32_t v, fid;
-        rx_tile(P, i, live, lane, s_wave[wv], off, len, v, fid);
+        rx_tile<kShift>(P, i, live, lane, s_wave[wv], off, len, v, fid);
         if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
             if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
             else if (P.flow_mode == kFlowGlobal)
@@ -794,14 +845,14 @@ __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {  // p is 2-
     *reinterpret_cast<uint16_t*>(p) = (uint16_t)bswap16(v);
 #endif
 }
-// Fast-path field write at frame byte k (k even, k < 64, 16-byte aligned frame): DK_TX_STORE 2 rewrites the whole
+// Fast-path field write at frame byte k (k even, k < 64, even frame address): DK_TX_STORE 2 rewrites the whole
 // 16-byte block from the register window when the block lies inside the frame (a full-block write needs no
 // read-modify-write below L2), else a 16-bit store.
 template <int k>
-__device__ __forceinline__ void store_field(uint8_t* f, const RegAcc& R, uint32_t len, uint32_t v) {
+__device__ __forceinline__ void store_field(uint8_t* f, const RegAcc& R, uint32_t len, uint32_t sh, uint32_t v) {
 #if DK_TX_STORE == 2
     constexpr int b = k / 16;
-    if ((uint32_t)(16 * b + 16) <= len) {
+    if (sh == 0 && (uint32_t)(16 * b + 16) <= len) {
         uint32_t d[4] = {R.w[4 * b], R.w[4 * b + 1], R.w[4 * b + 2], R.w[4 * b + 3]};
         constexpr int j = (k / 4) % 4;
         d[j] = (k & 2) ? (d[j] & 0xFFFFu) | (bswap16(v) << 16) : (d[j] & 0xFFFF0000u) | bswap16(v);
@@ -851,7 +902,7 @@ __device__ __noinline__ void tx_slow(uint8_t* f, uint32_t len) {
 __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t lane, WaveLds& W, uint32_t off,
                                         uint32_t len) {
     Chunk C;
-    stream_chunk(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+    stream_chunk<true>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
     if (!C.inb) return;
     uint8_t* f = P.frames + off;
     const RegAcc& R = C.R;
@@ -878,7 +929,7 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
         c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
     }
 #if DK_TX_STORE == 3
-    if (len >= 64) {  // rewrite the whole 64-byte header window: full-line writes, no partial-write merge below L2
+    if (len >= 64 && C.sh == 0) {  // rewrite the whole 64-byte header window: full-line writes, no partial-write merge below L2
         uint32_t d[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) d[k] = R.w[k];
@@ -891,10 +942,10 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
         return;
     }
 #endif
-    store_field<24>(f, R, len, ipc);
+    store_field<24>(f, R, len, C.sh, ipc);
     if (l4) {
-        if (tcp) store_field<50>(f, R, len, c);
-        else store_field<40>(f, R, len, c);
+        if (tcp) store_field<50>(f, R, len, C.sh, c);
+        else store_field<40>(f, R, len, C.sh, c);
     }
 }
 
@@ -925,7 +976,8 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
 
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_kernel, dk::kBlock, dyn_lds_bytes) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_kernel<true>, dk::kBlock, dyn_lds_bytes) !=
+        hipSuccess)
         return 0;
     return blocks;
 }
@@ -933,7 +985,10 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes) {
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
-    hipLaunchKernelGGL(dk::dk_rx_kernel, dim3(grid), dim3(dk::kBlock), dyn, (hipStream_t)stream, p);
+    if (p.aligned16)
+        hipLaunchKernelGGL(dk::dk_rx_kernel<false>, dim3(grid), dim3(dk::kBlock), dyn, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(dk::dk_rx_kernel<true>, dim3(grid), dim3(dk::kBlock), dyn, (hipStream_t)stream, p);
     if (hipGetLastError() != hipSuccess) return 5;
     if (p.flow_mode == dk::kFlowLds) {
         const dim3 g2((p.flow_words + dk::kBlock - 1) / dk::kBlock, (grid + dk::kReduceRows - 1) / dk::kReduceRows);

@@ -89,7 +89,9 @@ def _ptr(t) -> Optional[int]:
 class FrameBatch:
     """An HBM-resident batch: packed frame blob + per-frame (u32 offset, u16 length) descriptors."""
 
-    def __init__(self, blob, off, lens, frames_bytes: Optional[int] = None):
+    def __init__(self, blob, off, lens, frames_bytes: Optional[int] = None, aligned16: bool = False):
+        """aligned16: the DK_RX_BATCH_ALIGNED16 hint (every frame at a 16-byte aligned address); a wrong hint only
+        costs speed, never correctness."""
         import torch
 
         assert blob.dtype == torch.uint8 and blob.is_cuda
@@ -97,6 +99,7 @@ class FrameBatch:
         self.blob, self.off, self.len = blob, off, lens
         self.n = off.numel()
         self.frames_bytes = blob.numel() if frames_bytes is None else frames_bytes
+        self.aligned16 = aligned16
 
     @classmethod
     def from_numpy(cls, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, device: int = 0) -> "FrameBatch":
@@ -106,10 +109,12 @@ class FrameBatch:
         b = torch.from_numpy(np.ascontiguousarray(blob, dtype=np.uint8)).to(dev)
         o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint32).view(np.int32)).to(dev)
         ln = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint16).view(np.int16)).to(dev)
-        return cls(b, o, ln)
+        aligned = b.data_ptr() % 16 == 0 and bool(np.all(np.asarray(off, dtype=np.uint64) % 16 == 0))
+        return cls(b, o, ln, aligned16=aligned)
 
     def c_struct(self) -> N.DkRxBatch:
-        return N.DkRxBatch(_ptr(self.blob), self.frames_bytes, _ptr(self.off), _ptr(self.len), self.n, 0)
+        return N.DkRxBatch(_ptr(self.blob), self.frames_bytes, _ptr(self.off), _ptr(self.len), self.n,
+                           N.DK_RX_BATCH_ALIGNED16 if self.aligned16 else 0)
 
 
 class RxResults:
@@ -193,9 +198,14 @@ class RxEngine:
                "dk_rx_process")
 
     def receive_batch_host(self, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, results: RxResults,
-                           chunk_frames: int = 0) -> None:
-        """Host-resident batch (NIC ring / socket buffer): pipelined H2D -> kernel -> D2H. Synchronous."""
-        b = N.DkRxBatch(blob.ctypes.data, blob.nbytes, off.ctypes.data, lens.ctypes.data, len(off), 0)
+                           chunk_frames: int = 0, aligned16: Optional[bool] = None) -> None:
+        """Host-resident batch (NIC ring / socket buffer): pipelined H2D -> kernel -> D2H. Synchronous.
+        aligned16 (DK_RX_BATCH_ALIGNED16 hint; offsets are what matters, the staging keeps them mod 16): by default
+        computed from `off`."""
+        if aligned16 is None:
+            aligned16 = bool(np.all(np.asarray(off, dtype=np.uint64) % 16 == 0))
+        b = N.DkRxBatch(blob.ctypes.data, blob.nbytes, off.ctypes.data, lens.ctypes.data, len(off),
+                        N.DK_RX_BATCH_ALIGNED16 if aligned16 else 0)
         r = results.c_struct()
         _check(self.lib.dk_rx_process_host(self._ctx, ctypes.byref(b), ctypes.byref(r), chunk_frames),
                "dk_rx_process_host")

@@ -253,7 +253,8 @@ def build_device(tr: Traffic, engine, align: int = 64, seed: int = SEED):
             for k in range(int(d)):
                 blob[base + k] = 0
     batch = FrameBatch(blob, torch.from_numpy(off.view(np.int32)).to(dev),
-                       torch.from_numpy(tr.frame_len.view(np.int16)).to(dev))
+                       torch.from_numpy(tr.frame_len.view(np.int16)).to(dev),
+                       aligned16=blob.data_ptr() % 16 == 0)  # 64-byte slots
     engine.tx_checksum(batch)
     return batch
 

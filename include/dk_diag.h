@@ -13,7 +13,8 @@ extern "C" {
 /* Streaming read of `bytes` (multiple of 16) of device memory at `buf`; `scratch` = device u32[grid] (zeroed by the
  * caller). Used to measure the achievable HBM read bandwidth on the running box. Async on `stream`.
  * mode 0: grid-stride loads; 1: contiguous 8 KiB per wave step; 2: as 1 with nontemporal loads; 3: 16 KiB per wave
- * step, nontemporal; 4/5: 16 KiB per wave step by LDS-DMA (global_load_lds), nontemporal / default policy.
+ * step, nontemporal; 4/5: 16 KiB per wave step by LDS-DMA (global_load_lds), nontemporal / default policy;
+ * 6/7: as 3 with buffer_load_dwordx4 (32-bit offsets: bytes < 4 GiB), nontemporal / default policy.
  * Returns 0, EINVAL or EIO. */
 int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode, void* stream);
 

@@ -43,9 +43,15 @@ extern "C" {
 
 #define DK_RX_ABI_VERSION 2u
 
-/* Frames whose offset is a multiple of this take the vectorised path; any other offset is still processed
- * (bit-exact), by a per-lane byte-load path. */
-#define DK_RX_FAST_ALIGN 16u
+/* Frames at an address that is a multiple of this take the vectorised path (16-byte aligned frames directly, other
+ * even addresses — e.g. NIC buffers with the Ethernet header at 2 mod 16 — through a realigned header window); any
+ * other address is still processed (bit-exact), by a per-lane byte-load path. */
+#define DK_RX_FAST_ALIGN 2u
+
+/* dk_rx_batch.flags */
+#define DK_RX_BATCH_ALIGNED16 1u /* hint: frames are (mostly) at 16-byte aligned addresses; the engine launches its
+                                    instantiation without the realignment path (other frames then take the byte path,
+                                    still bit-exact) */
 
 /* flow_id value for frames that do not demux to a socket. */
 #define DK_FLOW_NONE 0xFFFFFFFFu
@@ -131,7 +137,7 @@ typedef struct dk_rx_batch {
     const uint32_t* off;      /* [n] byte offset of each frame in the blob                             */
     const uint16_t* len;      /* [n] frame length: Ethernet header included, FCS excluded              */
     uint32_t n;
-    uint32_t reserved;
+    uint32_t flags;           /* DK_RX_BATCH_* hints, 0 = none                                         */
 } dk_rx_batch;
 
 /* Per-frame results, struct-of-arrays, one element per frame. Required arrays: meta, src_ip, dst_ip, ports,

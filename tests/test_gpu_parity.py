@@ -22,12 +22,14 @@ def torch_cuda():
     return torch
 
 
-def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None):
+def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None, aligned16=None):
     import torch
 
     eng = RxEngine(cfg or Config(LOCAL), device=0)
     eng.set_sockets(flows)
     b = FrameBatch.from_numpy(blob, off, lens, device=0)
+    if aligned16 is not None:  # override the hint: both kernel instantiations see the same inputs
+        b.aligned16 = aligned16
     if frames_bytes is not None:
         b.frames_bytes = frames_bytes
     r = eng.results(len(off), tcp_fields=tcp_fields)
@@ -57,8 +59,8 @@ def assert_same(got, exp, ctx=""):
             raise AssertionError(f"{ctx}: '{k}' differs at {bad}: got {v[bad]} exp {e[bad]}{extra}")
 
 
-def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None):
-    got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes)
+def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None):
+    got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes, aligned16=aligned16)
     exp = run_oracle(blob, off, lens, flows, cfg, frames_bytes=frames_bytes)
     assert_same(got, exp, ctx)
     return got
@@ -81,8 +83,9 @@ def test_offload_flags(torch_cuda, tcp_off, udp_off):
     check(blob, off, lens, F.corpus_flows(), Config(LOCAL, tcp_off, udp_off), ctx="offload")
 
 
+@pytest.mark.parametrize("hint", [None, False])
 @pytest.mark.parametrize("mix", ["tcp1500", "udp64", "imix", "random_len"])
-def test_random_batches(torch_cuda, mix):
+def test_random_batches(torch_cuda, mix, hint):
     n = 20000
     flows = np.concatenate([synth.make_flows(512), synth.make_flows(32, kind="udp")])
     rng = np.random.default_rng(11)
@@ -93,7 +96,7 @@ def test_random_batches(torch_cuda, mix):
     tr = synth.traffic(n, ip_len, flows, seed=5)
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.05, tr))
-    got = check(blob, off, lens, flows, ctx=mix)
+    got = check(blob, off, lens, flows, ctx=f"{mix} hint={hint}", aligned16=hint)
     assert (got["meta"] & 0xFF <= 1).mean() > 0.9
 
 
@@ -107,6 +110,8 @@ def test_misaligned_and_offsets(torch_cuda):
     blob, off, lens2 = F.pack(frames, align=64, misalign=list(range(16)))
     perm = np.random.default_rng(1).permutation(n)
     check(blob, off[perm], lens2[perm], flows, ctx="misaligned")
+    # a wrong DK_RX_BATCH_ALIGNED16 hint costs speed only: misaligned frames then take the byte path
+    check(blob, off[perm], lens2[perm], flows, ctx="misaligned, aligned16 hint", aligned16=True)
 
 
 def test_fuzz_headers(torch_cuda):
@@ -351,3 +356,31 @@ def test_aligned_traffic_stays_on_vector_path(torch_cuda, mix):
     small = int((lens <= 64).sum())
     assert st.tolist() == [small, n - small, 0, 0], st
     assert (r.to_numpy()["meta"] & 0xFF <= 1).all()
+
+
+@pytest.mark.parametrize("shift", [2, 6, 14])
+def test_nic_offsets_stay_on_vector_path(torch_cuda, shift):
+    """Frames at an even offset that is not a multiple of 16 (NIC receive buffers put the Ethernet header at 2 mod 16
+    so the IP header is aligned) use the vector path with a realigned header window, bit-exact vs the oracle."""
+    import torch
+
+    n = 12000
+    flows = np.concatenate([synth.make_flows(256), synth.make_flows(16, kind="udp")])
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=3), flows, seed=4)
+    blob0, off0, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob0, off0, synth.corruption_plan(n, 0.03, tr))
+    frames = [blob0[o:o + L].tobytes() for o, L in zip(off0, lens)]
+    blob, off, lens2 = F.pack(frames, align=64, misalign=[shift])
+    eng = RxEngine(Config(LOCAL))
+    eng.set_sockets(flows)
+    eng.path_stats(True)
+    b = FrameBatch.from_numpy(blob, off, lens2)
+    r = eng.results(n, tcp_fields=True)
+    eng.receive_batch(b, r)
+    torch.cuda.synchronize()
+    st = eng.path_stats()
+    assert st[3] == 0, st  # no byte-path frames
+    small = int((lens2.astype(np.int64) + shift <= 64).sum())
+    assert st[0] == small, st
+    assert_same(r.to_numpy(), run_oracle(blob, off, lens2, flows), f"shift {shift}")
+    tx_check(blob, off, lens2, f"tx shift {shift}")
