@@ -53,6 +53,7 @@ struct dk_rx_ctx {
     uint32_t cu_count = 0;
     uint32_t occ_dyn = ~0u;   // occupancy cache: dynamic LDS bytes -> resident blocks per CU
     uint32_t occ_blocks = 0;
+    uint32_t occ_stage = 0;
     unsigned long long* d_path_stats = nullptr;  // dk_diag path counters (nullptr = off)
 };
 
@@ -121,17 +122,24 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
             p.flow_mode = dk::kFlowGlobal;
         }
     }
-    if (c->occ_dyn != dyn) {
-        c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn), 1);
-        c->occ_dyn = dyn;
-    }
-    // Schedule and resident workgroups per CU (measured, DESIGN.md "Tuning log"): large frames (>= 1 KiB of blob per
-    // frame) stream best with one contiguous share per wave and 3 workgroups/CU; small and mixed frames with
-    // round-robin tiles and 4/CU. Never more than the occupancy admits (large socket tables take LDS).
+    // Kernel instantiation, schedule and resident workgroups per CU (measured, DESIGN.md §8 "Tuning log"):
+    //  - frames of >= 128 bytes of blob on average: the result-staging kernel (stores leave in one burst per 8 chunks
+    //    instead of between the frame reads; -11 % at C2, -4 % IMIX; no gain for 64-byte frames, which are
+    //    issue-bound and want 4 WG/CU);
+    //  - round-robin 256-frame tiles (sched 0) for every frame size (contiguous per-wave shares, sched 1, measured
+    //    1-3 % slower once stores are staged).
+    // Never more workgroups per CU than the occupancy admits (large socket tables take LDS).
     const uint64_t bytes_per_frame = p.frames_bytes / p.n;
-    p.sched = bytes_per_frame >= 1024 ? 1u : 0u;
-    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.sched ? 3u : 4u);
-    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)atoi(e) ? 1u : 0u;
+    p.stage = bytes_per_frame >= 128 ? 1u : 0u;
+    if (const char* e = getenv("DK_RX_STAGE")) p.stage = atoi(e) ? 1u : 0u;  // tuning
+    p.sched = 0;
+    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 2);  // tuning
+    if (c->occ_dyn != dyn || c->occ_stage != p.stage) {
+        c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn, p.stage != 0), 1);
+        c->occ_dyn = dyn;
+        c->occ_stage = p.stage;
+    }
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.stage ? 3u : 4u);
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
     if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
@@ -142,8 +150,8 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         p.flow_scratch = fs.p;
     }
     if (getenv("DK_RX_DEBUG"))
-        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u\n", p.n, ntiles,
-                grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched);
+        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u\n", p.n,
+                ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage);
     return dk_launch_rx(p, grid, stream);
 }
 
@@ -447,6 +455,7 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
     }
     dk::TxParams p{frames, frames_bytes, off, len, n, frames_bytes / n >= 1024 ? 1u : 0u};
     uint32_t per_cu = std::min<uint32_t>(occ, p.sched ? 3u : 4u);
+    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 2);  // tuning
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);  // tuning
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
     return dk_launch_tx(p, grid, stream);

@@ -346,6 +346,9 @@ __device__ __forceinline__ uint32_t probe(const RxParams& P, uint32_t kind, uint
                                           uint32_t lport_rport) {
     const uint4* T = reinterpret_cast<const uint4*>(P.table);
     uint32_t h = flow_hash(kind, lip, rip, lport_rport) & P.table_mask;
+#ifdef DK_ABL_NOPROBE  // ablation (tuning only): no table load
+    return h & 1023u;
+#endif
     for (uint32_t i = 0; i <= P.table_mask; i++) {
         const uint4 s = T[h];
         if (s.x == 0) break;
@@ -604,13 +607,40 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& 
     return MemAcc{f}.sum_le16(34, (uint32_t)E);
 }
 
+#ifndef DK_RES_STORE
+#define DK_RES_STORE 0  // result stores: 0 plain, 1 nontemporal
+#endif
+__device__ __forceinline__ void st_res(uint32_t* p, uint32_t v) {
+#if DK_RES_STORE == 1
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // One frame per lane, 64 frames per wave chunk. Returns the verdict and the flow id (DK_FLOW_NONE if none).
 //   Phases A, B: stream_chunk.
 //   Phase C (lane): parse from registers, checksum = sum(all blocks) - sum[0, S) - sum[E, 16 * nblk) (exact integer
 //     arithmetic), T4/U3, options, demux, results.
-template <bool kShift>
+// The six required result words of one frame (dk_rx.h), held in registers when the kernel stages its stores.
+struct Rec {
+    uint32_t meta, src, dst, ports, pay, fid;
+};
+// Result staging: result stores interleaved with the frame stream cost ~11 % at C2 (every wave's
+// 6 x 256 B of results per chunk reach HBM as scattered write bursts between the reads; ablation: storing them in an
+// L2-resident window instead recovers it all). The staged kernels hold the last kStageK chunks' results in registers
+// and store them together, so a wave's writes leave in one burst per kStageK chunks (at exit for C2 at 3 WG/CU).
+#ifndef DK_STAGE_K
+#define DK_STAGE_K 8
+#endif
+#ifndef DK_MIN_WAVES_STAGED
+#define DK_MIN_WAVES_STAGED 3  // 8 x 6 staged words fit in 168 VGPRs without spills
+#endif
+constexpr int kStageK = DK_STAGE_K;
+
+template <bool kShift, bool kStage>
 __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
-                                        uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
+                                        uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out, Rec& rec) {
     Chunk C;
     stream_chunk<kShift>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
 #ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
@@ -682,6 +712,9 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
     }
 
     const uint32_t v = L.v;
+#ifdef DK_ABL_STOREMOD  // ablation (tuning only; needs n > 65535): results land in a 256 KB L2-resident window
+    i &= 0xFFFFu;
+#endif
     if (live) {
         // fields for delivered / no-socket TCP and UDP and for parsed ARP and ICMPv4 (codes 0..3, dk_rx.h)
         const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;
@@ -696,12 +729,20 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
             pay = poff | ((L.E - poff) << 16);
             if (is_tcp) { seq = L.seq; ack = L.ack; win = L.winurg; }
         }
-        P.res.meta[i] = meta;
-        P.res.src_ip[i] = src;
-        P.res.dst_ip[i] = dst;
-        P.res.ports[i] = ports;
-        P.res.payload[i] = pay;
-        P.res.flow_id[i] = fid;
+        rec = Rec{meta, src, dst, ports, pay, fid};
+        if (!kStage) {
+        st_res(P.res.meta + i, meta);
+#ifdef DK_ABL_NOSTORE  // ablation (tuning only): one result array
+        if (ports == 0x12345678u)
+#endif
+        {
+        st_res(P.res.src_ip + i, src);
+        st_res(P.res.dst_ip + i, dst);
+        st_res(P.res.ports + i, ports);
+        st_res(P.res.payload + i, pay);
+        st_res(P.res.flow_id + i, fid);
+        }
+        }
         if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
         if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
         if (P.res.tcp_win) P.res.tcp_win[i] = win;
@@ -718,21 +759,49 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
     fid_out = fid;
 }
 
-// Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"):
+// Store the nst most recent staged chunks (stg[k] belongs to frame i_last - k * cstep).
+__device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)[kStageK], uint32_t nst,
+                                             uint32_t i_last, uint32_t cstep, uint32_t f1) {
+#pragma unroll
+    for (int k = kStageK - 1; k >= 0; k--) {
+        if ((uint32_t)k >= nst) continue;
+        const uint32_t i = i_last - (uint32_t)k * cstep;
+        if (i >= f1) continue;
+        st_res(P.res.meta + i, stg[k].meta);
+        st_res(P.res.src_ip + i, stg[k].src);
+        st_res(P.res.dst_ip + i, stg[k].dst);
+        st_res(P.res.ports + i, stg[k].ports);
+        st_res(P.res.payload + i, stg[k].pay);
+        st_res(P.res.flow_id + i, stg[k].fid);
+    }
+}
+
+// Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). A wave's chunk c holds frames
+// i = c + lane_off (lane_off = lane unless noted), for c = f0, f0 + step, ... below f1; lanes with i >= f1 idle.
 //   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame) and walks it in 64-frame chunks
-//            (no tile quantization; best for large frames);
+//            (no tile quantization);
 //   sched 0: round-robin 256-frame tiles, wave wv of workgroup b takes frames [t * 256 + 64 wv, +64) of tiles
-//            t = b, b + G, ... (the grid sweeps one contiguous window of the blob; best for small/mixed frames).
+//            t = b, b + G, ... (the grid sweeps one contiguous window of the blob; best for small/mixed frames);
+//   sched 2: phase-B-step interleave: lane group g = lane / 8 of wave gw (of nw) takes the 8 consecutive frames
+//            c + 8 (g * nw + gw) + [0, 8), c = 0, 64 nw, ... A phase-B step streams one lane group, so at any moment
+//            the whole grid reads one contiguous window of ~nw * 8 frames (the read probe's sweep) instead of nw
+//            separate streams.
 struct WaveRange {
-    uint32_t f0, f1, step;  // chunks start at f0, f0 + step, ... below f1
+    uint32_t f0, f1, step, lane_off;
 };
-__device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint32_t wv) {
+__device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint32_t wv, uint32_t lane) {
     WaveRange r;
+    const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
+    r.lane_off = lane;
     if (sched == 1) {
-        const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
         r.f0 = (uint32_t)(((uint64_t)n * gw) / nw);
         r.f1 = (uint32_t)(((uint64_t)n * (gw + 1)) / nw);
         r.step = 64;
+    } else if (sched == 2) {
+        r.f0 = 8 * gw;
+        r.f1 = n;
+        r.step = 64 * nw;
+        r.lane_off = (lane >> 3) * 8 * nw + (lane & 7);
     } else {
         r.f0 = blockIdx.x * kBlock + wv * 64;
         r.f1 = n;
@@ -749,8 +818,9 @@ __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
-template <bool kShift>
-__global__ __launch_bounds__(kBlock, kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED) void dk_rx_kernel(RxParams P) {
+template <bool kShift, bool kStage>
+__global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED)
+void dk_rx_kernel(RxParams P) {
     __shared__ WaveLds s_wave[kWaves];        // per-wave phase B/C exchange
     __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
@@ -764,15 +834,17 @@ __global__ __launch_bounds__(kBlock, kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNE
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     __syncthreads();
 
-    const WaveRange r = wave_range(P.sched, P.n, wv);
+    const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     const uint32_t f0 = r.f0, f1 = r.f1, cstep = r.step;
+    Rec stg[kStage ? kStageK : 1];
+    uint32_t nstg = 0;  // wave-uniform
     uint32_t noff = 0, nlen = 0;  // descriptors of this wave's next chunk
-    if (f0 + lane < f1) {
-        noff = P.off[f0 + lane];
-        nlen = P.len[f0 + lane];
+    if (f0 + r.lane_off < f1) {
+        noff = P.off[f0 + r.lane_off];
+        nlen = P.len[f0 + r.lane_off];
     }
     for (uint32_t c = f0; c < f1; c += cstep) {
-        const uint32_t i = c + lane;
+        const uint32_t i = c + r.lane_off;
         const bool live = i < f1;
         const uint32_t off = noff, len = nlen;
         if (i + cstep < f1) {  // prefetch the next chunk's descriptors
@@ -780,7 +852,17 @@ __global__ __launch_bounds__(kBlock, kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNE
             nlen = P.len[i + cstep];
         }
         uint32_t v, fid;
-        rx_tile<kShift>(P, i, live, lane, s_wave[wv], off, len, v, fid);
+        Rec rec;
+        rx_tile<kShift, kStage>(P, i, live, lane, s_wave[wv], off, len, v, fid, rec);
+        if (kStage) {  // shift register of the last kStageK chunks' results; stored when full and at exit
+#pragma unroll
+            for (int k = kStageK - 1; k > 0; k--) stg[k] = stg[k - 1];
+            stg[0] = rec;
+            if (++nstg == kStageK) {
+                flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, i, cstep, f1);
+                nstg = 0;
+            }
+        }
         if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
             if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
             else if (P.flow_mode == kFlowGlobal)
@@ -798,6 +880,12 @@ __global__ __launch_bounds__(kBlock, kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNE
         }
     }
 
+    if (kStage && nstg) {
+        // the last chunk processed had c_last = f0 + (chunks - 1) * cstep
+        const uint32_t nch = (f1 - f0 + cstep - 1) / cstep;
+        flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, f0 + (nch - 1) * cstep + r.lane_off, cstep,
+                     f1);
+    }
     __syncthreads();
     if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
         atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
@@ -954,14 +1042,14 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
     __shared__ WaveLds s_wave[kWaves];
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6;
-    const WaveRange r = wave_range(P.sched, P.n, wv);
+    const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     uint32_t noff = 0, nlen = 0;
-    if (r.f0 + lane < r.f1) {
-        noff = P.off[r.f0 + lane];
-        nlen = P.len[r.f0 + lane];
+    if (r.f0 + r.lane_off < r.f1) {
+        noff = P.off[r.f0 + r.lane_off];
+        nlen = P.len[r.f0 + r.lane_off];
     }
     for (uint32_t c = r.f0; c < r.f1; c += r.step) {
-        const uint32_t i = c + lane;
+        const uint32_t i = c + r.lane_off;
         const uint32_t off = noff, len = nlen;
         if (i + r.step < r.f1) {
             noff = P.off[i + r.step];
@@ -974,21 +1062,25 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
 }  // namespace
 }  // namespace dk
 
-int dk_rx_resident_blocks(uint32_t dyn_lds_bytes) {
+int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, bool stage) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_kernel<true>, dk::kBlock, dyn_lds_bytes) !=
-        hipSuccess)
-        return 0;
+    const auto k = stage ? dk::dk_rx_kernel<true, true> : dk::dk_rx_kernel<true, false>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, dk::kBlock, dyn_lds_bytes) != hipSuccess) return 0;
     return blocks;
 }
 
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
-    if (p.aligned16)
-        hipLaunchKernelGGL(dk::dk_rx_kernel<false>, dim3(grid), dim3(dk::kBlock), dyn, (hipStream_t)stream, p);
+    const hipStream_t s = (hipStream_t)stream;
+    if (p.aligned16 && p.stage)
+        hipLaunchKernelGGL((dk::dk_rx_kernel<false, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+    else if (p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_kernel<false, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+    else if (p.stage)
+        hipLaunchKernelGGL((dk::dk_rx_kernel<true, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     else
-        hipLaunchKernelGGL(dk::dk_rx_kernel<true>, dim3(grid), dim3(dk::kBlock), dyn, (hipStream_t)stream, p);
+        hipLaunchKernelGGL((dk::dk_rx_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     if (hipGetLastError() != hipSuccess) return 5;
     if (p.flow_mode == dk::kFlowLds) {
         const dim3 g2((p.flow_words + dk::kBlock - 1) / dk::kBlock, (grid + dk::kReduceRows - 1) / dk::kReduceRows);

@@ -100,6 +100,25 @@ def test_random_batches(torch_cuda, mix, hint):
     assert (got["meta"] & 0xFF <= 1).mean() > 0.9
 
 
+@pytest.mark.parametrize("grid", [None, "2", "7"])
+@pytest.mark.parametrize("sched", ["0", "1", "2"])
+@pytest.mark.parametrize("stage", ["0", "1"])
+def test_kernel_variants(torch_cuda, monkeypatch, stage, sched, grid):
+    """Both kernel families (result staging on/off) under every wave schedule, with grids small enough that each wave
+    walks many chunks (staged results flushed mid-loop and at exit) and with the default grid."""
+    monkeypatch.setenv("DK_RX_STAGE", stage)
+    monkeypatch.setenv("DK_RX_SCHED", sched)
+    if grid is not None:
+        monkeypatch.setenv("DK_RX_GRID", grid)
+    n = 12345
+    flows = np.concatenate([synth.make_flows(300), synth.make_flows(20, kind="udp")])
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=4), flows, seed=6)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.05, tr))
+    perm = np.random.default_rng(8).permutation(n)
+    check(blob, off[perm], lens[perm], flows, ctx=f"stage={stage} sched={sched} grid={grid}")
+
+
 def test_misaligned_and_offsets(torch_cuda):
     """Frames at every offset mod 16 (fast path only at 0 mod 16) and in shuffled, gapped order."""
     flows = synth.make_flows(64)
