@@ -205,7 +205,7 @@ def tx_rate(eng, batch, frame_bytes, stream, iters=20):
 
 def read_ceiling(batch, stream, iters=10):
     """On-box streaming-read ceiling: dk_diag_read_probe over the same frame blob, register loads
-    (mode 3) and LDS-DMA (mode 4), 4 and 8 waves per CU; best GB/s and the configuration that reached it."""
+    (global mode 3, buffer mode 6) and LDS-DMA (mode 4), 4 and 8 waves per CU; best GB/s and its configuration."""
     import torch
 
     from demikernel_amd import _native as N
@@ -214,7 +214,8 @@ def read_ceiling(batch, stream, iters=10):
     nbytes = batch.blob.numel() // 16 * 16
     cus = torch.cuda.get_device_properties(batch.blob.device).multi_processor_count
     best = (0.0, "")
-    for mode in (3, 4):
+    names = {3: "global_load register", 4: "LDS-DMA", 6: "buffer_load register"}
+    for mode in (3, 4, 6):
         for per_cu in (4, 8):
             grid = per_cu * cus // 4  # 256-thread workgroups: 4 waves each
             scratch = torch.zeros(grid, dtype=torch.int32, device=batch.blob.device)
@@ -231,7 +232,7 @@ def read_ceiling(batch, stream, iters=10):
             torch.cuda.synchronize()
             gbs = nbytes / (e0.elapsed_time(e1) / 1e3 / iters) / 1e9
             if gbs > best[0]:
-                best = (gbs, f"dk_diag_read_probe mode {mode} ({'LDS-DMA' if mode == 4 else 'register'} loads), "
+                best = (gbs, f"dk_diag_read_probe mode {mode} ({names[mode]} loads), "
                              f"{per_cu} waves/CU, {nbytes / 1e9:.2f} GB")
     return best
 

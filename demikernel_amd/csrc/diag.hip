@@ -118,11 +118,39 @@ __global__ __launch_bounds__(kBlock) void read_probe16(const uint4* __restrict__
     if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
 }
 
+// mode 8: the receive kernel's phase-B access pattern without the rest of the kernel: 1536-byte slots, a wave step
+// covers 8 consecutive slots as 2 rounds of 4 quarter-waves x 6 buffer_load_dwordx4 (nt) of 256 contiguous bytes;
+// grid-strided wave steps (as mode 6).
+__global__ __launch_bounds__(kBlock) void read_probe_frames(const uint4* __restrict__ p, uint64_t n16, uint32_t* out) {
+    constexpr uint32_t kSlot16 = 96;  // 1536-byte slot in 16-byte granules
+    uint32_t acc = 0;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63, q = lane >> 4, l16 = lane & 15;
+    const uint64_t piece = 8 * kSlot16;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0xFFFFFFFF, 0x00020000);
+    for (uint64_t base = w * piece; base < n16; base += nwaves * piece) {
+        uint4 v[12];
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int u = 0; u < 6; u++) {
+                const uint64_t i = min(base + (4 * h + q) * kSlot16 + 16 * u + l16, n16 - 1);
+                const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 2);
+                v[6 * h + u] = make_uint4(r[0], r[1], r[2], r[3]);
+            }
+#pragma unroll
+        for (int u = 0; u < 12; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    acc = __reduce_add_sync(~0ull, acc);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
+}
+
 }  // namespace
 
 extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode,
                                   void* stream) {
-    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 7) return 22;
+    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 8) return 22;
     if (mode >= 6 && bytes > 0xFFFFFFFFull) return 22;  // buffer offsets are 32-bit
     const uint4* p = (const uint4*)buf;
     const hipStream_t s = (hipStream_t)stream;
@@ -134,5 +162,6 @@ extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scr
     if (mode == 5) hipLaunchKernelGGL(read_probe16<5>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 6) hipLaunchKernelGGL(read_probe16<6>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 7) hipLaunchKernelGGL(read_probe16<7>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 8) hipLaunchKernelGGL(read_probe_frames, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

@@ -123,7 +123,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         }
     }
     // Kernel instantiation, schedule and resident workgroups per CU (measured, DESIGN.md §8 "Tuning log"):
-    //  - frames of >= 128 bytes of blob on average: the result-staging kernel (stores leave in one burst per 8 chunks
+    //  - frames of >= 128 bytes of blob on average: the result-staging kernel (stores leave in one burst per 6 chunks
     //    instead of between the frame reads; -11 % at C2, -4 % IMIX; no gain for 64-byte frames, which are
     //    issue-bound and want 4 WG/CU);
     //  - round-robin 256-frame tiles (sched 0) for every frame size (contiguous per-wave shares, sched 1, measured
@@ -133,7 +133,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
     p.stage = bytes_per_frame >= 128 ? 1u : 0u;
     if (const char* e = getenv("DK_RX_STAGE")) p.stage = atoi(e) ? 1u : 0u;  // tuning
     p.sched = 0;
-    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 2);  // tuning
+    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
     if (c->occ_dyn != dyn || c->occ_stage != p.stage) {
         c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn, p.stage != 0), 1);
         c->occ_dyn = dyn;
@@ -284,7 +284,7 @@ int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, vo
     if (!c || !b || !r) return EINVAL;
     if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
     if (b->n && (!r->meta || !r->src_ip || !r->dst_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
-    if (b->frames_bytes > (1ull << 32)) return EINVAL;
+    if (b->frames_bytes > DK_RX_MAX_BLOB) return EINVAL;
     DeviceGuard g(c->cfg.device);
     dk::RxParams p = base_params(c);
     p.frames = b->frames;
@@ -301,7 +301,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
     if (!c || !b || !r) return EINVAL;
     if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
     if (b->n && (!r->meta || !r->src_ip || !r->dst_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
-    if (b->frames_bytes > (1ull << 32)) return EINVAL;
+    if (b->frames_bytes > DK_RX_MAX_BLOB) return EINVAL;
     if (b->n == 0) return 0;
     DeviceGuard g(c->cfg.device);
     const uint32_t chunk = chunk_frames ? chunk_frames : kDefaultChunkFrames;
@@ -439,6 +439,7 @@ int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
 int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
                    void* stream) {
     if (n && (!frames || !off || !len)) return EINVAL;
+    if (frames_bytes > DK_RX_MAX_BLOB) return EINVAL;
     if (n == 0) return 0;
     // Persistent grid on the current device, same schedule rule as the receive kernel (launch_batch).
     static thread_local int dev_cached = -1;
@@ -455,7 +456,7 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
     }
     dk::TxParams p{frames, frames_bytes, off, len, n, frames_bytes / n >= 1024 ? 1u : 0u};
     uint32_t per_cu = std::min<uint32_t>(occ, p.sched ? 3u : 4u);
-    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 2);  // tuning
+    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);  // tuning
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
     return dk_launch_tx(p, grid, stream);

@@ -85,20 +85,6 @@ __device__ __forceinline__ uint32_t block_sum_masked(uint32_t a, uint32_t b, uin
     return hsum2(d & bytes_mask(clamp4(lo - 12), clamp4(hi - 12)), acc);
 }
 
-// Streaming 16-byte load of once-read frame bytes (nontemporal by default: +3-4 % on C2/C4).
-__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
-#if DK_NT_LOADS
-    uint4 v;
-    v.x = __builtin_nontemporal_load(&p->x);
-    v.y = __builtin_nontemporal_load(&p->y);
-    v.z = __builtin_nontemporal_load(&p->z);
-    v.w = __builtin_nontemporal_load(&p->w);
-    return v;
-#else
-    return *p;
-#endif
-}
-
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 // x mod 0xFFFF in [0, 0xFFFE].
 __device__ __forceinline__ uint32_t mod_ffff(uint32_t x) {
@@ -341,21 +327,33 @@ __device__ __noinline__ uint32_t tcp_options(const uint8_t* o, uint32_t n) {
     return 0;
 }
 
-// Open-addressing probe of the device socket table (see rx_common.h).
+// Open-addressing probe of the device socket table (see rx_common.h), split so that the first slot's load can be issued
+// as soon as the key is parsed and consumed after the checksum work (its L2 latency is otherwise exposed per chunk:
+// -17 % on IMIX without the probe).
+struct ProbeKey {
+    uint32_t kind, lip, rip, lport_rport;
+};
+__device__ __forceinline__ uint32_t probe_slot(const RxParams& P, const ProbeKey& k) {
+    return flow_hash(k.kind, k.lip, k.rip, k.lport_rport) & P.table_mask;
+}
+__device__ __forceinline__ uint32_t probe_finish(const RxParams& P, const ProbeKey& k, uint32_t h, uint4 s) {
+    const uint4* T = reinterpret_cast<const uint4*>(P.table);
+    for (uint32_t i = 0; i <= P.table_mask; i++) {
+        if (s.x == 0) break;
+        if ((s.x >> 24) == k.kind && s.y == k.lip && s.z == k.rip && s.w == k.lport_rport) return s.x & 0xFFFFFFu;
+        h = (h + 1) & P.table_mask;
+        s = T[h];
+    }
+    return DK_FLOW_NONE;
+}
 __device__ __forceinline__ uint32_t probe(const RxParams& P, uint32_t kind, uint32_t lip, uint32_t rip,
                                           uint32_t lport_rport) {
-    const uint4* T = reinterpret_cast<const uint4*>(P.table);
-    uint32_t h = flow_hash(kind, lip, rip, lport_rport) & P.table_mask;
+    const ProbeKey k{kind, lip, rip, lport_rport};
+    const uint32_t h = probe_slot(P, k);
 #ifdef DK_ABL_NOPROBE  // ablation (tuning only): no table load
     return h & 1023u;
 #endif
-    for (uint32_t i = 0; i <= P.table_mask; i++) {
-        const uint4 s = T[h];
-        if (s.x == 0) break;
-        if ((s.x >> 24) == kind && s.y == lip && s.z == rip && s.w == lport_rport) return s.x & 0xFFFFFFu;
-        h = (h + 1) & P.table_mask;
-    }
-    return DK_FLOW_NONE;
+    return probe_finish(P, k, h, reinterpret_cast<const uint4*>(P.table)[h]);
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -370,57 +368,45 @@ struct CoopSlot {
     bool has;
 };
 
-#ifndef DK_BUFFER_LOADS
-#define DK_BUFFER_LOADS 1  // frame bytes by buffer_load_dwordx4 (SGPR resource + 32-bit lane offset) vs global_load
-#endif
-// Frame-blob granule loads. buffer_load_dwordx4 with the nontemporal policy streams ~12 % faster than
-// global_load_dwordx4 on gfx950 (dk_diag_read_probe modes 6 vs 3: 6.87 vs 6.09 TB/s on one box) and needs one offset
-// VGPR instead of a 64-bit address; the blob is < 4 GiB (dk_rx.h), so 32-bit offsets cover it.
+// Frame-blob granule loads: buffer_load_dwordx4 (SGPR resource + 32-bit lane offset). With the nontemporal policy it
+// streams ~12 % faster than global_load_dwordx4 on gfx950 (dk_diag_read_probe modes 6 vs 3), needs one offset VGPR
+// instead of a 64-bit address, and its range check is the phase-B mask: the resource covers the blob rounded up to
+// 16 bytes (a granule holding a frame byte is loaded whole; it never crosses a page), so a load at kOob returns zeros
+// without touching memory — no exec masking, no branch around each load. Blobs are <= DK_RX_MAX_BLOB (dk_rx.h).
+constexpr uint32_t kOob = 0xFFFFFFF0u;
 struct Blob {
-#if DK_BUFFER_LOADS
     __amdgpu_buffer_rsrc_t rs;
-    __device__ __forceinline__ explicit Blob(const uint8_t* frames)
-        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(frames), 0, 0xFFFFFFFF, 0x00020000)) {}
+    __device__ __forceinline__ Blob(const uint8_t* frames, uint64_t frames_bytes)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(frames), 0,
+                                               (int)(uint32_t)((frames_bytes + 15) & ~15ull), 0x00020000)) {}
     template <bool kNt>
     __device__ __forceinline__ uint4 ld(uint32_t byte_off) const {
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, kNt ? 2 : 0);
         return make_uint4(r[0], r[1], r[2], r[3]);
     }
-#else
-    const uint8_t* f;
-    __device__ __forceinline__ explicit Blob(const uint8_t* frames) : f(frames) {}
-    template <bool kNt>
-    __device__ __forceinline__ uint4 ld(uint32_t byte_off) const {
-        const uint4* p = reinterpret_cast<const uint4*>(f + byte_off);
-        return kNt ? ld_stream(p) : *p;
-    }
-#endif
 };
 
-// Strides of 5 and 3 uint4 keep the owner-lane ds_read_b128 conflict-free (compact 4/2 strides: DESIGN.md §8).
-constexpr uint32_t kHdrStride = 5, kTailStride = 3;
+// Strides of 5 uint4 keep the owner-lane ds_read_b128 conflict-free (compact 4: DESIGN.md §8).
+constexpr uint32_t kHdrStride = 5;
 struct WaveLds {
-    uint2 rec[64];         // phase B: per rank {owner lane | blocks << 8, offset of the frame's 16-byte base}
-    uint32_t csum[64];     // phase B: whole-frame LE-half sums by owner lane
-    uint4 hdr[64][kHdrStride];    // phase B -> C: the first 5 blocks of each big frame (bytes [0, 64) + shift)
-    uint4 tail[64][kTailStride];  // phase B -> C: the last two 16-byte blocks of each big frame
+    uint2 rec[64];              // phase B: per rank {owner lane | granules << 8, offset of the frame's first granule}
+    uint32_t csum[64];          // phase B: whole-frame LE-half sums by owner lane
+    uint4 hdr[64][kHdrStride];  // phase B -> C: granules 0..4 of each big frame (bytes [0, 64) + shift)
+    uint4 tail[64];             // phase B -> C: the last granule of each big frame
 };
 typedef __attribute__((address_space(3))) void lds_void;
 
 
-// The bytes of one 64-frame chunk (phases A and B), shared by the RX and TX kernels. Every lane of the wave calls it
-// (phase B is wave-cooperative).
+// The bytes of one 64-frame chunk (phases A and B), shared by the RX and TX kernels:
 //   Phase A (lane): descriptor; frames of <= 64 bytes load their bytes straight into registers.
 //   Phase B (quarter-wave per frame, 4 frames per wave per round): frames of > 64 bytes are streamed whole, once, by
-//     16 lanes (kCoopU x dwordx4 in flight each): blocks summed with v_dot2_u32_u16, the header window and the last
-//     32 bytes deposited in LDS for the owner lane, the quarter's sum reduced by a DPP row scan. Reading each frame in
+//     16 lanes (kCoopU x dwordx4 in flight each): granules summed with v_dot2_u32_u16, the header window and the last
+//     granule deposited in LDS for the owner lane, the quarter's sum reduced by a DPP row scan. Reading each frame in
 //     one contiguous pass keeps DRAM rows open (a separate 64-byte header read per frame cost 8 %).
-// Any even frame address takes this vector path: blocks are the 16-byte granules from a = f - sh (sh = f mod 16, even,
+// Any even frame address takes this vector path: granules are the 16-byte blocks from a = f - sh (sh = f mod 16, even,
 // so the frame's 16-bit word grid is the granules' grid), loaded whole (a granule never crosses a page, so reading
 // its bytes outside the frame cannot fault; they are masked or subtracted out of every sum). Odd addresses take the
 // byte path.
-// On return the owner lane holds frame bytes [0, 64) in C.R (realigned when sh != 0) and, for big frames, the LE-half
-// sum of frame bytes [0, 16 * nblk - sh) in C.fsum and the last two granules in W.tail[lane].
 struct Chunk {
     RegAcc R;       // frame bytes [0, 64) (bytes past the frame end are not defined)
     uint32_t fsum;  // big frames: LE-half sum from the frame start to the end of the last granule
@@ -448,142 +434,201 @@ __device__ __forceinline__ void realign(uint32_t (&w)[16], const uint32_t (&x)[4
     for (int k = 0; k < 16; k++) w[k] = __builtin_amdgcn_alignbyte(u[k + 1], u[k], b);
 }
 
-// kShift = false: only 16-byte aligned frames take the vector path (others the byte path); the receive kernel's
-// instantiation for batches the caller flags DK_RX_BATCH_ALIGNED16, which then needs no realignment code and fewer
-// registers.
+// Phase A facts of one lane's frame, from its descriptor. kShift = false: only 16-byte aligned frames take the vector
+// path (others the byte path); the receive kernel's instantiation for batches the caller flags DK_RX_BATCH_ALIGNED16,
+// which then needs no realignment code and fewer registers.
+template <bool kShift>
+struct FrameDesc {
+    bool inb, vec, big;  // descriptor in bounds; even address (vector path); streamed by a quarter-wave
+    uint32_t sh;         // f - a, even (a = granule base)
+    uint32_t span;       // bytes from a to the frame end
+    uint32_t nblk;       // big frames: granules covering [a, f + len)
+    __device__ __forceinline__ FrameDesc(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t off,
+                                         uint32_t len) {
+        inb = live && (uint64_t)off + len <= frames_bytes;
+        const uint32_t fmod = (uint32_t)reinterpret_cast<uintptr_t>(frames + off) & 15u;
+        sh = kShift ? fmod : 0u;
+        vec = inb && (kShift ? (fmod & 1u) == 0 : fmod == 0);
+        span = sh + len;
+        big = vec && span > 64;
+        nblk = big ? (span + 15) >> 4 : 0;
+    }
+};
+
+// Phase A, small frames (<= 64 bytes from the granule base): straight into the register window.
+template <bool kShift>
+__device__ __forceinline__ void small_load(const FrameDesc<kShift>& F, const Blob& B, uint32_t off, RegAcc& R) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (F.vec && !F.big && (uint32_t)(16 * k) < F.span) q = B.template ld<false>(off - F.sh + 16 * k);
+        R.w[4 * k + 0] = q.x;
+        R.w[4 * k + 1] = q.y;
+        R.w[4 * k + 2] = q.z;
+        R.w[4 * k + 3] = q.w;
+    }
+}
+
+// ---------------- Phase B: whole-frame quarter-wave streams ----------------
+// Every frame of > 64 bytes is streamed once, whole, by 16 lanes. Lane l16 of a quarter-wave loads granules
+// b = 96 it + 16 u + l16 (u < kCoopU) of its frame, in address order; slots past the frame load at kOob (zeros): no
+// exec masking, no branch around a load. The header window (granules 0..4) is lanes 0..4's first load; the last
+// granule (nb - 1) is stored by the lane that loads it; both go to LDS for the owner lane, with the quarter's sum
+// (DPP row scan). A step = kRoundsPerStep rounds of 4 frames, all loads in flight together.
+struct CoopPlan {  // wave-uniform
+    uint32_t ncoop;  // big frames in the chunk
+    uint32_t maxit;  // iterations per round (1 unless a frame exceeds kCoopSpan granules, i.e. > 1536 bytes)
+};
+struct CoopStep {
+    CoopSlot sl[kRoundsPerStep];
+    uint4 d[kRoundsPerStep][kCoopU];
+};
+
+// Per-rank records of the chunk's big frames in W.rec; wave-uniform plan. Ends with a wave barrier.
+template <bool kShift>
+__device__ __forceinline__ CoopPlan coop_plan(const FrameDesc<kShift>& F, uint32_t lane, uint32_t off, WaveLds& W) {
+    CoopPlan pl;
+    const uint64_t cm = __ballot(F.big);
+    pl.ncoop = (uint32_t)__popcll(cm);
+    pl.maxit = 1;
+    if (pl.ncoop == 0) return pl;
+    if (F.big) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+        W.rec[rank] = make_uint2(lane | (F.nblk << 8), off - F.sh);  // one ds_read_b64 per round
+    }
+    if (__ballot(F.nblk > kCoopSpan)) {
+        uint32_t mx = F.nblk;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+        pl.maxit = __builtin_amdgcn_readfirstlane((mx - 1) / kCoopSpan + 1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return pl;
+}
+
+// Slots of step r (rounds r .. r + kRoundsPerStep - 1) and the loads of its iteration 0.
+__device__ __forceinline__ void coop_issue(const CoopPlan& pl, uint32_t r, uint32_t lane, const WaveLds& W,
+                                           const Blob& B, CoopStep& S, uint32_t it) {
+    const uint32_t q = lane >> 4, l16 = lane & 15;
+    if (it == 0) {
+#pragma unroll
+        for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+            const uint32_t k = (r + h) * 4 + q;
+            S.sl[h].has = k < pl.ncoop;
+            const uint2 rec = S.sl[h].has ? W.rec[k] : make_uint2(0, 0);
+            S.sl[h].j = rec.x & 0xFFu;
+            S.sl[h].nb = rec.x >> 8;  // 0 for an empty slot: every load is then out of range
+            S.sl[h].boff = rec.y;
+            S.sl[h].acc = 0;
+        }
+    }
+    const uint32_t b0 = it * kCoopSpan + l16;
+#pragma unroll
+    for (uint32_t h = 0; h < kRoundsPerStep; h++)
+#pragma unroll
+        for (uint32_t u = 0; u < kCoopU; u++) {
+            const uint32_t b = b0 + 16 * u;
+            S.d[h][u] = B.template ld<DK_NT_LOADS != 0>(b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob);
+        }
+}
+
+template <bool kShift>
+__device__ __forceinline__ void coop_consume(CoopStep& S, WaveLds& W, uint32_t lane, uint32_t it) {
+    constexpr uint32_t kHdrGran = kShift ? 5u : 4u;  // header granules the owner lane needs
+    const uint32_t l16 = lane & 15, b0 = it * kCoopSpan + l16;
+#pragma unroll
+    for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+#pragma unroll
+        for (uint32_t u = 0; u < kCoopU; u++) {
+            S.sl[h].acc = block_sum(S.d[h][u], S.sl[h].acc);
+            if (b0 + 16 * u + 1 == S.sl[h].nb) W.tail[S.sl[h].j] = S.d[h][u];  // nb == 0: never
+        }
+        if (S.sl[h].has && it == 0 && l16 < kHdrGran) W.hdr[S.sl[h].j][l16] = S.d[h][0];
+    }
+}
+
+// Finish step r whose iteration-0 loads are in flight in S: consume them, run the remaining iterations, reduce.
+template <bool kShift>
+__device__ __forceinline__ void coop_finish(const CoopPlan& pl, uint32_t r, uint32_t lane, WaveLds& W, const Blob& B,
+                                            CoopStep& S) {
+    coop_consume<kShift>(S, W, lane, 0);
+    for (uint32_t it = 1; it < pl.maxit; it++) {
+        coop_issue(pl, r, lane, W, B, S, it);
+        coop_consume<kShift>(S, W, lane, it);
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+        // Quarter = DPP row of 16 lanes: inclusive row scan by row_shr 1/2/4/8; lane 15 holds the sum.
+        uint32_t acc = S.sl[h].acc;
+        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xF, 0xF, false);
+        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x112, 0xF, 0xF, false);
+        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x114, 0xF, 0xF, false);
+        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x118, 0xF, 0xF, false);
+        if (S.sl[h].has && (lane & 15) == 15) W.csum[S.sl[h].j] = acc;
+    }
+}
+
+// After the last step: the owner lane's whole-frame sum and header window (big frames), then frames not on a 16-byte
+// boundary drop the granule bytes before the frame from the sum and shift the window into frame coordinates.
+template <bool kShift>
+__device__ __forceinline__ void coop_gather(const FrameDesc<kShift>& F, const CoopPlan& pl, uint32_t lane,
+                                            const WaveLds& W, Chunk& C) {
+    RegAcc& R = C.R;
+    C.fsum = 0;
+    if (pl.ncoop) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (F.big) {
+            C.fsum = W.csum[lane];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint4 h = W.hdr[lane][k];
+                R.w[4 * k + 0] = h.x;
+                R.w[4 * k + 1] = h.y;
+                R.w[4 * k + 2] = h.z;
+                R.w[4 * k + 3] = h.w;
+            }
+        }
+    }
+    if (kShift && __ballot(F.vec && F.sh != 0)) {
+        uint32_t x[4] = {0, 0, 0, 0};
+        if (F.big && F.sh != 0) {
+            const uint4 h = W.hdr[lane][4];
+            x[0] = h.x; x[1] = h.y; x[2] = h.z; x[3] = h.w;
+            C.fsum -= block_sum_masked(R.w[0], R.w[1], R.w[2], R.w[3], 0, (int)F.sh, 0);
+        }
+        if (F.vec && F.sh != 0) realign(R.w, x, F.sh);
+    }
+    C.sh = F.sh;
+    C.inb = F.inb;
+    C.vec = F.vec;
+    C.big = F.big;
+    C.nblk = F.nblk;
+}
+
+// Phases A and B of one 64-frame chunk, shared by the RX and TX kernels; every lane of the wave calls it.
+// On return the owner lane holds frame bytes [0, 64) in C.R (realigned when sh != 0) and, for big frames, the LE-half
+// sum of frame bytes [0, 16 * nblk - sh) in C.fsum and the last granule in W.tail[lane].
 template <bool kShift>
 __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t lane,
                                              WaveLds& W, uint32_t off, uint32_t len, Chunk& C) {
-    // ---------------- Phase A: descriptor (loaded by the caller); small frames into registers ----------------
-    const bool inb = live && (uint64_t)off + len <= frames_bytes;
-    const uint8_t* f = frames + off;
-    const uint32_t fmod = (uint32_t)reinterpret_cast<uintptr_t>(f) & 15u;
-    const uint32_t sh = kShift ? fmod : 0u;
-    const bool vec = inb && (kShift ? (fmod & 1u) == 0 : fmod == 0);  // vector path
-    const uint32_t span = sh + len;                        // bytes from the granule base a = f - sh
-    const bool big = vec && span > 64;                     // streamed by a quarter-wave
-    const uint32_t nblk = big ? (span + 15) >> 4 : 0;      // granules covering [a, f + len)
-
-    RegAcc& R = C.R;
-    const Blob B(frames);
-    {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            uint4 q = make_uint4(0, 0, 0, 0);
-            if (vec && !big && (uint32_t)(16 * k) < span) q = B.template ld<false>(off - sh + 16 * k);
-            R.w[4 * k + 0] = q.x;
-            R.w[4 * k + 1] = q.y;
-            R.w[4 * k + 2] = q.z;
-            R.w[4 * k + 3] = q.w;
-        }
+    const FrameDesc<kShift> F(frames, frames_bytes, live, off, len);
+    const Blob B(frames, frames_bytes);
+    small_load(F, B, off, C.R);
+    const CoopPlan pl = coop_plan(F, lane, off, W);
+    for (uint32_t r = 0; r * 4 < pl.ncoop; r += kRoundsPerStep) {
+        CoopStep S;
+        coop_issue(pl, r, lane, W, B, S, 0);
+        coop_finish<kShift>(pl, r, lane, W, B, S);
     }
-
-    // ---------------- Phase B: whole-frame quarter-wave streams ----------------
-    uint32_t& fsum = C.fsum;  // big frames: LE-half sum over blocks [0, nblk)
-    fsum = 0;
-    {
-        const uint64_t cm = __ballot(big);
-        const uint32_t ncoop = (uint32_t)__popcll(cm);
-        if (ncoop) {
-            if (big) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-                W.rec[rank] = make_uint2(lane | (nblk << 8), off - sh);  // per-rank record: one ds_read_b64 per round
-            }
-            // Wave-uniform iterations per round (1 unless a frame exceeds kCoopSpan blocks, i.e. > 1536 bytes).
-            uint32_t maxit = 1;
-            if (__ballot(nblk > kCoopSpan)) {
-                uint32_t mx = nblk;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
-                maxit = __builtin_amdgcn_readfirstlane((mx + kCoopSpan - 1) / kCoopSpan);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t q = lane >> 4, l16 = lane & 15;
-            for (uint32_t r = 0; r * 4 < ncoop; r += kRoundsPerStep) {
-                // kRoundsPerStep rounds per step: their loads are all in flight together (kRoundsPerStep * 4
-                // consecutive frames per wave, one contiguous region of the blob).
-                CoopSlot sl[kRoundsPerStep];
-#pragma unroll
-                for (uint32_t h = 0; h < kRoundsPerStep; h++) {
-                    const uint32_t k = (r + h) * 4 + q;
-                    sl[h].has = k < ncoop;
-                    const uint2 rec = sl[h].has ? W.rec[k] : make_uint2(0, 0);
-                    sl[h].j = rec.x & 0xFFu;
-                    sl[h].nb = rec.x >> 8;
-                    sl[h].boff = rec.y;
-                    sl[h].acc = 0;
-                }
-                for (uint32_t it = 0; it < maxit; it++) {
-                    const uint32_t b0 = it * kCoopSpan + l16;
-                    uint4 d[kRoundsPerStep][kCoopU];
-#pragma unroll
-                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
-#pragma unroll
-                        for (uint32_t u = 0; u < kCoopU; u++) {
-                            const uint32_t b = b0 + 16 * u;
-                            d[h][u] = b < sl[h].nb ? B.template ld<DK_NT_LOADS != 0>(sl[h].boff + 16 * b) : make_uint4(0, 0, 0, 0);
-                        }
-#pragma unroll
-                    for (uint32_t h = 0; h < kRoundsPerStep; h++)
-#pragma unroll
-                        for (uint32_t u = 0; u < kCoopU; u++) {
-                            const uint32_t b = b0 + 16 * u;
-                            sl[h].acc = block_sum(d[h][u], sl[h].acc);
-                            // header window: 4 granules, a 5th when frames may start off a 16-byte boundary
-                            if (sl[h].has && b < (kShift ? 5u : 4u)) W.hdr[sl[h].j][b] = d[h][u];  // 5 <= nb
-                            if (b < sl[h].nb && b + 2 >= sl[h].nb) W.tail[sl[h].j][b + 2 - sl[h].nb] = d[h][u];
-                        }
-                }
-#pragma unroll
-                for (uint32_t h = 0; h < kRoundsPerStep; h++) {
-                    // Quarter = DPP row of 16 lanes: inclusive row scan by row_shr 1/2/4/8; lane 15 holds the sum.
-                    uint32_t acc = sl[h].acc;
-                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xF, 0xF, false);
-                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x112, 0xF, 0xF, false);
-                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x114, 0xF, 0xF, false);
-                    acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x118, 0xF, 0xF, false);
-                    if (sl[h].has && l16 == 15) W.csum[sl[h].j] = acc;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (big) {
-                fsum = W.csum[lane];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint4 h = W.hdr[lane][k];
-                    R.w[4 * k + 0] = h.x;
-                    R.w[4 * k + 1] = h.y;
-                    R.w[4 * k + 2] = h.z;
-                    R.w[4 * k + 3] = h.w;
-                }
-            }
-        }
-    }
-    // Frames not on a 16-byte boundary: drop the granule bytes before the frame from the whole-frame sum and shift
-    // the header window into frame coordinates (skipped when the whole wave is aligned).
-    if (kShift && __ballot(vec && sh != 0)) {
-        uint32_t x[4] = {0, 0, 0, 0};
-        if (big && sh != 0) {
-            const uint4 h = W.hdr[lane][4];
-            x[0] = h.x; x[1] = h.y; x[2] = h.z; x[3] = h.w;
-            fsum -= block_sum_masked(R.w[0], R.w[1], R.w[2], R.w[3], 0, (int)sh, 0);
-        }
-        if (vec && sh != 0) realign(R.w, x, sh);
-    }
-    C.sh = sh;
-    C.inb = inb;
-    C.vec = vec;
-    C.big = big;
-    C.nblk = nblk;
+    coop_gather(F, pl, lane, W, C);
 }
 
 // LE-half sum of frame bytes [34, E) on the fast path (IHL == 5), from what stream_chunk left: the register window
-// for small frames; for big frames sum(all blocks) - sum[0, 34) - sum[E, 16 * nblk), the last two blocks being in
+// for small frames; for big frames sum(all granules) - sum[0, 34) - sum[E, 16 * nblk), the last granule being in
 // LDS; a direct byte sum when IPv4 total_length ends more than 32 bytes before the last block (rare; sets resum).
 __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& W, uint32_t lane, const uint8_t* f,
                                                  int E, bool& resum) {
@@ -593,14 +638,13 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& 
         const uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
         return block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
     }
-    if ((int)(16 * C.nblk - C.sh) - E <= 32) {
+    if ((int)(16 * C.nblk - C.sh) - E <= 16) {
         uint32_t pre = block_sum(make_uint4(R.w[0], R.w[1], R.w[2], R.w[3]), 0);
         pre = block_sum(make_uint4(R.w[4], R.w[5], R.w[6], R.w[7]), pre);
         pre += R.w[8] & 0xFFFFu;
-        const int t0 = (int)(16 * C.nblk - C.sh) - 32;  // frame offset of the first tail byte
-        const uint4 a = W.tail[lane][0], c = W.tail[lane][1];
-        uint32_t post = block_sum_masked(a.x, a.y, a.z, a.w, E - t0, 16, 0);
-        post = block_sum_masked(c.x, c.y, c.z, c.w, E - t0 - 16, 16, post);
+        const int t0 = (int)(16 * C.nblk - C.sh) - 16;  // frame offset of the last granule's first byte
+        const uint4 a = W.tail[lane];
+        const uint32_t post = block_sum_masked(a.x, a.y, a.z, a.w, E - t0, 16, 0);
         return C.fsum - pre - post;
     }
     resum = true;
@@ -631,20 +675,26 @@ struct Rec {
 // L2-resident window instead recovers it all). The staged kernels hold the last kStageK chunks' results in registers
 // and store them together, so a wave's writes leave in one burst per kStageK chunks (at exit for C2 at 3 WG/CU).
 #ifndef DK_STAGE_K
-#define DK_STAGE_K 8
+#define DK_STAGE_K 6
 #endif
 #ifndef DK_MIN_WAVES_STAGED
-#define DK_MIN_WAVES_STAGED 3  // 8 x 6 staged words fit in 168 VGPRs without spills
+#define DK_MIN_WAVES_STAGED 3  // 6 x 6 staged words fit in 168 VGPRs without spills
 #endif
 constexpr int kStageK = DK_STAGE_K;
 
+// Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
+// results (stored, or handed back in rec for staging).
 template <bool kShift, bool kStage>
-__device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
-                                        uint32_t off, uint32_t len, uint32_t& v_out, uint32_t& fid_out, Rec& rec) {
-    Chunk C;
-    stream_chunk<kShift>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+__device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
+                                          uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
+                                          uint32_t& fid_out, Rec& rec) {
 #ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
-    if (live) P.res.meta[i] = C.fsum ^ C.R.w[3] ^ C.R.w[9];
+#ifdef DK_DIAG_NO_STORE
+    if (live && (C.fsum ^ C.R.w[3] ^ C.R.w[9]) == 0x9E3779B1u)
+#else
+    if (live)
+#endif
+        P.res.meta[i] = C.fsum ^ C.R.w[3] ^ C.R.w[9];
     v_out = kNone;
     fid_out = DK_FLOW_NONE;
     return;
@@ -667,12 +717,18 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
         L.v = DK_V_BAD_DESC;
     } else if (fast) {
         parse_fast(R, len, P, L);
-        if (L.need) L.lsum = seg_sum_fast(C, W, lane, f, (int)L.E, resum);
     } else {
-        const MemAcc M{f};
-        parse_headers(M, len, P, L);
-        if (L.need) L.lsum = M.sum_le16(L.S, L.E);
+        parse_headers(MemAcc{f}, len, P, L);
     }
+    // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
+    const bool pend4 = L.v == kPendTcp || L.v == kPendUdp;
+    const ProbeKey k1 = L.v == kPendTcp
+                            ? ProbeKey{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)}
+                            : ProbeKey{DK_FLOW_UDP, P.local_ip, 0u, L.ports >> 16};
+    const uint32_t h1 = probe_slot(P, k1);
+    uint4 s1 = make_uint4(0, 0, 0, 0);
+    if (pend4) s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+    if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
 
     uint32_t fid = DK_FLOW_NONE;
     if (L.v == kPendIcmp) {
@@ -700,12 +756,12 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
         const uint32_t sport = L.ports & 0xFFFFu, dport = L.ports >> 16;
         if (L.v == kPendTcp) {
             // SocketId::Active(local=(local_ip, dport), remote=(src, sport)), then Passive(local) (tcp/peer.rs:241-251)
-            fid = probe(P, DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, dport | (sport << 16));
+            fid = probe_finish(P, k1, h1, s1);  // Active(local, remote)
             if (fid == DK_FLOW_NONE) fid = probe(P, DK_FLOW_TCP_PASSIVE, P.local_ip, 0u, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
         } else if (L.v == kPendUdp) {
             // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
-            fid = probe(P, DK_FLOW_UDP, P.local_ip, 0u, dport);
+            fid = probe_finish(P, k1, h1, s1);  // (local_ip, port)
             if (fid == DK_FLOW_NONE) fid = probe(P, DK_FLOW_UDP, 0u, 0u, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
         }
@@ -759,40 +815,43 @@ __device__ __forceinline__ void rx_tile(const RxParams& P, uint32_t i, bool live
     fid_out = fid;
 }
 
-// Store the nst most recent staged chunks (stg[k] belongs to frame i_last - k * cstep).
-__device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)[kStageK], uint32_t nst,
-                                             uint32_t i_last, uint32_t cstep, uint32_t f1) {
-#pragma unroll
-    for (int k = kStageK - 1; k >= 0; k--) {
-        if ((uint32_t)k >= nst) continue;
-        const uint32_t i = i_last - (uint32_t)k * cstep;
-        if (i >= f1) continue;
-        st_res(P.res.meta + i, stg[k].meta);
-        st_res(P.res.src_ip + i, stg[k].src);
-        st_res(P.res.dst_ip + i, stg[k].dst);
-        st_res(P.res.ports + i, stg[k].ports);
-        st_res(P.res.payload + i, stg[k].pay);
-        st_res(P.res.flow_id + i, stg[k].fid);
-    }
-}
-
-// Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). A wave's chunk c holds frames
-// i = c + lane_off (lane_off = lane unless noted), for c = f0, f0 + step, ... below f1; lanes with i >= f1 idle.
-//   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame) and walks it in 64-frame chunks
-//            (no tile quantization);
+// Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). Chunk k of a wave holds the
+// frames i = c_k + lane_off (lane_off = lane unless noted) with i < lim_k:
 //   sched 0: round-robin 256-frame tiles, wave wv of workgroup b takes frames [t * 256 + 64 wv, +64) of tiles
-//            t = b, b + G, ... (the grid sweeps one contiguous window of the blob; best for small/mixed frames);
+//            t = b, b + G, ... (the grid sweeps one contiguous window of the blob);
+//   sched 3: sched 0 for the full rounds, then the frames of the last, partial round split evenly over all waves (one
+//            short chunk each) instead of whole 64-frame chunks for some waves and none for the rest;
+//   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame), walked in 64-frame chunks;
 //   sched 2: phase-B-step interleave: lane group g = lane / 8 of wave gw (of nw) takes the 8 consecutive frames
-//            c + 8 (g * nw + gw) + [0, 8), c = 0, 64 nw, ... A phase-B step streams one lane group, so at any moment
-//            the whole grid reads one contiguous window of ~nw * 8 frames (the read probe's sweep) instead of nw
-//            separate streams.
+//            c + 8 (g * nw + gw) + [0, 8), c = 0, 64 nw, ...: at any moment the whole grid reads one window of
+//            ~nw * 8 frames.
 struct WaveRange {
     uint32_t f0, f1, step, lane_off;
+    uint32_t nfull, t0, t1;  // sched 3: chunks k < nfull are full; chunk nfull is [t0, t1)
+    bool tail;
+    // Chunk k: false when the wave has no chunk k.
+    __device__ __forceinline__ bool chunk(uint32_t k, uint32_t& c, uint32_t& lim) const {
+        if (tail) {
+            if (k < nfull) {
+                c = f0 + k * step;
+                lim = c + 64;
+                return true;
+            }
+            c = t0;
+            lim = t1;
+            return k == nfull && t0 < t1;
+        }
+        c = f0 + k * step;
+        lim = f1;
+        return c < f1;
+    }
 };
 __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint32_t wv, uint32_t lane) {
     WaveRange r;
     const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
     r.lane_off = lane;
+    r.tail = false;
+    r.nfull = r.t0 = r.t1 = 0;
     if (sched == 1) {
         r.f0 = (uint32_t)(((uint64_t)n * gw) / nw);
         r.f1 = (uint32_t)(((uint64_t)n * (gw + 1)) / nw);
@@ -803,11 +862,38 @@ __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint
         r.step = 64 * nw;
         r.lane_off = (lane >> 3) * 8 * nw + (lane & 7);
     } else {
-        r.f0 = blockIdx.x * kBlock + wv * 64;
+        r.f0 = gw * 64;  // == blockIdx.x * kBlock + wv * 64
         r.f1 = n;
-        r.step = gridDim.x * kBlock;
+        r.step = 64 * nw;
+        if (sched == 3) {
+            r.tail = true;
+            r.nfull = n / (64 * nw);
+            const uint32_t base = r.nfull * 64 * nw, rem = n - base;
+            r.t0 = base + (uint32_t)(((uint64_t)rem * gw) / nw);
+            r.t1 = base + (uint32_t)(((uint64_t)rem * (gw + 1)) / nw);
+        }
     }
     return r;
+}
+
+// Store the nst most recent staged chunks: stg[q] holds the results of chunk k_last - q (kNoRec marks idle lanes).
+constexpr uint32_t kNoRec = 0xFFFFFFFFu;  // never a meta word (verdicts < 64)
+__device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)[kStageK], uint32_t nst,
+                                             const WaveRange& r, uint32_t k_last) {
+#pragma unroll
+    for (int q = kStageK - 1; q >= 0; q--) {
+        if ((uint32_t)q >= nst) continue;
+        uint32_t c, lim;
+        (void)r.chunk(k_last - (uint32_t)q, c, lim);
+        if (stg[q].meta == kNoRec) continue;
+        const uint32_t i = c + r.lane_off;
+        st_res(P.res.meta + i, stg[q].meta);
+        st_res(P.res.src_ip + i, stg[q].src);
+        st_res(P.res.dst_ip + i, stg[q].dst);
+        st_res(P.res.ports + i, stg[q].ports);
+        st_res(P.res.payload + i, stg[q].pay);
+        st_res(P.res.flow_id + i, stg[q].fid);
+    }
 }
 
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
@@ -835,40 +921,56 @@ void dk_rx_kernel(RxParams P) {
     __syncthreads();
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
-    const uint32_t f0 = r.f0, f1 = r.f1, cstep = r.step;
     Rec stg[kStage ? kStageK : 1];
     uint32_t nstg = 0;  // wave-uniform
+    uint32_t c, lim, nc, nlim;
+    bool have = r.chunk(0, c, lim);
     uint32_t noff = 0, nlen = 0;  // descriptors of this wave's next chunk
-    if (f0 + r.lane_off < f1) {
-        noff = P.off[f0 + r.lane_off];
-        nlen = P.len[f0 + r.lane_off];
+    if (have && c + r.lane_off < lim) {
+        noff = P.off[c + r.lane_off];
+        nlen = P.len[c + r.lane_off];
     }
-    for (uint32_t c = f0; c < f1; c += cstep) {
+    WaveLds& W = s_wave[wv];
+    uint32_t nchunks = 0;
+    for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
+        nchunks = k + 1;
         const uint32_t i = c + r.lane_off;
-        const bool live = i < f1;
+        const bool live = i < lim;
         const uint32_t off = noff, len = nlen;
-        if (i + cstep < f1) {  // prefetch the next chunk's descriptors
-            noff = P.off[i + cstep];
-            nlen = P.len[i + cstep];
+        have = r.chunk(k + 1, nc, nlim);
+        if (have && nc + r.lane_off < nlim) {  // prefetch the next chunk's descriptors
+            noff = P.off[nc + r.lane_off];
+            nlen = P.len[nc + r.lane_off];
         }
         uint32_t v, fid;
         Rec rec;
-        rx_tile<kShift, kStage>(P, i, live, lane, s_wave[wv], off, len, v, fid, rec);
+        rec.meta = kNoRec;
+        Chunk C;
+        stream_chunk<kShift>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+        rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (kStage) {  // shift register of the last kStageK chunks' results; stored when full and at exit
 #pragma unroll
-            for (int k = kStageK - 1; k > 0; k--) stg[k] = stg[k - 1];
+            for (int q = kStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
             stg[0] = rec;
             if (++nstg == kStageK) {
-                flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, i, cstep, f1);
+                flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, k);
                 nstg = 0;
             }
         }
+#ifdef DK_ABL_NOCOUNT  // ablation (tuning only): no flow / verdict counting
+        if (false) {
+#else
         if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
+#endif
             if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
             else if (P.flow_mode == kFlowGlobal)
                 atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
         }
+#ifdef DK_ABL_NOCOUNT
+        if (false) {
+#else
         if (P.res.verdict_counts) {  // one LDS add per distinct verdict per wave
+#endif
             uint64_t todo = __ballot(live);
             while (todo) {
                 const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
@@ -880,12 +982,7 @@ void dk_rx_kernel(RxParams P) {
         }
     }
 
-    if (kStage && nstg) {
-        // the last chunk processed had c_last = f0 + (chunks - 1) * cstep
-        const uint32_t nch = (f1 - f0 + cstep - 1) / cstep;
-        flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, f0 + (nch - 1) * cstep + r.lane_off, cstep,
-                     f1);
-    }
+    if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     __syncthreads();
     if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
         atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
@@ -1043,19 +1140,22 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6;
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
+    uint32_t c, lim, nc, nlim;
+    bool have = r.chunk(0, c, lim);
     uint32_t noff = 0, nlen = 0;
-    if (r.f0 + r.lane_off < r.f1) {
-        noff = P.off[r.f0 + r.lane_off];
-        nlen = P.len[r.f0 + r.lane_off];
+    if (have && c + r.lane_off < lim) {
+        noff = P.off[c + r.lane_off];
+        nlen = P.len[c + r.lane_off];
     }
-    for (uint32_t c = r.f0; c < r.f1; c += r.step) {
+    for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
         const uint32_t i = c + r.lane_off;
         const uint32_t off = noff, len = nlen;
-        if (i + r.step < r.f1) {
-            noff = P.off[i + r.step];
-            nlen = P.len[i + r.step];
+        have = r.chunk(k + 1, nc, nlim);
+        if (have && nc + r.lane_off < nlim) {
+            noff = P.off[nc + r.lane_off];
+            nlen = P.len[nc + r.lane_off];
         }
-        tx_tile(P, i < r.f1, lane, s_wave[wv], off, len);
+        tx_tile(P, i < lim, lane, s_wave[wv], off, len);
     }
 }
 

@@ -112,7 +112,7 @@ def layout(frame_len: np.ndarray, align: int = 64) -> tuple[np.ndarray, int]:
     off = np.zeros(len(frame_len), np.int64)
     np.cumsum(slots[:-1], out=off[1:])
     total = int(off[-1] + slots[-1]) if len(frame_len) else 0
-    assert total <= 2**32, "a batch blob is limited to 4 GiB (u32 offsets)"
+    assert total <= 0xFFFFFF00, "a batch blob is limited to DK_RX_MAX_BLOB = 4 GiB - 256 (u32 offsets)"
     return off.astype(np.uint32), total
 
 

@@ -14,7 +14,8 @@ extern "C" {
  * caller). Used to measure the achievable HBM read bandwidth on the running box. Async on `stream`.
  * mode 0: grid-stride loads; 1: contiguous 8 KiB per wave step; 2: as 1 with nontemporal loads; 3: 16 KiB per wave
  * step, nontemporal; 4/5: 16 KiB per wave step by LDS-DMA (global_load_lds), nontemporal / default policy;
- * 6/7: as 3 with buffer_load_dwordx4 (32-bit offsets: bytes < 4 GiB), nontemporal / default policy.
+ * 6/7: as 3 with buffer_load_dwordx4 (32-bit offsets: bytes < 4 GiB), nontemporal / default policy;
+ * 8: the receive kernel's phase-B pattern alone (1536-byte slots, quarter-waves reading 256-byte runs, nontemporal).
  * Returns 0, EINVAL or EIO. */
 int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode, void* stream);
 

@@ -53,6 +53,10 @@ extern "C" {
                                     instantiation without the realignment path (other frames then take the byte path,
                                     still bit-exact) */
 
+/* Largest frame blob of one batch (bytes): offsets are u32 and the engine keeps 256 bytes of the 32-bit range for its
+ * out-of-range loads. */
+#define DK_RX_MAX_BLOB 0xFFFFFF00ull
+
 /* flow_id value for frames that do not demux to a socket. */
 #define DK_FLOW_NONE 0xFFFFFFFFu
 
@@ -133,7 +137,7 @@ typedef struct dk_flow {
  * For dk_rx_process all pointers are device pointers (HBM-resident batch). */
 typedef struct dk_rx_batch {
     const uint8_t* frames;    /* frame blob base                                                       */
-    uint64_t frames_bytes;    /* blob size in bytes; frames outside it get DK_V_BAD_DESC (<= 4 GiB)    */
+    uint64_t frames_bytes;    /* blob size in bytes (<= DK_RX_MAX_BLOB); frames outside it: DK_V_BAD_DESC */
     const uint32_t* off;      /* [n] byte offset of each frame in the blob                             */
     const uint16_t* len;      /* [n] frame length: Ethernet header included, FCS excluded              */
     uint32_t n;
@@ -184,7 +188,7 @@ int dk_rx_flow_table_set(dk_rx_ctx* ctx, const dk_flow* flows, uint32_t n);
 uint32_t dk_rx_flow_table_size(const dk_rx_ctx* ctx);
 
 /* Process one HBM-resident batch on `stream` (hipStream_t or NULL). Asynchronous: returns after the launch.
- * Returns 0, EINVAL (null required pointer, frames_bytes > 4 GiB) or EIO (launch failure). */
+ * Returns 0, EINVAL (null required pointer, frames_bytes > DK_RX_MAX_BLOB) or EIO (launch failure). */
 int dk_rx_process(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results* res, void* stream);
 
 /* Process a batch that lives in host memory (a NIC ring / raw-socket buffer): chunked pinned-host -> HBM copies,

@@ -6,6 +6,7 @@ import pytest
 
 import frames as F
 from demikernel_amd import Config, FrameBatch, RxEngine, V, VERDICTS, ipv4, synth
+from demikernel_amd.rx import Fail
 from demikernel_amd._native import FLOW_DTYPE
 from oracle.oracle import OraclePeer
 
@@ -101,7 +102,7 @@ def test_random_batches(torch_cuda, mix, hint):
 
 
 @pytest.mark.parametrize("grid", [None, "2", "7"])
-@pytest.mark.parametrize("sched", ["0", "1", "2"])
+@pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("stage", ["0", "1"])
 def test_kernel_variants(torch_cuda, monkeypatch, stage, sched, grid):
     """Both kernel families (result staging on/off) under every wave schedule, with grids small enough that each wave
@@ -171,6 +172,10 @@ def test_bad_descriptors_and_edges(torch_cuda):
     assert VERDICTS[got["meta"][-1] & 0xFF] == "BAD_DESC" and VERDICTS[got["meta"][-2] & 0xFF] == "BAD_DESC"
     # frames_bytes smaller than the blob: the tail frames become BAD_DESC
     check(blob, off, lens, flows, ctx="short blob", frames_bytes=int(off[2]))
+    # a blob above DK_RX_MAX_BLOB (4 GiB - 256) is refused before any launch
+    with pytest.raises(Fail) as e:
+        run_gpu(blob, off, lens, flows, frames_bytes=0xFFFFFF01)
+    assert e.value.errno == 22
 
 
 def test_empty_batch(torch_cuda):

@@ -72,8 +72,8 @@ def main():
     if args.probe or args.probe_one:
         lib = N.load_library()
         nbytes = batch.blob.numel() // 16 * 16
-        for mode in ((1,) if args.probe_one else (3, 4, 6, 7)):
-            for grid in ((1024,) if args.probe_one else (512, 1024, 2048, 3072)):
+        for mode in ((1,) if args.probe_one else (3, 4, 6, 7, 8)):
+            for grid in ((1024,) if args.probe_one else (256, 512, 768, 1024)):
                 scratch = torch.zeros(grid, dtype=torch.int32, device="cuda")
                 s = torch.cuda.current_stream().cuda_stream
 
