@@ -66,6 +66,7 @@ struct RxParams {
     uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave
     uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path
     uint32_t stage;          // launch the instantiation that stages result stores in registers (large frames)
+    uint32_t split;          // launch the split (stream waves / finish waves) kernel (largest frames)
     dk_rx_results res;
 };
 
@@ -82,7 +83,11 @@ struct TxParams {
 }  // namespace dk
 
 // Launchers implemented in rx_kernels.hip (internal symbols, not part of the C ABI).
-int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, bool stage);  // occupancy of dk_rx_kernel per CU (0 on error)
+// Receive kernel families (launch_batch picks one per launch).
+namespace dk {
+constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2;
+}
+int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
 int dk_tx_resident_blocks();  // occupancy of dk_tx_kernel per CU (0 on error)
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream);

@@ -53,7 +53,7 @@ struct dk_rx_ctx {
     uint32_t cu_count = 0;
     uint32_t occ_dyn = ~0u;   // occupancy cache: dynamic LDS bytes -> resident blocks per CU
     uint32_t occ_blocks = 0;
-    uint32_t occ_stage = 0;
+    uint32_t occ_family = ~0u;
     unsigned long long* d_path_stats = nullptr;  // dk_diag path counters (nullptr = off)
 };
 
@@ -131,15 +131,18 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
     // Never more workgroups per CU than the occupancy admits (large socket tables take LDS).
     const uint64_t bytes_per_frame = p.frames_bytes / p.n;
     p.stage = bytes_per_frame >= 128 ? 1u : 0u;
+    p.split = bytes_per_frame >= 1024 ? 1u : 0u;
     if (const char* e = getenv("DK_RX_STAGE")) p.stage = atoi(e) ? 1u : 0u;  // tuning
+    if (const char* e = getenv("DK_RX_SPLIT")) p.split = atoi(e) ? 1u : 0u;  // tuning
     p.sched = 0;
     if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
-    if (c->occ_dyn != dyn || c->occ_stage != p.stage) {
-        c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn, p.stage != 0), 1);
+    const uint32_t family = p.split ? dk::kFamilySplit : p.stage ? dk::kFamilyStaged : dk::kFamilyUnstaged;
+    if (c->occ_dyn != dyn || c->occ_family != family) {
+        c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn, family), 1);
         c->occ_dyn = dyn;
-        c->occ_stage = p.stage;
+        c->occ_family = family;
     }
-    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.stage ? 3u : 4u);
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.split ? 1u : p.stage ? 3u : 4u);
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
     if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
@@ -150,8 +153,8 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         p.flow_scratch = fs.p;
     }
     if (getenv("DK_RX_DEBUG"))
-        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u\n", p.n,
-                ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage);
+        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u\n",
+                p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split);
     return dk_launch_rx(p, grid, stream);
 }
 

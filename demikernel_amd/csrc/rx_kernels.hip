@@ -896,6 +896,30 @@ __device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)
     }
 }
 
+// Per-chunk counters: the delivered frame's flow (packed-u16 LDS histogram, or a u64 global atomic for tables too
+// large for LDS) and one LDS add per distinct verdict per wave.
+__device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32_t lane, uint32_t v, uint32_t fid,
+                                            bool lds_flows, uint32_t* s_flow, uint32_t* s_vh) {
+#ifdef DK_ABL_NOCOUNT  // ablation (tuning only): no flow / verdict counting
+    return;
+#endif
+    if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
+        if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
+        else if (P.flow_mode == kFlowGlobal)
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
+    }
+    if (P.res.verdict_counts) {
+        uint64_t todo = __ballot(live);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
+            const uint64_t m = __ballot(live && v == v0);
+            if (lane == leader) atomicAdd(&s_vh[v0], (uint32_t)__popcll(m));
+            todo &= ~m;
+        }
+    }
+}
+
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
 // per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
@@ -957,29 +981,7 @@ void dk_rx_kernel(RxParams P) {
                 nstg = 0;
             }
         }
-#ifdef DK_ABL_NOCOUNT  // ablation (tuning only): no flow / verdict counting
-        if (false) {
-#else
-        if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
-#endif
-            if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
-            else if (P.flow_mode == kFlowGlobal)
-                atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
-        }
-#ifdef DK_ABL_NOCOUNT
-        if (false) {
-#else
-        if (P.res.verdict_counts) {  // one LDS add per distinct verdict per wave
-#endif
-            uint64_t todo = __ballot(live);
-            while (todo) {
-                const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
-                const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
-                const uint64_t m = __ballot(live && v == v0);
-                if (lane == leader) atomicAdd(&s_vh[v0], (uint32_t)__popcll(m));
-                todo &= ~m;
-            }
-        }
+        count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
     }
 
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
@@ -989,6 +991,109 @@ void dk_rx_kernel(RxParams P) {
     if (lds_flows) {
         uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.flow_words;
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) row[k] = s_flow[k];
+    }
+}
+
+// Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
+// chunk p into LDS buffer p % 2 (header windows, last granules, whole-frame sums) while finish waves 4..7 run phase C
+// of chunk p - 1 from the other buffer; one workgroup barrier per period. The streaming waves never stop for parse,
+// demux, counters or result stores — 4 streaming waves per CU is also the count at which the read probe peaks — and
+// the finish waves stage their results in registers (kSplitStageK chunks, 256 VGPRs at 2 waves/SIMD) for one burst
+// at exit. Stream wave w and finish wave w + 4 walk the same chunk sequence (sched 0 over 4 waves per workgroup).
+constexpr int kSplitBlock = 512;
+#ifndef DK_SPLIT_STAGE_K
+#define DK_SPLIT_STAGE_K 16
+#endif
+constexpr int kSplitStageK = DK_SPLIT_STAGE_K;
+__device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[kSplitStageK], uint32_t nst,
+                                            const WaveRange& r, uint32_t k_last) {
+#pragma unroll
+    for (int q = kSplitStageK - 1; q >= 0; q--) {
+        if ((uint32_t)q >= nst) continue;
+        uint32_t c, lim;
+        (void)r.chunk(k_last - (uint32_t)q, c, lim);
+        if (stg[q].meta == kNoRec) continue;
+        const uint32_t i = c + r.lane_off;
+        st_res(P.res.meta + i, stg[q].meta);
+        st_res(P.res.src_ip + i, stg[q].src);
+        st_res(P.res.dst_ip + i, stg[q].dst);
+        st_res(P.res.ports + i, stg[q].ports);
+        st_res(P.res.payload + i, stg[q].pay);
+        st_res(P.res.flow_id + i, stg[q].fid);
+    }
+}
+
+template <bool kShift>
+__global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P) {
+    __shared__ WaveLds s_buf[2][kWaves];   // [period parity][stream wave]
+    __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6, sw = wv & (kWaves - 1);
+    const bool finisher = wv >= (uint32_t)kWaves;
+    const bool lds_flows = P.flow_mode == kFlowLds;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kSplitBlock) s_vh[k] = 0;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += kSplitBlock) s_flow[k] = 0;
+    __syncthreads();
+
+    const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
+    const WaveRange r0 = wave_range(0, P.n, 0, lane);  // stream wave 0 has the most chunks
+    uint32_t nper = 0, c0, l0;
+    while (r0.chunk(nper, c0, l0)) nper++;
+    const Blob B(P.frames, P.frames_bytes);
+    Rec stg[kSplitStageK];
+    uint32_t nstg = 0, klast = 0;
+    for (uint32_t p = 0; p <= nper; p++) {
+        uint32_t c, lim;
+        if (!finisher) {
+            if (r.chunk(p, c, lim)) {
+                WaveLds& W = s_buf[p & 1][sw];
+                const uint32_t i = c + r.lane_off;
+                const bool live = i < lim;
+                const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+                const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
+                const CoopPlan pl = coop_plan(F, lane, off, W);
+                for (uint32_t rr = 0; rr * 4 < pl.ncoop; rr += kRoundsPerStep) {
+                    CoopStep S;
+                    coop_issue(pl, rr, lane, W, B, S, 0);
+                    coop_finish<kShift>(pl, rr, lane, W, B, S);
+                }
+            }
+        } else if (p > 0 && r.chunk(p - 1, c, lim)) {
+            WaveLds& W = s_buf[(p - 1) & 1][sw];
+            const uint32_t i = c + r.lane_off;
+            const bool live = i < lim;
+            const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+            const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
+            Chunk C;
+            small_load(F, B, off, C.R);
+            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 1};
+            coop_gather(F, pl, lane, W, C);
+            uint32_t v, fid;
+            Rec rec;
+            rec.meta = kNoRec;
+            rx_finish<kShift, true>(P, i, live, lane, W, off, len, C, v, fid, rec);
+#pragma unroll
+            for (int q = kSplitStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
+            stg[0] = rec;
+            klast = p - 1;
+            if (++nstg == kSplitStageK) {
+                flush_split(P, stg, nstg, r, klast);
+                nstg = 0;
+            }
+            count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+        }
+        __syncthreads();
+    }
+    if (finisher && nstg) flush_split(P, stg, nstg, r, klast);
+    if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
+    if (lds_flows) {
+        uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.flow_words;
+        for (uint32_t k = tid; k < P.flow_words; k += kSplitBlock) row[k] = s_flow[k];
     }
 }
 
@@ -1162,18 +1267,28 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
 }  // namespace
 }  // namespace dk
 
-int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, bool stage) {
+int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     int blocks = 0;
-    const auto k = stage ? dk::dk_rx_kernel<true, true> : dk::dk_rx_kernel<true, false>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, dk::kBlock, dyn_lds_bytes) != hipSuccess) return 0;
-    return blocks;
+    hipError_t e;
+    if (family == dk::kFamilySplit)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true>, dk::kSplitBlock,
+                                                          dyn_lds_bytes);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, family == dk::kFamilyStaged ? dk::dk_rx_kernel<true, true> : dk::dk_rx_kernel<true, false>,
+            dk::kBlock, dyn_lds_bytes);
+    return e == hipSuccess ? blocks : 0;
 }
 
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
-    if (p.aligned16 && p.stage)
+    if (p.split && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<false>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
+    else if (p.split)
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<true>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
+    else if (p.aligned16 && p.stage)
         hipLaunchKernelGGL((dk::dk_rx_kernel<false, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     else if (p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_kernel<false, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);

@@ -103,11 +103,13 @@ def test_random_batches(torch_cuda, mix, hint):
 
 @pytest.mark.parametrize("grid", [None, "2", "7"])
 @pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
-@pytest.mark.parametrize("stage", ["0", "1"])
-def test_kernel_variants(torch_cuda, monkeypatch, stage, sched, grid):
-    """Both kernel families (result staging on/off) under every wave schedule, with grids small enough that each wave
-    walks many chunks (staged results flushed mid-loop and at exit) and with the default grid."""
-    monkeypatch.setenv("DK_RX_STAGE", stage)
+@pytest.mark.parametrize("family", ["unstaged", "staged", "split"])
+def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
+    """Every kernel family (results stored per chunk / staged in registers / split stream+finish waves) under every
+    wave schedule, with grids small enough that each wave walks many chunks (staged results flushed mid-loop and at
+    exit) and with the default grid. The split kernel always walks sched 0."""
+    monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
+    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
     monkeypatch.setenv("DK_RX_SCHED", sched)
     if grid is not None:
         monkeypatch.setenv("DK_RX_GRID", grid)
@@ -117,7 +119,7 @@ def test_kernel_variants(torch_cuda, monkeypatch, stage, sched, grid):
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.05, tr))
     perm = np.random.default_rng(8).permutation(n)
-    check(blob, off[perm], lens[perm], flows, ctx=f"stage={stage} sched={sched} grid={grid}")
+    check(blob, off[perm], lens[perm], flows, ctx=f"{family} sched={sched} grid={grid}")
 
 
 def test_misaligned_and_offsets(torch_cuda):

@@ -6,4 +6,4 @@ for f in sorted(glob.glob(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab_*
     for l in open(f):
         if l.startswith("{"):
             d = json.loads(l)
-            print(f"  {d['variant']:<22} g={d['grid_per_cu']} s={d['sched']}  {d['ms']*1000:8.1f} us  {d['algo_GBps']:8.1f} GB/s  spread {d['spread']}")
+            print(f"  {d['variant']:<34} g={d['grid_per_cu']} s={d['sched']}  {d['ms']*1000:8.1f} us  {d['algo_GBps']:8.1f} GB/s  spread {d['spread']}")

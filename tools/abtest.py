@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--scheds", default="", help="comma list of DK_RX_SCHED values to interleave (default: host rule)")
+    ap.add_argument("--knob", default="", help="NAME=v1,v2,...: interleave values of one more env knob (e.g. DK_RX_SPLIT=0,1)")
     ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
     args = ap.parse_args()
     import torch
@@ -41,13 +42,18 @@ def main():
     algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES)
     grids = [int(g) for g in args.grids.split(",")]
     scheds = args.scheds.split(",") if args.scheds else [None]
-    times = {(k, g, sc): [] for k in engines for g in grids for sc in scheds}
+    kname, kvals = (args.knob.split("=")[0], args.knob.split("=")[1].split(",")) if args.knob else ("", [None])
+    configs = [(sc, kv) for sc in scheds for kv in kvals]
+    times = {(k, g, cf): [] for k in engines for g in grids for cf in configs}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rep in range(args.reps):
-        for g, sc in [(g, sc) for g in grids for sc in scheds]:
+        for g, cf in [(g, cf) for g in grids for cf in configs]:
+            sc, kv = cf
             os.environ["DK_RX_GRID_PER_CU"] = str(g)
             if sc is not None:
                 os.environ["DK_RX_SCHED"] = sc
+            if kv is not None:
+                os.environ[kname] = kv
             for k, (e, r) in engines.items():
                 run = (lambda: e.tx_checksum(batch)) if args.tx else (lambda: e.receive_batch(batch, r))  # noqa: E731
                 run()
@@ -56,10 +62,11 @@ def main():
                     run()
                 ev1.record()
                 torch.cuda.synchronize()
-                times[(k, g, sc)].append(ev0.elapsed_time(ev1) / args.iters)
-    for (k, g, sc), ts in sorted(times.items(), key=lambda x: (x[0][1], str(x[0][2]), x[0][0])):
+                times[(k, g, cf)].append(ev0.elapsed_time(ev1) / args.iters)
+    for (k, g, cf), ts in sorted(times.items(), key=lambda x: (x[0][1], str(x[0][2]), x[0][0])):
         ms = float(np.median(ts))
-        print(json.dumps({"variant": k, "grid_per_cu": g, "sched": sc, "workload": args.workload, "tx": args.tx, "ms": round(ms, 4),
+        name = k if cf[1] is None else f"{k}[{kname}={cf[1]}]"
+        print(json.dumps({"variant": name, "grid_per_cu": g, "sched": cf[0], "workload": args.workload, "tx": args.tx, "ms": round(ms, 4),
                           "algo_GBps": round(algo / ms / 1e6, 1), "spread": round((max(ts) - min(ts)) / ms, 3)}))
 
 
