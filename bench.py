@@ -184,6 +184,35 @@ def host_path_rate(eng, batch, flows, nframes, reps=3):
             "pipeline": "3 streams, 65536-frame chunks, pinned host memory (dk_rx_process_host)"}
 
 
+def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=3):
+    """end-to-end GB/s of frame bytes for frames sitting in a TPACKET_V3 receive ring (the
+    layout AF_PACKET fills; page-locked with hipHostRegister): block scan on the host, H2D of the blocks' byte ranges,
+    kernel, D2H of the results (dk_rx_process_tpacket3). PCIe-inclusive; reported beside `value`, never as `value`."""
+    from demikernel_amd import RxResults
+    from demikernel_amd import ring as RG
+
+    n = min(nframes, batch.n)
+    off = batch.off[:n].cpu().numpy().view(np.uint32).astype(np.int64)
+    lens = batch.len[:n].cpu().numpy().view(np.uint16).copy()
+    end = int(off[-1]) + int(lens[-1])
+    blob = batch.blob[:end].cpu().numpy()
+    ring, used, _, elen = RG.build_tpacket3(blob, off, lens, block_size)
+    r = RG.TpacketRing(ring, block_size)
+    res = RxResults(n, len(flows), host=True)
+    nbytes = int(elen.astype(np.int64).sum())
+    rates = []
+    try:
+        for _ in range(reps):
+            t = time.perf_counter()
+            nf, nb = r.receive(eng, 0, used, res)
+            rates.append(nbytes / (time.perf_counter() - t) / 1e9)
+            assert nf == n and nb == used
+    finally:
+        r.close()
+    return {"gbps": round(max(rates), 2), "frames": n, "bytes": nbytes, "blocks": used, "block_size": block_size,
+            "reps": reps, "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
+
+
 def tx_rate(eng, batch, frame_bytes, stream, iters=20):
     """dk_tx_checksum kernel time over an HBM-resident batch: frame bytes read, 2 checksum fields written per frame."""
     import torch
@@ -367,6 +396,7 @@ def main():
         # host-resident path (NIC ring / socket buffer in pinned host memory): H2D frames + descriptors, kernel,
         # D2H results, pipelined on 3 streams (dk_rx_process_host). Reported beside `value`, never as `value`.
         out["host_path"] = host_path_rate(eng, batch, flows, args.host_frames)
+        out["ring_path"] = ring_path_rate(eng, batch, flows, args.host_frames)
         # TX checksum fill (dk_tx_checksum) over the same batch (rewrites its checksum fields)
         out["tx_checksum"] = tx_rate(eng, batch, frame_bytes, stream)
         out["tx_checksum"]["traffic"] = load_traffic_profile(name + "_tx")

@@ -75,6 +75,17 @@ FUNCTIONS = [
     ("dk_rx_device_count", c_int, []),
 ]
 
+# include/dk_ring.h (TPACKET_V3 ring ingest)
+RING_FUNCTIONS = [
+    ("dk_ring_register", c_int, [c_void_p, c_uint64]),
+    ("dk_ring_unregister", c_int, [c_void_p]),
+    ("dk_ring_scan_tpacket3", c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_uint32,
+                                      POINTER(c_uint32), POINTER(c_uint32)]),
+    ("dk_ring_release_tpacket3", c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_uint32]),
+    ("dk_rx_process_tpacket3", c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint32,
+                                       POINTER(DkRxResults), c_uint32, POINTER(c_uint32), POINTER(c_uint32)]),
+]
+
 # include/dk_diag.h (diagnostics, not the receive ABI)
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
@@ -100,10 +111,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
-    for name, restype, argtypes in FUNCTIONS + DIAG_FUNCTIONS:
+    for name, restype, argtypes in FUNCTIONS + RING_FUNCTIONS + DIAG_FUNCTIONS:
         fn = getattr(lib, name, None)
         if fn is None:
-            if (name, restype, argtypes) in DIAG_FUNCTIONS and path != LIB_PATH:
+            if (name, restype, argtypes) in DIAG_FUNCTIONS + RING_FUNCTIONS and path != LIB_PATH:
                 continue  # older tuning builds may predate a diagnostic
             raise ImportError(f"{path}: missing {name}")
         fn.restype = restype

@@ -10,7 +10,7 @@ import pytest
 from demikernel_amd import _native as N
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("dk_rx.h", "dk_diag.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("dk_rx.h", "dk_diag.h", "dk_ring.h")]
 
 
 def declared_functions(path):
@@ -30,11 +30,11 @@ def test_every_declared_function_is_exported():
     names = set()
     for h in HEADERS:
         names |= set(declared_functions(h))
-    assert {"dk_rx_process", "dk_rx_ctx_create", "dk_tx_checksum", "dk_diag_read_probe"} <= names
+    assert {"dk_rx_process", "dk_rx_ctx_create", "dk_tx_checksum", "dk_diag_read_probe", "dk_rx_process_tpacket3"} <= names
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
     assert names <= exported, names - exported
-    bound = {f[0] for f in N.FUNCTIONS + N.DIAG_FUNCTIONS}
+    bound = {f[0] for f in N.FUNCTIONS + N.RING_FUNCTIONS + N.DIAG_FUNCTIONS}
     assert bound == names, (names ^ bound)
     for n in names:
         getattr(lib, n)

@@ -1,0 +1,93 @@
+"""TPACKET_V3 ring ingest (include/dk_ring.h) on CPU: the block walker gives exactly the frames a
+Linux TPACKET_V3 ring holds, in ring order, and stops, wraps, caps and rejects the way dk_ring.h says. Layout facts of
+the ring (48-byte block descriptor and tpacket3_hdr, 8-byte packet alignment, tp_mac) are checked against the C
+structures of <linux/if_packet.h>."""
+import subprocess
+
+import numpy as np
+import pytest
+
+from demikernel_amd import ring as RG
+from demikernel_amd import synth
+from demikernel_amd.rx import Fail
+
+EBADMSG, ENOSPC, EINVAL = 74, 28, 22
+
+
+def frames(n, seed=3):
+    flows = synth.make_flows(32)
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=seed), flows, seed=seed)
+    return synth.build_numpy(tr)
+
+
+def test_linux_struct_layout(tmp_path):
+    src = tmp_path / "l.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include <linux/if_packet.h>\nint main(void){'
+                   'printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(struct tpacket_block_desc), sizeof(struct tpacket3_hdr),'
+                   'offsetof(struct tpacket_block_desc, hdr.bh1.block_status),'
+                   'offsetof(struct tpacket_block_desc, hdr.bh1.num_pkts), offsetof(struct tpacket3_hdr, tp_mac),'
+                   'offsetof(struct tpacket3_hdr, tp_snaplen)); return 0;}')
+    exe = tmp_path / "l"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(x) for x in got] == [RG.BLOCK_DESC_BYTES, RG.PKT_HDR_BYTES, 8, 12, 24, 12]
+
+
+@pytest.mark.parametrize("block_size", [1 << 16, 1 << 20])
+def test_scan_gives_ring_frames_in_order(block_size):
+    blob, off, lens = frames(3000)
+    ring, used, eoff, elen = RG.build_tpacket3(blob, off, lens, block_size)
+    r = RG.TpacketRing(ring, block_size, register=False)
+    o, ln, nb = r.scan(0, used, len(off))
+    assert nb == used and np.array_equal(o, eoff) and np.array_equal(ln, elen)
+    assert set(int(x) % 16 for x in o) <= {2, 10}  # Ethernet header at 2 mod 8, like NIC buffers
+    for k in range(0, len(off), 97):
+        assert ring[o[k]:o[k] + ln[k]].tobytes() == blob[off[k]:off[k] + lens[k]].tobytes()
+
+
+def test_scan_stops_at_kernel_owned_block_and_wraps():
+    blob, off, lens = frames(2000)
+    bs = 1 << 16
+    ring, used, eoff, elen = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+    assert used >= 4
+    r = RG.TpacketRing(ring, bs, register=False)
+    r.release(2, 1)  # block 2 handed back to the kernel: the scan stops before it
+    o, ln, nb = r.scan(0, used, len(off))
+    per_block = np.bincount((eoff // bs).astype(np.int64), minlength=used)
+    assert nb == 2 and len(o) == per_block[:2].sum()
+    # wrap: starting at the last block, two blocks = the last one then block 0
+    o2, _, nb2 = r.scan(used - 1, 2, len(off))
+    assert nb2 == 2 and np.array_equal(o2, np.concatenate([eoff[eoff // bs == used - 1], eoff[eoff // bs == 0]]))
+
+
+def test_scan_capacity():
+    blob, off, lens = frames(2000)
+    bs = 1 << 16
+    ring, used, eoff, _ = RG.build_tpacket3(blob, off, lens, bs)
+    r = RG.TpacketRing(ring, bs, register=False)
+    first = int((eoff // bs == 0).sum())
+    o, _, nb = r.scan(0, used, first + 5)  # room for block 0 only
+    assert nb == 1 and len(o) == first
+    with pytest.raises(Fail) as e:
+        r.scan(0, used, first - 1)  # not even block 0 fits
+    assert e.value.errno == ENOSPC
+
+
+def test_malformed_blocks_rejected():
+    blob, off, lens = frames(200)
+    bs = 1 << 16
+    ring, used, eoff, _ = RG.build_tpacket3(blob, off, lens, bs)
+    bad = ring.copy()
+    first_pkt = RG.BLOCK_DESC_BYTES
+    bad[first_pkt:first_pkt + 4] = 0  # tp_next_offset 0 on a packet that is not the block's last
+    with pytest.raises(Fail) as e:
+        RG.TpacketRing(bad, bs, register=False).scan(0, used, 10000)
+    assert e.value.errno == EBADMSG
+    bad = ring.copy()
+    bad[first_pkt + 12:first_pkt + 16] = np.frombuffer(np.uint32(bs).tobytes(), np.uint8)  # snaplen past the block
+    with pytest.raises(Fail) as e:
+        RG.TpacketRing(bad, bs, register=False).scan(0, used, 10000)
+    assert e.value.errno == EBADMSG
+    with pytest.raises(Fail) as e:
+        RG.TpacketRing(ring, bs, register=False).scan(used + 100, 1, 10)  # first block outside the ring
+    assert e.value.errno == EINVAL
