@@ -45,12 +45,12 @@ int scan_block(const uint8_t* ring, uint64_t base, uint32_t block_size, uint32_t
 
 // Page-locked descriptor staging for dk_rx_process_tpacket3 (one per host thread; contexts are single-threaded,
 // dk_rx.h): the pipeline's descriptor copies then run as DMA like the frame copies instead of bouncing through
-// pageable memory.
+// pageable memory. Grown on demand and kept for the process lifetime (no destructor: freeing at thread exit could run
+// after the HIP runtime has shut down).
 struct PinnedDescs {
     uint32_t* off = nullptr;
     uint16_t* len = nullptr;
     uint32_t cap = 0;
-    ~PinnedDescs() { release(); }
     void release() {
         if (off) (void)hipHostFree(off);
         if (len) (void)hipHostFree(len);
