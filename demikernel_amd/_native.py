@@ -86,6 +86,44 @@ RING_FUNCTIONS = [
                                        POINTER(DkRxResults), c_uint32, POINTER(c_uint32), POINTER(c_uint32)]),
 ]
 
+# include/dk_tcp.h (established-state TCP receive processing)
+DK_TCP_OOO_MAX = 16
+DK_TCP_DELIV_EXTRA = 18
+DK_TCP_REF_EOF = 0xFFFFFFFF
+DK_TCP_NONE, DK_TCP_ESTABLISHED, DK_TCP_CLOSED = 0, 1, 2
+TCP_ACTIONS = ["SKIP", "DELIVERED", "STORED", "STORE_DUP", "NO_DATA", "FIN", "DUPLICATE", "OUT_OF_WINDOW", "RST",
+               "SYN", "NO_ACK", "ACK_UNSENT", "UNPROCESSED"]
+A = {name: i for i, name in enumerate(TCP_ACTIONS)}
+VIEW_DTYPE = np.dtype([("ref", "<u4"), ("off", "<u4"), ("len", "<u4")])
+CONN_DTYPE = np.dtype([("state", "<u4"), ("receive_next", "<u4"), ("reader_next", "<u4"), ("buffer_size", "<u4"),
+                       ("send_next", "<u4"), ("fin_pending", "<u4"), ("fin_seq", "<u4"), ("ooo_count", "<u4"),
+                       ("ooo_start", "<u4", (DK_TCP_OOO_MAX,)), ("ooo", VIEW_DTYPE, (DK_TCP_OOO_MAX,))])
+assert CONN_DTYPE.itemsize == 288
+
+
+class DkTcpView(ctypes.Structure):
+    _fields_ = [("ref", c_uint32), ("off", c_uint32), ("len", c_uint32)]
+
+
+class DkTcpConn(ctypes.Structure):
+    _fields_ = [("state", c_uint32), ("receive_next", c_uint32), ("reader_next", c_uint32),
+                ("buffer_size", c_uint32), ("send_next", c_uint32), ("fin_pending", c_uint32), ("fin_seq", c_uint32),
+                ("ooo_count", c_uint32), ("ooo_start", c_uint32 * DK_TCP_OOO_MAX),
+                ("ooo", DkTcpView * DK_TCP_OOO_MAX)]
+
+
+class DkTcpOut(ctypes.Structure):
+    _fields_ = [("action", c_void_p), ("view", c_void_p), ("deliv", c_void_p), ("deliv_start", c_void_p),
+                ("deliv_count", c_void_p)]
+
+
+TCP_FUNCTIONS = [
+    ("dk_tcp_ctx_create", c_int, [c_int32, POINTER(c_void_p)]),
+    ("dk_tcp_ctx_destroy", None, [c_void_p]),
+    ("dk_tcp_rx_process", c_int, [c_void_p, POINTER(DkRxResults), c_uint32, c_void_p, c_uint32, POINTER(DkTcpOut),
+                                  c_void_p]),
+]
+
 # include/dk_diag.h (diagnostics, not the receive ABI)
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
@@ -111,10 +149,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
-    for name, restype, argtypes in FUNCTIONS + RING_FUNCTIONS + DIAG_FUNCTIONS:
+    for name, restype, argtypes in FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS:
         fn = getattr(lib, name, None)
         if fn is None:
-            if (name, restype, argtypes) in DIAG_FUNCTIONS + RING_FUNCTIONS and path != LIB_PATH:
+            if (name, restype, argtypes) in DIAG_FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS and path != LIB_PATH:
                 continue  # older tuning builds may predate a diagnostic
             raise ImportError(f"{path}: missing {name}")
         fn.restype = restype

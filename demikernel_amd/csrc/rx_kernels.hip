@@ -753,7 +753,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
             const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20);
             if (e) L.v = e;
         }
-        const uint32_t sport = L.ports & 0xFFFFu, dport = L.ports >> 16;
+        const uint32_t dport = L.ports >> 16;
         if (L.v == kPendTcp) {
             // SocketId::Active(local=(local_ip, dport), remote=(src, sport)), then Passive(local) (tcp/peer.rs:241-251)
             fid = probe_finish(P, k1, h1, s1);  // Active(local, remote)

@@ -101,6 +101,69 @@ def traffic(n: int, ip_len, flows: np.ndarray, local_ip: str = BOB_IPV4, seed: i
         ip_id=rng.integers(0, 65536, n, dtype=np.uint16), ttl=np.full(n, 64, np.uint8), flow=fidx.astype(np.int64))
 
 
+def tcp_streams(n: int, nconns: int, ip_len=None, *, reorder: float = 3.0, dup: float = 0.02, oow: float = 0.005,
+                fin: float = 0.3, rare: float = 0.002, buffer_size: int = 65535, seed: int = SEED):
+    """Established TCP byte streams for the dk_tcp path: `n` data segments over `nconns` Active connections, each
+    connection's segments contiguous in sequence space from a random RCV.NXT (wrapping included), arriving with local
+    reordering (each segment displaced by up to ~`reorder` places within its connection), a `dup` fraction resent from
+    earlier stream offsets (duplicates and partial overlaps), an `oow` fraction far beyond the window, FIN on the last
+    segment of a `fin` fraction of the connections, and a `rare` fraction each of RST / SYN / ACK-bit-clear /
+    ack-beyond-SND.NXT. Returns (flows, Traffic, host connection table for dk_tcp (one row per flow; the Passive
+    listener's row is DK_TCP_NONE))."""
+    from .tcp import CONN_DTYPE, ESTABLISHED
+
+    rng = np.random.default_rng(seed + 7)
+    flows = make_flows(nconns, seed=seed)
+    tr = traffic(n, 40 if ip_len is None else ip_len, flows, seed=seed)
+    if ip_len is None:
+        tr.ip_len = (40 + rng.integers(0, 1461, n)).astype(np.uint16)
+        tr.frame_len = np.maximum(tr.ip_len.astype(np.int64) + 14, ETH_MIN_FRAME).astype(np.uint16)
+    plen = tr.ip_len.astype(np.int64) - 40
+    f = tr.flow
+    isn = rng.integers(0, 2**32, nconns, dtype=np.uint64)
+    isn[: min(nconns, 4)] = 2**32 - 3000  # a few streams wrap inside the batch
+    snd = rng.integers(0, 2**32, nconns, dtype=np.uint64)
+    # stream order: arrival rank within the connection plus noise, re-ranked
+    arr = np.arange(n)
+    key = np.lexsort((arr + rng.uniform(0, reorder + 1e-9, n), f))  # frames sorted by (conn, noisy arrival)
+    order_len = plen[key]
+    csum = np.cumsum(order_len)
+    first = np.ones(n, bool)
+    first[1:] = f[key][1:] != f[key][:-1]
+    base = np.maximum.accumulate(np.where(first, csum - order_len, 0))
+    stream_off = np.empty(n, np.int64)
+    stream_off[key] = csum - order_len - base
+    seq = (isn[f] + stream_off.astype(np.uint64)) & 0xFFFFFFFF
+    r = rng.random(n)
+    d = r < dup
+    seq[d] = (seq[d] - rng.integers(1, 3000, int(d.sum())).astype(np.uint64)) & 0xFFFFFFFF
+    o = (r >= dup) & (r < dup + oow)
+    seq[o] = (seq[o] + np.uint64(buffer_size) + rng.integers(0, 1 << 20, int(o.sum())).astype(np.uint64)) & 0xFFFFFFFF
+    tr.seq = seq.astype(np.uint32)
+    tr.ack = ((snd[f] - rng.integers(0, 4096, n).astype(np.uint64)) & 0xFFFFFFFF).astype(np.uint32)
+    flags = np.full(n, 0x18, np.uint8)  # PSH | ACK
+    last = np.zeros(n, bool)
+    last_key = np.ones(n, bool)
+    last_key[:-1] = f[key][1:] != f[key][:-1]
+    last[key[last_key]] = True
+    fin_conn = rng.random(nconns) < fin
+    flags[last & fin_conn[f]] |= 0x01
+    for bit in (0x04, 0x02):  # RST, SYN
+        flags[rng.random(n) < rare] |= bit
+    flags[rng.random(n) < rare] &= ~np.uint8(0x10)  # ACK bit clear
+    unsent = rng.random(n) < rare
+    tr.ack[unsent] = ((snd[f[unsent]] + rng.integers(1, 1 << 20, int(unsent.sum())).astype(np.uint64))
+                      & 0xFFFFFFFF).astype(np.uint32)
+    tr.flags = flags
+    table = np.zeros(len(flows), CONN_DTYPE)
+    table["state"][:nconns] = ESTABLISHED
+    table["receive_next"][:nconns] = isn.astype(np.uint32)
+    table["reader_next"][:nconns] = isn.astype(np.uint32)
+    table["buffer_size"][:nconns] = buffer_size
+    table["send_next"][:nconns] = snd.astype(np.uint32)
+    return flows, tr, table
+
+
 def imix_ip_lengths(n: int, seed: int = SEED) -> np.ndarray:
     """Simple IMIX: IPv4 total lengths 40 / 576 / 1500 in ratio 7:4:1, shuffled."""
     rng = np.random.default_rng(seed + 1)

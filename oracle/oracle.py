@@ -58,6 +58,8 @@ def lib() -> ctypes.CDLL:
         L.dko_generic_checksum.argtypes = [vp, c_size_t, c_int, c_uint32]
         L.dko_tx_fill_checksums.restype = c_int
         L.dko_tx_fill_checksums.argtypes = [vp, c_size_t]
+        L.dko_tcp_process.restype = c_int
+        L.dko_tcp_process.argtypes = [vp, c_uint32, c_uint32] + [vp] * 10
         _lib = L
     return _lib
 
@@ -164,3 +166,28 @@ def generic_checksum(buf: bytes, start: int | None = None) -> int:
 def tx_fill_checksums(frame: bytearray) -> int:
     a = np.frombuffer(frame, np.uint8)
     return lib().dko_tx_fill_checksums(a.ctypes.data, len(frame))
+
+
+# include/dk_tcp.h mirrors (tests/test_tcp_oracle.py checks them against demikernel_amd._native)
+TCP_OOO_MAX, TCP_DELIV_EXTRA = 16, 18
+TCP_VIEW_DTYPE = np.dtype([("ref", "<u4"), ("off", "<u4"), ("len", "<u4")])
+TCP_CONN_DTYPE = np.dtype([("state", "<u4"), ("receive_next", "<u4"), ("reader_next", "<u4"), ("buffer_size", "<u4"),
+                           ("send_next", "<u4"), ("fin_pending", "<u4"), ("fin_seq", "<u4"), ("ooo_count", "<u4"),
+                           ("ooo_start", "<u4", (TCP_OOO_MAX,)), ("ooo", TCP_VIEW_DTYPE, (TCP_OOO_MAX,))])
+
+
+def tcp_process(conns: np.ndarray, rx: dict) -> dict:
+    """dko_tcp_process: the batch's TCP segments through `conns` (TCP_CONN_DTYPE, updated in place). rx holds the
+    dk_rx results meta, flow_id, tcp_seq, tcp_ack, payload (u32[n]). Returns action, view, deliv, deliv_start,
+    deliv_count in the dk_tcp_rx_process layout, deliv trimmed to its used span."""
+    assert conns.dtype == TCP_CONN_DTYPE and conns.flags.c_contiguous
+    f = {k: np.ascontiguousarray(rx[k], np.uint32) for k in ("meta", "flow_id", "tcp_seq", "tcp_ack", "payload")}
+    n, nc = len(f["meta"]), len(conns)
+    out = {"action": np.zeros(n, np.uint8), "view": np.zeros(n, TCP_VIEW_DTYPE),
+           "deliv": np.zeros(n + TCP_DELIV_EXTRA * nc, TCP_VIEW_DTYPE),
+           "deliv_start": np.zeros(nc, np.uint32), "deliv_count": np.zeros(nc, np.uint32)}
+    p = lambda a: a.ctypes.data if a.size else None  # noqa: E731
+    rc = lib().dko_tcp_process(p(conns), nc, n, *[p(f[k]) for k in ("meta", "flow_id", "tcp_seq", "tcp_ack", "payload")],
+                               *[p(out[k]) for k in ("action", "view", "deliv", "deliv_start", "deliv_count")])
+    assert rc == 0
+    return out

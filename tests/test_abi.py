@@ -10,7 +10,7 @@ import pytest
 from demikernel_amd import _native as N
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("dk_rx.h", "dk_diag.h", "dk_ring.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("dk_rx.h", "dk_diag.h", "dk_ring.h", "dk_tcp.h")]
 
 
 def declared_functions(path):
@@ -30,11 +30,12 @@ def test_every_declared_function_is_exported():
     names = set()
     for h in HEADERS:
         names |= set(declared_functions(h))
-    assert {"dk_rx_process", "dk_rx_ctx_create", "dk_tx_checksum", "dk_diag_read_probe", "dk_rx_process_tpacket3"} <= names
+    assert {"dk_rx_process", "dk_rx_ctx_create", "dk_tx_checksum", "dk_diag_read_probe", "dk_rx_process_tpacket3",
+            "dk_tcp_rx_process"} <= names
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
     assert names <= exported, names - exported
-    bound = {f[0] for f in N.FUNCTIONS + N.RING_FUNCTIONS + N.DIAG_FUNCTIONS}
+    bound = {f[0] for f in N.FUNCTIONS + N.RING_FUNCTIONS + N.TCP_FUNCTIONS + N.DIAG_FUNCTIONS}
     assert bound == names, (names ^ bound)
     for n in names:
         getattr(lib, n)
@@ -42,8 +43,10 @@ def test_every_declared_function_is_exported():
 
 def test_struct_layout_matches_ctypes(tmp_path):
     """sizeof/offsetof from the C compiler == the ctypes mirror (dk_rx_cfg, dk_flow, dk_rx_batch, dk_rx_results)."""
-    structs = {"dk_rx_cfg": N.DkRxCfg, "dk_flow": N.DkFlow, "dk_rx_batch": N.DkRxBatch, "dk_rx_results": N.DkRxResults}
-    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADERS[0]}"', "int main(void) {"]
+    structs = {"dk_rx_cfg": N.DkRxCfg, "dk_flow": N.DkFlow, "dk_rx_batch": N.DkRxBatch, "dk_rx_results": N.DkRxResults,
+               "dk_tcp_view": N.DkTcpView, "dk_tcp_conn": N.DkTcpConn, "dk_tcp_out": N.DkTcpOut}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADERS[0]}"', f'#include "{HEADERS[3]}"',
+             "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
         for fname, _ in cls._fields_:
@@ -60,6 +63,18 @@ def test_struct_layout_matches_ctypes(tmp_path):
         for fname, _ in cls._fields_:
             assert int(got[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert ctypes.sizeof(N.DkFlow) == N.FLOW_DTYPE.itemsize == 16
+    assert ctypes.sizeof(N.DkTcpConn) == N.CONN_DTYPE.itemsize == 288
+    for fname, _ in N.DkTcpConn._fields_:
+        assert N.CONN_DTYPE.fields[fname][1] == getattr(N.DkTcpConn, fname).offset, fname
+
+
+def test_tcp_header_constants():
+    hdr = open(HEADERS[3]).read()
+    for i, name in enumerate(N.TCP_ACTIONS):
+        assert re.search(rf"DK_TCP_{name} = {i}[,\s]", hdr), name
+    assert f"DK_TCP_OOO_MAX {N.DK_TCP_OOO_MAX}u" in hdr and f"DK_TCP_DELIV_EXTRA {N.DK_TCP_DELIV_EXTRA}u" in hdr
+    for name, v in (("NONE", N.DK_TCP_NONE), ("ESTABLISHED", N.DK_TCP_ESTABLISHED), ("CLOSED", N.DK_TCP_CLOSED)):
+        assert re.search(rf"DK_TCP_{name} = {v}", hdr), name
 
 
 def test_verdict_tables():

@@ -1,0 +1,171 @@
+"""GPU parity of established-state TCP receive processing (dk_tcp_rx_process) with the CPU
+restatement (oracle/dk_tcp_oracle.cpp): every per-frame action and view, every delivered buffer and the whole
+connection table (RCV.NXT, state, FIN, the out-of-order store) bit for bit — on the hand-built branch scenarios of
+tests/test_tcp_oracle.py and on synthetic streams that go through dk_rx first (frames -> verdicts/flow ids ->
+TCP), over several batches so state carries across calls."""
+import numpy as np
+import pytest
+
+import test_tcp_oracle as S
+from demikernel_amd import Config, FrameBatch, RxEngine, RxResults, synth
+from demikernel_amd import _native as N
+from demikernel_amd.rx import Fail
+from demikernel_amd.tcp import TcpOut, TcpReceiver
+from oracle import oracle as O
+from oracle.oracle import OraclePeer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tcp():
+    import torch
+
+    assert torch.cuda.is_available()
+    r = TcpReceiver(0)
+    yield r
+    r.close()
+
+
+def rx_device(rx: dict):
+    import torch
+
+    n = len(rx["meta"])
+    r = RxResults(n, 1, device=torch.device("cuda", 0), tcp_fields=True, counts=False)
+    for k in ("meta", "flow_id", "tcp_seq", "tcp_ack", "payload"):
+        r.t[k].copy_(torch.from_numpy(np.ascontiguousarray(rx[k], np.uint32).view(np.int32)))
+    return r
+
+
+def gpu_process(tcp, table: np.ndarray, r: RxResults) -> tuple[np.ndarray, dict]:
+    import torch
+
+    conns = tcp.conns_to_device(table)
+    out = TcpOut(r.n, len(table))
+    tcp.process(r, conns, out)
+    torch.cuda.synchronize()
+    return tcp.conns_to_host(conns), out.to_numpy()
+
+
+def assert_same(got_t, got, exp_t, exp, ctx=""):
+    for k in ("action", "view", "deliv_start", "deliv_count"):
+        if not np.array_equal(got[k], exp[k]):
+            bad = np.nonzero(got[k] != exp[k])[0][:8]
+            raise AssertionError(f"{ctx}: {k} differs at {bad}: got {got[k][bad]} exp {exp[k][bad]}")
+    for c in range(len(exp_t)):  # only the used delivery slots are defined
+        s, m = int(exp["deliv_start"][c]), int(exp["deliv_count"][c])
+        assert np.array_equal(got["deliv"][s:s + m], exp["deliv"][s:s + m]), f"{ctx}: deliv of conn {c}"
+    if not np.array_equal(got_t.view(np.uint8), exp_t.view(np.uint8)):
+        bad = np.nonzero((got_t.view(np.uint8).reshape(len(got_t), -1) !=
+                          exp_t.view(np.uint8).reshape(len(exp_t), -1)).any(1))[0][:8]
+        raise AssertionError(f"{ctx}: connection table differs at {bad}: got {got_t[bad]} exp {exp_t[bad]}")
+
+
+SCENARIOS = {
+    "fin_in_order": (S.conns(rn=1), [(0, 1, 1, S.FIN | S.ACK, 0)]),
+    "ooo_fin": (S.conns(rn=1, snd=1001), [(0, 1001, 1001, S.FIN | S.ACK, 0), (0, 1, 1001, S.PSH | S.ACK, 1000)]),
+    "dup_partial": (S.conns(rn=1001), [(0, 1, 1, S.ACK, 1000), (0, 501, 1, S.ACK, 1000)]),
+    "window": (S.conns(rn=1), [(0, 65536, 1, S.ACK, 10), (0, 65535, 1, S.ACK, 10)]),
+    "fin_trim": (S.conns(rn=1, bufsz=100), [(0, 1, 1, S.FIN | S.ACK, 100)]),
+    "zero_window": (S.conns(rn=1001, reader=1, bufsz=1000), [(0, 1001, 1, S.ACK, 10)]),
+    "syn": (S.conns(rn=100), [(0, 99, 1, S.SYN | S.ACK, 100), (0, 200, 1, S.SYN | S.ACK, 0)]),
+    "wrap": (S.conns(rn=0xFFFFFF00), [(0, 0xFFFFFF00, 1, S.ACK, 1000), (0, 0xFFFFFF00, 1, S.ACK, 1000),
+                                      (0, 0x2E8, 1, S.ACK, 8)]),
+    "rst": (S.conns(rn=1), [(0, 0, 1, S.RST | S.ACK, 0), (0, 1, 1, S.RST, 0), (0, 1, 1, S.ACK, 10)]),
+    "ack": (S.conns(rn=1, snd=5), [(0, 1, 0xFFFFFFF0, S.ACK, 0), (0, 1, 10, S.ACK, 0), (0, 1, 5, S.PSH, 10)]),
+    "recovery": (S.conns(rn=1), [(0, 1001, 1, S.ACK, 1000), (0, 2001, 1, S.ACK, 1000), (0, 1, 1, S.ACK, 1000)]),
+    "encompass": (S.conns(rn=1), [(0, 1501, 1, S.ACK, 100), (0, 1521, 1, S.ACK, 50), (0, 1001, 1, S.ACK, 1000)]),
+    "end_overlap": (S.conns(rn=1), [(0, 1001, 1, S.ACK, 1000), (0, 1501, 1, S.ACK, 1000), (0, 1, 1, S.ACK, 1000)]),
+    "front_overlap": (S.conns(rn=1), [(0, 2001, 1, S.ACK, 1000), (0, 1501, 1, S.ACK, 1000), (0, 1, 1, S.ACK, 1500)]),
+    "sixteen": (S.conns(rn=1), [(0, 1001 + 200 * k, 1, S.ACK, 100) for k in range(17)] + [(0, 801, 1, S.ACK, 100)]),
+    "ooo_fin_data": (S.conns(rn=1), [(0, 1001, 1, S.FIN | S.ACK, 100), (0, 1, 1, S.ACK, 1000),
+                                     (0, 1102, 1, S.ACK, 5)]),
+    "skip_layout": (S.conns(4, rn=1), [(0, 1, 1, S.ACK, 10), (1, 1, 1, S.ACK, 10), (2, 1, 1, S.ACK, 10),
+                                       (1, 11, 1, S.ACK, 10), (N.DK_FLOW_NONE, 1, 1, S.ACK, 10),
+                                       (3, 1, 1, S.ACK, 10, 25), (7, 1, 1, S.ACK, 10), (3, 1, 1, S.FIN | S.ACK, 0)]),
+    "closed": (S.conns(2, rn=1, state=N.DK_TCP_CLOSED), [(0, 1, 1, S.ACK, 10), (1, 1, 1, S.ACK, 0)]),
+    "empty_batch": (S.conns(3, rn=1), []),
+}
+
+
+@pytest.mark.parametrize("name", list(SCENARIOS))
+def test_branch_scenarios(tcp, name):
+    table, segs = SCENARIOS[name]
+    if name == "skip_layout":
+        table = table.copy()
+        table["state"][2] = N.DK_TCP_NONE
+    rx = S.batch(segs) if segs else {k: np.zeros(0, np.uint32) for k in
+                                     ("meta", "flow_id", "tcp_seq", "tcp_ack", "payload")}
+    exp_t = table.copy()
+    exp = O.tcp_process(exp_t, rx)
+    got_t, got = gpu_process(tcp, table.copy(), rx_device(rx))
+    assert_same(got_t, got, exp_t, exp, name)
+
+
+def test_carried_out_of_order_store(tcp):
+    """A store left by one call is recovered by the next (the table is the only state between calls)."""
+    t = S.conns(rn=1)
+    b1 = S.batch([(0, 1001, 1, S.ACK, 1000), (0, 3001, 1, S.ACK, 1000)])
+    b2 = S.batch([(0, 2001, 1, S.ACK, 1000), (0, 1, 1, S.ACK, 1000)])
+    exp_t = t.copy()
+    O.tcp_process(exp_t, b1)
+    exp2 = O.tcp_process(exp_t, b2)
+    got_t, _ = gpu_process(tcp, t.copy(), rx_device(b1))
+    got_t, got2 = gpu_process(tcp, got_t, rx_device(b2))
+    assert_same(got_t, got2, exp_t, exp2, "carry")
+    assert int(got_t["receive_next"][0]) == 4001 and len(got2["deliv"][:got2["deliv_count"][0]]) == 4
+
+
+@pytest.mark.parametrize("n,nconns,batches", [(1, 1, 1), (3000, 1, 2), (20000, 7, 2), (60000, 1000, 3),
+                                              (200000, 20000, 2), (100000, 300, 1)])
+def test_streams_through_rx(tcp, n, nconns, batches):
+    """Frames -> dk_rx (verdicts, flow ids, seq/ack) -> dk_tcp on the GPU, against the oracle chain on the same
+    frames, batch after batch with the connection table carried."""
+    import torch
+
+    flows, tr, table = synth.tcp_streams(n * batches, nconns, seed=1000 + n + nconns)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(len(off), 0.01, tr))  # some frames never reach TCP
+    eng = RxEngine(Config(synth.BOB_IPV4), device=0)
+    eng.set_sockets(flows)
+    peer = OraclePeer(synth.ipv4(synth.BOB_IPV4))
+    peer.set_flows(flows)
+    exp_t, dev_conns = table.copy(), tcp.conns_to_device(table)
+    for b in range(batches):
+        sl = slice(b * n, (b + 1) * n)
+        boff, blens = off[sl], lens[sl]
+        batch = FrameBatch.from_numpy(blob, boff, blens, device=0)
+        r = eng.results(n, tcp_fields=True)
+        eng.receive_batch(batch, r)
+        out = TcpOut(n, len(table))
+        tcp.process(r, dev_conns, out)
+        torch.cuda.synchronize()
+        got = out.to_numpy()
+        exp_rx = peer.process(blob, boff, blens)
+        exp = O.tcp_process(exp_t, exp_rx)
+        got_t = tcp.conns_to_host(dev_conns)
+        assert_same(got_t, got, exp_t, exp, f"batch {b}")
+        hist = np.bincount(got["action"], minlength=len(N.TCP_ACTIONS))
+        if n >= 20000:
+            for a in ("DELIVERED", "STORED", "DUPLICATE", "SKIP"):
+                assert hist[N.A[a]] > 0, (a, hist)
+        # the application reads everything delivered (Receiver::pop moves reader_next, ctrlblk.rs:113-129): window reopens
+        exp_t["reader_next"] = exp_t["receive_next"]
+        got_t["reader_next"] = got_t["receive_next"]
+        dev_conns = tcp.conns_to_device(got_t)
+    eng.close()
+
+
+def test_rejects_missing_tcp_fields(tcp):
+    import ctypes
+
+    import torch
+
+    r = RxResults(8, 1, device=torch.device("cuda", 0), tcp_fields=False, counts=False)
+    conns = tcp.conns_to_device(S.conns(1))
+    out = TcpOut(8, 1)
+    with pytest.raises(Fail) as e:
+        tcp.process(r, conns, out)
+    assert e.value.errno == 22
+    h = ctypes.c_void_p()
+    assert tcp.lib.dk_tcp_ctx_create(-1, ctypes.byref(h)) == 22
