@@ -102,14 +102,16 @@ def traffic(n: int, ip_len, flows: np.ndarray, local_ip: str = BOB_IPV4, seed: i
 
 
 def tcp_streams(n: int, nconns: int, ip_len=None, *, reorder: float = 3.0, dup: float = 0.02, oow: float = 0.005,
-                fin: float = 0.3, rare: float = 0.002, buffer_size: int = 65535, seed: int = SEED):
+                fin: float = 0.3, rare: float = 0.002, rst: float = 0.05, buffer_size: int = 65535,
+                seed: int = SEED):
     """Established TCP byte streams for the dk_tcp path: `n` data segments over `nconns` Active connections, each
     connection's segments contiguous in sequence space from a random RCV.NXT (wrapping included), arriving with local
-    reordering (each segment displaced by up to ~`reorder` places within its connection), a `dup` fraction resent from
-    earlier stream offsets (duplicates and partial overlaps), an `oow` fraction far beyond the window, FIN on the last
-    segment of a `fin` fraction of the connections, and a `rare` fraction each of RST / SYN / ACK-bit-clear /
-    ack-beyond-SND.NXT. Returns (flows, Traffic, host connection table for dk_tcp (one row per flow; the Passive
-    listener's row is DK_TCP_NONE))."""
+    reordering (each segment displaced by up to ~`reorder` places within its connection), plus a `dup` fraction of
+    retransmissions from earlier stream offsets (duplicates and partial overlaps) and an `oow` fraction of strays far
+    beyond the window (neither takes stream bytes, so the streams stay gap-free), FIN on the last
+    segment of a `fin` fraction of the connections, RST on about a `rst` fraction of the connections, and a `rare`
+    fraction of extra copies with SYN / ACK bit clear / ack beyond SND.NXT. Returns (flows, Traffic, host connection table for
+    dk_tcp (one row per flow; the Passive listener's row is DK_TCP_NONE))."""
     from .tcp import CONN_DTYPE, ESTABLISHED
 
     rng = np.random.default_rng(seed + 7)
@@ -125,8 +127,12 @@ def tcp_streams(n: int, nconns: int, ip_len=None, *, reorder: float = 3.0, dup: 
     snd = rng.integers(0, 2**32, nconns, dtype=np.uint64)
     # stream order: arrival rank within the connection plus noise, re-ranked
     arr = np.arange(n)
+    r = rng.random(n)
+    d = r < dup
+    o = (r >= dup) & (r < dup + oow)
+    x = (r >= dup + oow) & (r < dup + oow + 3 * rare)  # copies that the SYN / ACK checks will drop
     key = np.lexsort((arr + rng.uniform(0, reorder + 1e-9, n), f))  # frames sorted by (conn, noisy arrival)
-    order_len = plen[key]
+    order_len = np.where((d | o | x)[key], 0, plen[key])  # resent / stray segments take no new stream bytes
     csum = np.cumsum(order_len)
     first = np.ones(n, bool)
     first[1:] = f[key][1:] != f[key][:-1]
@@ -134,10 +140,7 @@ def tcp_streams(n: int, nconns: int, ip_len=None, *, reorder: float = 3.0, dup: 
     stream_off = np.empty(n, np.int64)
     stream_off[key] = csum - order_len - base
     seq = (isn[f] + stream_off.astype(np.uint64)) & 0xFFFFFFFF
-    r = rng.random(n)
-    d = r < dup
     seq[d] = (seq[d] - rng.integers(1, 3000, int(d.sum())).astype(np.uint64)) & 0xFFFFFFFF
-    o = (r >= dup) & (r < dup + oow)
     seq[o] = (seq[o] + np.uint64(buffer_size) + rng.integers(0, 1 << 20, int(o.sum())).astype(np.uint64)) & 0xFFFFFFFF
     tr.seq = seq.astype(np.uint32)
     tr.ack = ((snd[f] - rng.integers(0, 4096, n).astype(np.uint64)) & 0xFFFFFFFF).astype(np.uint32)
@@ -148,10 +151,13 @@ def tcp_streams(n: int, nconns: int, ip_len=None, *, reorder: float = 3.0, dup: 
     last[key[last_key]] = True
     fin_conn = rng.random(nconns) < fin
     flags[last & fin_conn[f]] |= 0x01
-    for bit in (0x04, 0x02):  # RST, SYN
-        flags[rng.random(n) < rare] |= bit
-    flags[rng.random(n) < rare] &= ~np.uint8(0x10)  # ACK bit clear
-    unsent = rng.random(n) < rare
+    # segments the checks drop carry no stream bytes of their own (rare SYN / no-ACK / unsent-ACK copies), so they
+    # leave no holes; RST closes its connection wherever it lands
+    extra = d | o | x
+    flags[extra & (rng.random(n) < 0.2)] |= 0x02  # SYN
+    flags[extra & (rng.random(n) < 0.2)] &= ~np.uint8(0x10)  # ACK bit clear
+    flags[rng.random(n) < rst * nconns / max(n, 1)] |= 0x04  # RST: about `rst` of the connections get one
+    unsent = extra & (rng.random(n) < 0.2)
     tr.ack[unsent] = ((snd[f[unsent]] + rng.integers(1, 1 << 20, int(unsent.sum())).astype(np.uint64))
                       & 0xFFFFFFFF).astype(np.uint32)
     tr.flags = flags

@@ -123,14 +123,15 @@ def test_streams_through_rx(tcp, n, nconns, batches):
     frames, batch after batch with the connection table carried."""
     import torch
 
-    flows, tr, table = synth.tcp_streams(n * batches, nconns, seed=1000 + n + nconns)
+    flows, tr, table = synth.tcp_streams(n * batches, nconns, buffer_size=1 << 22, seed=1000 + n + nconns)
     blob, off, lens = synth.build_numpy(tr)
-    synth.corrupt_numpy(blob, off, synth.corruption_plan(len(off), 0.01, tr))  # some frames never reach TCP
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(len(off), 0.002, tr))  # a few frames never reach TCP (holes)
     eng = RxEngine(Config(synth.BOB_IPV4), device=0)
     eng.set_sockets(flows)
     peer = OraclePeer(synth.ipv4(synth.BOB_IPV4))
     peer.set_flows(flows)
     exp_t, dev_conns = table.copy(), tcp.conns_to_device(table)
+    hist = np.zeros(len(N.TCP_ACTIONS), np.int64)
     for b in range(batches):
         sl = slice(b * n, (b + 1) * n)
         boff, blens = off[sl], lens[sl]
@@ -145,14 +146,14 @@ def test_streams_through_rx(tcp, n, nconns, batches):
         exp = O.tcp_process(exp_t, exp_rx)
         got_t = tcp.conns_to_host(dev_conns)
         assert_same(got_t, got, exp_t, exp, f"batch {b}")
-        hist = np.bincount(got["action"], minlength=len(N.TCP_ACTIONS))
-        if n >= 20000:
-            for a in ("DELIVERED", "STORED", "DUPLICATE", "SKIP"):
-                assert hist[N.A[a]] > 0, (a, hist)
+        hist += np.bincount(got["action"], minlength=len(N.TCP_ACTIONS))
         # the application reads everything delivered (Receiver::pop moves reader_next, ctrlblk.rs:113-129): window reopens
         exp_t["reader_next"] = exp_t["receive_next"]
         got_t["reader_next"] = got_t["receive_next"]
         dev_conns = tcp.conns_to_device(got_t)
+    if n >= 20000:
+        for a in ("DELIVERED", "STORED", "DUPLICATE", "OUT_OF_WINDOW", "SYN", "NO_ACK", "ACK_UNSENT", "SKIP"):
+            assert hist[N.A[a]] > 0, (a, hist)
     eng.close()
 
 
