@@ -213,6 +213,58 @@ def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=3):
             "reps": reps, "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
 
 
+def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
+    """dk_tcp_rx_process over one dk_rx batch's results (nseg 1460-byte TCP segments spread
+    over nconns established connections, reordered / duplicated / stray as synth.tcp_streams makes them), Mseg/s from
+    HIP events around each call (the connection table is restored from a pristine copy between calls, outside the
+    timed span); the CPU restatement (oracle/dk_tcp_oracle.cpp, 1 thread) on the same arrays beside it."""
+    import torch
+
+    from demikernel_amd import RxResults, synth
+    from demikernel_amd.tcp import TcpOut, TcpReceiver
+    from oracle import oracle as O
+
+    dev = stream.device
+    _, tr, table = synth.tcp_streams(nseg, nconns, 1500, buffer_size=1 << 24)
+    rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
+          "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
+          "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
+    r = RxResults(nseg, 1, device=dev, tcp_fields=True, counts=False)
+    for k, v in rx.items():
+        r.t[k].copy_(torch.from_numpy(v.view(np.int32)))
+    tcp = TcpReceiver(dev.index or 0)
+    pristine = tcp.conns_to_device(table)
+    conns = pristine.clone()
+    out = TcpOut(nseg, len(table), dev.index or 0)
+    times = []
+    with torch.cuda.stream(stream):
+        for i in range(iters + 2):
+            conns.copy_(pristine)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            tcp.process(r, conns, out, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if i >= 2:
+                times.append(e0.elapsed_time(e1) / 1e3)
+    got = out.to_numpy()
+    hist = np.bincount(got["action"], minlength=13)
+    t = float(np.median(times))
+    tcp.close()
+    # CPU restatement on the same segments (bounded: repeat until cpu_seconds)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.tcp_process(table.copy(), rx)
+        reps += 1
+        if time.perf_counter() - t0 >= cpu_seconds:
+            break
+    tc = (time.perf_counter() - t0) / reps
+    return {"mseg_s": round(nseg / t / 1e6, 1), "ms_avg": round(t * 1e3, 4), "segments": nseg, "connections": nconns,
+            "delivered_frac": round(float(hist[1]) / nseg, 3),
+            "cpu_baseline": {"mseg_s": round(nseg / tc / 1e6, 2), "cores": 1, "kind": "port", "reps": reps},
+            "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (store in LDS)"}
+
+
 def tx_rate(eng, batch, frame_bytes, stream, iters=20):
     """dk_tx_checksum kernel time over an HBM-resident batch: frame bytes read, 2 checksum fields written per frame."""
     import torch
@@ -400,6 +452,7 @@ def main():
         # TX checksum fill (dk_tx_checksum) over the same batch (rewrites its checksum fields)
         out["tx_checksum"] = tx_rate(eng, batch, frame_bytes, stream)
         out["tx_checksum"]["traffic"] = load_traffic_profile(name + "_tx")
+        out["tcp_rx"] = tcp_rate(stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -3,16 +3,18 @@
 // The reference queues each delivered segment on its socket (tcp/socket.rs:308-314, ctrlblk.rs:345-347) and
 // ControlBlock::poll runs process_packet on them one at a time (ctrlblk.rs:350-440). Connections are independent;
 // within one, order matters (RCV.NXT, the out-of-order store). For a whole dk_rx batch:
-//   1. dk_tcp_key_kernel: frame -> key (its connection, for delivered TCP segments of a connection in the table; else
-//      nconns) and value (its index); per-connection segment counts; default outputs;
-//   2. an exclusive scan of the counts (each connection's range) and a stable radix sort of (key, index) over the key's
-//      bits (hipCUB / rocPRIM): each connection's segments, contiguous, in arrival order;
-//   3. dk_tcp_gather_kernel: the sorted segments' {seq, ack, meta, payload} into one contiguous array;
-//   4. dk_tcp_walk_kernel: one lane per connection runs its segments through the state machine in order, kBatch
-//      segments' fields loaded together. The walk is the only sequential part (latency-bound, lanes = connections);
-//      everything else is a pass over the batch.
+//   1. dk_tcp_key_kernel (one pass over the batch, coalesced): frame -> key (its connection, for delivered TCP segments
+//      of a connection in the table; else nconns) and its {seq, ack, meta, payload} record; skipped frames' outputs;
+//   2. a stable LSD radix sort of (key, frame index) over the key's bits (rocPRIM onesweep, 8 bits per pass): each
+//      connection's segments contiguous, in arrival order;
+//   3. dk_tcp_range_kernel: each connection's range = lower_bound of its key in the sorted keys;
+//   4. dk_tcp_walk_kernel: one lane per connection (its out-of-order store in LDS) runs its segments through the
+//      state machine in order, reading each segment's record through the sorted frame index (pipelined: indices two
+//      batches of kBatch ahead, records one batch ahead). The walk is the only sequential part
+//      (latency-bound, lanes = connections); everything else is a pass over the batch.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <cerrno>
@@ -24,6 +26,11 @@ namespace {
 
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kBatch = 8;  // segments whose fields a walker lane loads together
+
+// Onesweep for every size above one block: rocPRIM's default switches to a merge sort up to 1M items, 3-4x slower
+// here (20 launches for 1M 15-bit keys vs 2 onesweep passes).
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
 
 __device__ __forceinline__ bool lt(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
 __device__ __forceinline__ bool le(uint32_t a, uint32_t b) { return (int32_t)(a - b) <= 0; }
@@ -39,43 +46,67 @@ struct Params {
     dk_tcp_conn* conns;
     uint32_t nconns;
     uint32_t* keys;
-    uint32_t* vals;
     uint32_t* skeys;
     uint32_t* svals;
-    uint32_t* counts;
-    uint32_t* seg_start;
-    uint4* seg;  // sorted {seq, ack, meta, payload}
+    uint4* rec;        // [n] {seq, ack, meta, payload} in frame order
+    uint32_t* range;   // [nconns + 1]: connection c's segments are svals[range[c] .. range[c + 1])
     dk_tcp_out out;
 };
 
 __global__ __launch_bounds__(kBlock) void dk_tcp_key_kernel(Params P) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= P.n) return;
+    const uint32_t meta = P.meta[i], pay = P.payload[i];
     uint32_t key = P.nconns;
-    if ((P.meta[i] & 0xFFu) == DK_V_OK_TCP) {
+    if ((meta & 0xFFu) == DK_V_OK_TCP) {
         const uint32_t f = P.flow_id[i];
-        if (f < P.nconns && P.conns[f].state != DK_TCP_NONE) {
-            key = f;
-            atomicAdd(P.counts + f, 1u);
-        }
+        if (f < P.nconns && P.conns[f].state != DK_TCP_NONE) key = f;
     }
     P.keys[i] = key;
-    P.vals[i] = i;
-    P.out.action[i] = DK_TCP_SKIP;
-    const uint32_t pay = P.payload[i];
-    P.out.view[i] = dk_tcp_view{i, pay & 0xFFFFu, pay >> 16};
+    P.rec[i] = make_uint4(P.seq[i], P.ack[i], meta, pay);
+    if (key == P.nconns) {  // the walk writes the outputs of every segment it owns
+        P.out.action[i] = DK_TCP_SKIP;
+        P.out.view[i] = dk_tcp_view{i, pay & 0xFFFFu, pay >> 16};
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void dk_tcp_gather_kernel(Params P) {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= P.n || P.skeys[p] >= P.nconns) return;
-    const uint32_t i = P.svals[p];
-    P.seg[p] = make_uint4(P.seq[i], P.ack[i], P.meta[i], P.payload[i]);
+__global__ __launch_bounds__(kBlock) void dk_tcp_range_kernel(Params P) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c > P.nconns) return;
+    uint32_t lo = 0, hi = P.n;  // first p with skeys[p] >= c
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (P.skeys[mid] < c)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    P.range[c] = lo;
 }
 
-// One connection's scalar receive state, in registers during the walk (the store's entries stay in global memory).
+// One connection's scalar receive state, in registers during the walk.
 struct Walk {
     uint32_t state, rn, reader, bufsz, snd, fin_pending, fin_seq, nooo;
+};
+
+// The connection's out-of-order store in LDS, one column per lane ([field][entry][lane]: conflict-free, each lane
+// touches only its own column). Loaded from the table at the start of the walk and written back at the end, so the
+// store's scans and shifts cost LDS latency, not HBM latency.
+constexpr uint32_t kWalkBlock = 64;
+struct Store {
+    uint32_t* lds;  // [4][DK_TCP_OOO_MAX][kWalkBlock] + lane
+    __device__ __forceinline__ uint32_t& start(uint32_t k) { return lds[(0 * DK_TCP_OOO_MAX + k) * kWalkBlock]; }
+    __device__ __forceinline__ uint32_t& ref(uint32_t k) { return lds[(1 * DK_TCP_OOO_MAX + k) * kWalkBlock]; }
+    __device__ __forceinline__ uint32_t& off(uint32_t k) { return lds[(2 * DK_TCP_OOO_MAX + k) * kWalkBlock]; }
+    __device__ __forceinline__ uint32_t& len(uint32_t k) { return lds[(3 * DK_TCP_OOO_MAX + k) * kWalkBlock]; }
+    __device__ __forceinline__ dk_tcp_view view(uint32_t k) { return dk_tcp_view{ref(k), off(k), len(k)}; }
+    __device__ __forceinline__ void set(uint32_t k, uint32_t s, dk_tcp_view v) {
+        start(k) = s;
+        ref(k) = v.ref;
+        off(k) = v.off;
+        len(k) = v.len;
+    }
+    __device__ __forceinline__ void copy(uint32_t to, uint32_t from) { set(to, start(from), view(from)); }
 };
 
 struct Out {  // the connection's delivery slots
@@ -88,24 +119,21 @@ struct Out {  // the connection's delivery slots
     }
 };
 
-__device__ void ooo_remove(dk_tcp_conn* s, Walk& w, uint32_t at) {
-    for (uint32_t k = at; k + 1 < w.nooo; k++) {
-        s->ooo_start[k] = s->ooo_start[k + 1];
-        s->ooo[k] = s->ooo[k + 1];
-    }
+__device__ __forceinline__ void ooo_remove(Store& s, Walk& w, uint32_t at) {
+    for (uint32_t k = at; k + 1 < w.nooo; k++) s.copy(k, k + 1);
     w.nooo--;
 }
 
 // store_out_of_order_segment (ctrlblk.rs:844-941) on the fixed arrays.
-__device__ __noinline__ uint32_t ooo_store(dk_tcp_conn* s, Walk& w, uint32_t new_start, uint32_t new_end,
-                                           dk_tcp_view buf) {
+__device__ __forceinline__ uint32_t ooo_store(Store& s, Walk& w, uint32_t new_start, uint32_t new_end,
+                                              dk_tcp_view buf) {
     uint32_t at = w.nooo;
     bool again = true;
     while (again) {
         again = false;
         at = w.nooo;
         for (uint32_t i = 0; i < w.nooo; i++) {
-            const uint32_t ss = s->ooo_start[i], se = ss + (s->ooo[i].len - 1);
+            const uint32_t ss = s.start(i), se = ss + (s.len(i) - 1);
             if (lt(new_start, ss)) {
                 if (lt(new_end, ss)) {
                     at = i;
@@ -132,22 +160,18 @@ __device__ __noinline__ uint32_t ooo_store(dk_tcp_conn* s, Walk& w, uint32_t new
     }
     // VecDeque::insert at `at`, then pop_back while longer than the cap
     if (at >= DK_TCP_OOO_MAX) return DK_TCP_STORED;
-    for (uint32_t k = min(w.nooo, DK_TCP_OOO_MAX - 1); k > at; k--) {
-        s->ooo_start[k] = s->ooo_start[k - 1];
-        s->ooo[k] = s->ooo[k - 1];
-    }
-    s->ooo_start[at] = new_start;
-    s->ooo[at] = buf;
+    for (uint32_t k = min(w.nooo, DK_TCP_OOO_MAX - 1); k > at; k--) s.copy(k, k - 1);
+    s.set(at, new_start, buf);
     w.nooo = min(w.nooo + 1, DK_TCP_OOO_MAX);
     return DK_TCP_STORED;
 }
 
 // receive_data (ctrlblk.rs:951-1001): true if a stored FIN is now in order.
-__device__ __noinline__ bool receive_data(dk_tcp_conn* s, Walk& w, dk_tcp_view buf, Out& o) {
+__device__ __forceinline__ bool receive_data(Store& s, Walk& w, dk_tcp_view buf, Out& o) {
     uint32_t recv_next = w.rn + buf.len;
     o.push(buf, w);
-    while (w.nooo > 0 && s->ooo_start[0] == recv_next) {
-        const dk_tcp_view t = s->ooo[0];
+    while (w.nooo > 0 && s.start(0) == recv_next) {
+        const dk_tcp_view t = s.view(0);
         ooo_remove(s, w, 0);
         recv_next += t.len;
         o.push(t, w);
@@ -156,7 +180,7 @@ __device__ __noinline__ bool receive_data(dk_tcp_conn* s, Walk& w, dk_tcp_view b
 }
 
 // process_packet (ctrlblk.rs:403-440) for segment g = {seq, ack, meta, payload} of frame i.
-__device__ __noinline__ uint32_t process(dk_tcp_conn* s, Walk& w, uint4 g, uint32_t i, Out& o, dk_tcp_view& view) {
+__device__ __forceinline__ uint32_t process(Store& s, Walk& w, uint4 g, uint32_t i, Out& o, dk_tcp_view& view) {
     const uint32_t flags = (g.z >> 16) & 0xFFu;
     bool syn = flags & 0x02u, fin = flags & 0x01u;
     const bool rst = flags & 0x04u, ack = flags & 0x10u;
@@ -230,46 +254,71 @@ __device__ __noinline__ uint32_t process(dk_tcp_conn* s, Walk& w, uint4 g, uint3
     return action;
 }
 
-__global__ __launch_bounds__(kBlock) void dk_tcp_walk_kernel(Params P) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+__global__ __launch_bounds__(kWalkBlock) void dk_tcp_walk_kernel(Params P) {
+    __shared__ uint32_t lds[4 * DK_TCP_OOO_MAX * kWalkBlock];
+    const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
     if (c >= P.nconns) return;
-    dk_tcp_conn* s = P.conns + c;
-    const uint32_t k0 = P.seg_start[c], cnt = P.counts[c];
+    dk_tcp_conn* t = P.conns + c;
+    const uint32_t k0 = P.range[c], cnt = P.range[c + 1] - k0;
     const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c;
     P.out.deliv_start[c] = d0;
-    Walk w{s->state, s->receive_next, s->reader_next, s->buffer_size, s->send_next, s->fin_pending, s->fin_seq,
-           min(s->ooo_count, DK_TCP_OOO_MAX)};
+    Walk w{t->state, t->receive_next, t->reader_next, t->buffer_size, t->send_next, t->fin_pending, t->fin_seq,
+           min(t->ooo_count, DK_TCP_OOO_MAX)};
+    Store s{lds + threadIdx.x};
+    for (uint32_t k = 0; k < w.nooo; k++) s.set(k, t->ooo_start[k], t->ooo[k]);
     Out o{P.out.deliv + d0, 0, cnt + DK_TCP_DELIV_EXTRA};
+    // Software pipeline over batches of kBatch segments: frame indices two batches ahead, their records one batch
+    // ahead, so neither load level waits in the loop (the walk is latency-bound: about one wave per SIMD).
+    uint32_t ia[kBatch], ib[kBatch], ic[kBatch];
+    uint4 gb[kBatch], gc[kBatch];
+#pragma unroll
+    for (uint32_t j = 0; j < kBatch; j++) {
+        ib[j] = j < cnt ? P.svals[k0 + j] : 0u;
+        ia[j] = kBatch + j < cnt ? P.svals[k0 + kBatch + j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kBatch; j++)
+        if (j < cnt) gb[j] = P.rec[ib[j]];
     for (uint32_t k = 0; k < cnt; k += kBatch) {
-        uint4 g[kBatch];
-        uint32_t idx[kBatch];
 #pragma unroll
         for (uint32_t j = 0; j < kBatch; j++) {
-            if (k + j < cnt) {
-                g[j] = P.seg[k0 + k + j];
-                idx[j] = P.svals[k0 + k + j];
+            gc[j] = gb[j];
+            ic[j] = ib[j];
+        }
+        if (k + kBatch < cnt) {
+#pragma unroll
+            for (uint32_t j = 0; j < kBatch; j++) {
+                if (k + kBatch + j < cnt) gb[j] = P.rec[ia[j]];
+                ib[j] = ia[j];
             }
+        }
+        if (k + 2 * kBatch < cnt) {
+#pragma unroll
+            for (uint32_t j = 0; j < kBatch; j++)
+                if (k + 2 * kBatch + j < cnt) ia[j] = P.svals[k0 + k + 2 * kBatch + j];
         }
 #pragma unroll
         for (uint32_t j = 0; j < kBatch; j++) {
             if (k + j >= cnt) break;
             if (w.state != DK_TCP_ESTABLISHED) {
-                P.out.action[idx[j]] = DK_TCP_UNPROCESSED;
+                P.out.action[ic[j]] = DK_TCP_UNPROCESSED;
+                P.out.view[ic[j]] = dk_tcp_view{ic[j], gc[j].w & 0xFFFFu, gc[j].w >> 16};
                 continue;
             }
             dk_tcp_view v;
-            P.out.action[idx[j]] = (uint8_t)process(s, w, g[j], idx[j], o, v);
-            P.out.view[idx[j]] = v;
+            P.out.action[ic[j]] = (uint8_t)process(s, w, gc[j], ic[j], o, v);
+            P.out.view[ic[j]] = v;
         }
     }
-    s->state = w.state;
-    s->receive_next = w.rn;
-    s->fin_pending = w.fin_pending;
-    s->fin_seq = w.fin_seq;
-    s->ooo_count = w.nooo;
-    for (uint32_t k = w.nooo; k < DK_TCP_OOO_MAX; k++) {
-        s->ooo_start[k] = 0;
-        s->ooo[k] = dk_tcp_view{0, 0, 0};
+    t->state = w.state;
+    t->receive_next = w.rn;
+    t->fin_pending = w.fin_pending;
+    t->fin_seq = w.fin_seq;
+    t->ooo_count = w.nooo;
+    for (uint32_t k = 0; k < DK_TCP_OOO_MAX; k++) {
+        const bool live = k < w.nooo;
+        t->ooo_start[k] = live ? s.start(k) : 0u;
+        t->ooo[k] = live ? s.view(k) : dk_tcp_view{0, 0, 0};
     }
     P.out.deliv_count[c] = o.n;
 }
@@ -301,12 +350,10 @@ int grow(T*& p, size_t& cap, size_t n) {
 
 struct dk_tcp_ctx {
     int device = 0;
-    uint32_t *keys = nullptr, *vals = nullptr, *skeys = nullptr, *svals = nullptr;
-    size_t keys_cap = 0, vals_cap = 0, skeys_cap = 0, svals_cap = 0;
-    uint4* seg = nullptr;
-    size_t seg_cap = 0;
-    uint32_t *counts = nullptr, *seg_start = nullptr;
-    size_t counts_cap = 0, start_cap = 0;
+    uint32_t *keys = nullptr, *skeys = nullptr, *svals = nullptr, *range = nullptr;
+    size_t keys_cap = 0, skeys_cap = 0, svals_cap = 0, range_cap = 0;
+    uint4* rec = nullptr;
+    size_t rec_cap = 0;
     uint8_t* temp = nullptr;
     size_t temp_cap = 0;
 };
@@ -327,8 +374,7 @@ int dk_tcp_ctx_create(int32_t device, dk_tcp_ctx** out) {
 void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     if (!t) return;
     dk_tcp::DeviceGuard g(t->device);
-    for (void* p : {(void*)t->keys, (void*)t->vals, (void*)t->skeys, (void*)t->svals, (void*)t->seg, (void*)t->counts,
-                    (void*)t->seg_start, (void*)t->temp})
+    for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp})
         if (p) (void)hipFree(p);
     delete t;
 }
@@ -347,19 +393,18 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     DeviceGuard g(t->device);
     const hipStream_t s = (hipStream_t)stream;
     int rc = 0;
-    if ((rc = grow(t->keys, t->keys_cap, n)) || (rc = grow(t->vals, t->vals_cap, n)) ||
-        (rc = grow(t->skeys, t->skeys_cap, n)) || (rc = grow(t->svals, t->svals_cap, n)) ||
-        (rc = grow(t->seg, t->seg_cap, n)) || (rc = grow(t->counts, t->counts_cap, nconns)) ||
-        (rc = grow(t->seg_start, t->start_cap, nconns)))
+    if ((rc = grow(t->keys, t->keys_cap, n)) || (rc = grow(t->skeys, t->skeys_cap, n)) ||
+        (rc = grow(t->svals, t->svals_cap, n)) || (rc = grow(t->rec, t->rec_cap, n)) ||
+        (rc = grow(t->range, t->range_cap, (size_t)nconns + 1)))
         return rc;
     int bits = 1;
     while (bits < 32 && (1ull << bits) <= nconns) bits++;  // keys are 0 .. nconns
-    size_t sort_bytes = 0, scan_bytes = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, t->keys, t->skeys, t->vals, t->svals, (int)n, 0, bits,
-                                           s) != hipSuccess ||
-        hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, t->counts, t->seg_start, (int)nconns, s) != hipSuccess)
+    const rocprim::counting_iterator<uint32_t> index(0);
+    size_t sort_bytes = 0;
+    if (rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, t->keys, t->skeys, index, t->svals, n, 0, bits,
+                                              s) != hipSuccess)
         return EINVAL;
-    if ((rc = grow(t->temp, t->temp_cap, std::max(sort_bytes, scan_bytes)))) return rc;
+    if ((rc = grow(t->temp, t->temp_cap, sort_bytes))) return rc;
 
     Params P{};
     P.meta = rx->meta;
@@ -371,29 +416,21 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     P.conns = conns;
     P.nconns = nconns;
     P.keys = t->keys;
-    P.vals = t->vals;
     P.skeys = t->skeys;
     P.svals = t->svals;
-    P.counts = t->counts;
-    P.seg_start = t->seg_start;
-    P.seg = t->seg;
+    P.rec = t->rec;
+    P.range = t->range;
     P.out = *out;
-    if (nconns && hipMemsetAsync(t->counts, 0, nconns * sizeof(uint32_t), s) != hipSuccess) return EINVAL;
-    const dim3 gn((n + kBlock - 1) / kBlock), gc((nconns + kBlock - 1) / kBlock);
-    if (n) hipLaunchKernelGGL(dk_tcp_key_kernel, gn, dim3(kBlock), 0, s, P);
-    if (nconns) {
-        size_t b = t->temp_cap;
-        if (hipcub::DeviceScan::ExclusiveSum(t->temp, b, t->counts, t->seg_start, (int)nconns, s) != hipSuccess)
-            return EINVAL;
-    }
+    const dim3 gn((n + kBlock - 1) / kBlock), gr((nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
     if (n) {
+        hipLaunchKernelGGL(dk_tcp_key_kernel, gn, dim3(kBlock), 0, s, P);
         size_t b = t->temp_cap;
-        if (hipcub::DeviceRadixSort::SortPairs(t->temp, b, t->keys, t->skeys, t->vals, t->svals, (int)n, 0, bits, s) !=
+        if (rocprim::radix_sort_pairs<SortConfig>(t->temp, b, t->keys, t->skeys, index, t->svals, n, 0, bits, s) !=
             hipSuccess)
             return EINVAL;
-        hipLaunchKernelGGL(dk_tcp_gather_kernel, gn, dim3(kBlock), 0, s, P);
     }
-    if (nconns) hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kBlock), 0, s, P);
+    if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
+    if (nconns) hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
     return hipGetLastError() == hipSuccess ? 0 : EINVAL;
 }
 
