@@ -53,6 +53,10 @@ def main():
     stats = os.path.join(src, "bench", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+    tstats = os.path.join(src, "tcp", "run_kernel_stats.csv")
+    if os.path.exists(tstats):
+        shutil.copy(tstats, os.path.join(dst, f"{tag}_tcp_kernel_stats.csv"))
+        shutil.copy(os.path.join(src, "tcp.json"), os.path.join(dst, f"{tag}_tcp_under_rocprof.json"))
     if os.path.exists(os.path.join(src, "bench.json")):
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench_under_rocprof.json"))
     traffic = {}
@@ -67,17 +71,18 @@ def main():
         rx, probe, tx = kbench_info(os.path.join(src, f"fetch_{wl}.log"))
         fk = {k[0]: v for k, v in fc.items() if k[1] == "FETCH_SIZE"}
         wk = {k[0]: v for k, v in wc.items() if k[1] == "WRITE_SIZE"}
-        rxk = next(k for k in fk if "dk_rx_kernel" in k)
+        rxk = next(k for k in fk if "dk_rx_kernel" in k or "dk_rx_split_kernel" in k)
+        rxname = "dk_rx_split_kernel" if "split" in rxk else "dk_rx_kernel"
         pk = next(k for k in fk if "read_probe" in k)
         factor = probe["bytes"] / (fk[pk] * 1024.0)
         rd = fk[rxk] * 1024.0 * factor
         wr = wk.get(rxk, 0.0) * 1024.0
         algo = rx["algo_bytes"]
         traffic[wl] = {"hbm_bytes_per_launch": int(rd + wr), "hbm_read_bytes": int(rd), "hbm_write_bytes": int(wr),
-                       "fetch_size_kb_raw": fk[rxk], "write_size_kb_raw": wk.get(rxk, 0.0),
+                       "kernel": rxname, "fetch_size_kb_raw": fk[rxk], "write_size_kb_raw": wk.get(rxk, 0.0),
                        "fetch_calibration_factor": round(factor, 4), "algorithmic_bytes_per_launch": algo,
                        "source": f"profiles/{tag}_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
-        rows.append([wl, "dk_rx_kernel", f"{fk[rxk]:.0f}", f"{wk.get(rxk, 0.0):.0f}", f"{factor:.4f}", f"{rd:.0f}",
+        rows.append([wl, rxname, f"{fk[rxk]:.0f}", f"{wk.get(rxk, 0.0):.0f}", f"{factor:.4f}", f"{rd:.0f}",
                      f"{wr:.0f}", algo, f"{(rd + wr) / algo:.3f}"])
         rows.append([wl, "read_probe", f"{fk[pk]:.0f}", f"{wk.get(pk, 0.0):.0f}", "", probe["bytes"], "", "", ""])
         txk = next((k for k in fk if "dk_tx_kernel" in k), None)
