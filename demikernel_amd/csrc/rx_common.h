@@ -44,6 +44,7 @@ constexpr uint32_t kFlowNone = 0;    // no flow_counts requested
 constexpr uint32_t kFlowLds = 1;     // per-workgroup packed-u16 LDS histogram + scratch rows + reduce kernel
 constexpr uint32_t kFlowGlobal = 2;  // per-frame u64 global atomics (tables too large for LDS)
 constexpr uint32_t kMaxLdsFlowWords = 16384;  // 64 KiB of LDS -> up to 32768 flows on the LDS path
+constexpr uint32_t kVerdictWords = (DK_V_COUNT + 3) & ~3u;  // verdict histogram columns of a scratch row
 constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
 
 // Kernel parameters (passed by value).
@@ -60,8 +61,10 @@ struct RxParams {
     uint32_t table_mask;
     uint32_t nflows;
     uint32_t flow_mode;      // kFlow*
-    uint32_t flow_words;     // kFlowLds: ceil(nflows / 2)
-    uint32_t* flow_scratch;  // kFlowLds: [grid][flow_words]
+    uint32_t flow_words;     // kFlowLds: ceil(nflows / 2), else 0
+    uint32_t row_words;      // words per workgroup row of flow_scratch: flow_words + (verdict_counts ? kVerdictWords : 0)
+    uint32_t* flow_scratch;  // [grid][row_words]: the packed-u16 flow histogram (kFlowLds), then the u32 verdict
+                             // histogram; nullptr when row_words == 0
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
     uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave
     uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path

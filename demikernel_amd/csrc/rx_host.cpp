@@ -110,6 +110,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
     const uint32_t ntiles = (p.n + 255) / 256;
     p.flow_mode = dk::kFlowNone;
     p.flow_words = 0;
+    p.row_words = 0;
     p.flow_scratch = nullptr;
     uint32_t dyn = 0;
     if (p.res.flow_counts && c->nflows) {
@@ -146,9 +147,12 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
     if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
-    if (p.flow_mode == dk::kFlowLds) {
+    if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
-        int rc = ensure_scratch(fs, (size_t)grid * p.flow_words);
+    // Per-workgroup histogram rows (flow pairs, then verdicts), added up by dk_flow_reduce_kernel.
+    p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
+    if (p.row_words) {
+        int rc = ensure_scratch(fs, (size_t)grid * p.row_words);
         if (rc) return rc;
         p.flow_scratch = fs.p;
     }

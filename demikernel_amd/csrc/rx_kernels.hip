@@ -903,11 +903,16 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
 #ifdef DK_ABL_NOCOUNT  // ablation (tuning only): no flow / verdict counting
     return;
 #endif
+#ifndef DK_ABL_NOFLOWCOUNT  // ablation (tuning only)
     if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
         if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
         else if (P.flow_mode == kFlowGlobal)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
     }
+#endif
+#ifdef DK_ABL_NOVCOUNT  // ablation (tuning only)
+    return;
+#endif
     if (P.res.verdict_counts) {
         uint64_t todo = __ballot(live);
         while (todo) {
@@ -920,11 +925,24 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
     }
 }
 
+// Workgroup exit: the LDS histograms go to this workgroup's scratch row with plain stores — flow words (kFlowLds),
+// then the verdict words — and dk_flow_reduce_kernel adds the rows into the caller's u64 counters. (A u64 device-scope
+// atomic per workgroup on the same few verdict addresses serialises at the memory side: 1024 workgroups cost ~14 us, a
+// third of a 64-byte-frame batch)
+__device__ __forceinline__ void write_row(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
+                                          const uint32_t* s_flow, const uint32_t* s_vh) {
+    if (!P.row_words) return;
+    uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_words;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
+    if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
+}
+
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
 // per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
-// wraps). At exit the histogram row is written with plain stores to flow_scratch[b][*] and dk_flow_reduce_kernel adds
-// the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
+// wraps). At exit both histograms are written with plain stores to flow_scratch[b][*] (write_row) and
+// dk_flow_reduce_kernel adds the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
@@ -986,12 +1004,7 @@ void dk_rx_kernel(RxParams P) {
 
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     __syncthreads();
-    if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
-    if (lds_flows) {
-        uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.flow_words;
-        for (uint32_t k = tid; k < P.flow_words; k += kBlock) row[k] = s_flow[k];
-    }
+    write_row(P, tid, kBlock, lds_flows, s_flow, s_vh);
 }
 
 // Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
@@ -1089,29 +1102,33 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
         __syncthreads();
     }
     if (finisher && nstg) flush_split(P, stg, nstg, r, klast);
-    if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + tid), (unsigned long long)s_vh[tid]);
-    if (lds_flows) {
-        uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.flow_words;
-        for (uint32_t k = tid; k < P.flow_words; k += kSplitBlock) row[k] = s_flow[k];
-    }
+    write_row(P, tid, kSplitBlock, lds_flows, s_flow, s_vh);
 }
 
-// Adds the per-workgroup packed-u16 rows of flow_scratch[rows][words] into flow_counts[nflows] (u64). Block (x, y)
-// sums rows [y * kReduceRows, ...) of 256 consecutive words (coalesced row reads, loads independent) and adds the two
-// 64-bit partials with device-scope atomics; (rows / kReduceRows) * nflows adds in all, contiguous per wave.
+// Adds the per-workgroup rows of flow_scratch[rows][row_words] into the caller's u64 counters: columns
+// [0, flow_words) are packed-u16 flow pairs (flow_counts), the next DK_V_COUNT are u32 verdict counts
+// (verdict_counts). Block (x, y) sums rows [y * kReduceRows, ...) of 256 consecutive columns (coalesced row reads,
+// loads independent) and adds its 64-bit partials with device-scope atomics: rows / kReduceRows adds per counter.
 constexpr uint32_t kReduceRows = 32;
 __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* scratch, uint32_t rows,
-                                                                uint32_t words, uint32_t nflows, uint64_t* counts) {
+                                                                uint32_t row_words, uint32_t flow_words,
+                                                                uint32_t nflows, uint64_t* counts,
+                                                                uint64_t* verdicts) {
     const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
-    if (w >= words) return;
+    if (w >= row_words) return;
     const uint32_t r0 = blockIdx.y * kReduceRows, r1 = min(rows, r0 + kReduceRows);
     uint64_t lo = 0, hi = 0;
 #pragma unroll 8
     for (uint32_t r = r0; r < r1; r++) {
-        const uint32_t x = scratch[(size_t)r * words + w];
+        const uint32_t x = scratch[(size_t)r * row_words + w];
         lo += x & 0xFFFFu;
         hi += x >> 16;
+    }
+    if (w >= flow_words) {  // verdict column: a plain u32 count
+        const uint32_t v = w - flow_words;
+        const uint64_t t = lo + (hi << 16);
+        if (t && v < DK_V_COUNT) atomicAdd(reinterpret_cast<unsigned long long*>(verdicts + v), (unsigned long long)t);
+        return;
     }
     if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2 * w), (unsigned long long)lo);
     if (hi && 2 * w + 1 < nflows) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2 * w + 1), (unsigned long long)hi);
@@ -1297,10 +1314,11 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     else
         hipLaunchKernelGGL((dk::dk_rx_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     if (hipGetLastError() != hipSuccess) return 5;
-    if (p.flow_mode == dk::kFlowLds) {
-        const dim3 g2((p.flow_words + dk::kBlock - 1) / dk::kBlock, (grid + dk::kReduceRows - 1) / dk::kReduceRows);
+    if (p.row_words) {
+        const dim3 g2((p.row_words + dk::kBlock - 1) / dk::kBlock, (grid + dk::kReduceRows - 1) / dk::kReduceRows);
         hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, (hipStream_t)stream,
-                           p.flow_scratch, grid, p.flow_words, p.nflows, p.res.flow_counts);
+                           p.flow_scratch, grid, p.row_words, p.flow_words, p.nflows, p.res.flow_counts,
+                           p.res.verdict_counts);
         if (hipGetLastError() != hipSuccess) return 5;
     }
     return 0;
