@@ -70,6 +70,7 @@ struct RxParams {
     uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path
     uint32_t stage;          // launch the instantiation that stages result stores in registers (large frames)
     uint32_t split;          // launch the split (stream waves / finish waves) kernel (largest frames)
+    uint32_t small;          // launch the small-frame kernel (minimum-size frames)
     dk_rx_results res;
 };
 
@@ -88,7 +89,7 @@ struct TxParams {
 // Launchers implemented in rx_kernels.hip (internal symbols, not part of the C ABI).
 // Receive kernel families (launch_batch picks one per launch).
 namespace dk {
-constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2;
+constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFamilySmall = 3;
 }
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);

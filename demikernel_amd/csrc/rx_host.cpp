@@ -135,15 +135,21 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
     p.split = bytes_per_frame >= 1024 ? 1u : 0u;
     if (const char* e = getenv("DK_RX_STAGE")) p.stage = atoi(e) ? 1u : 0u;  // tuning
     if (const char* e = getenv("DK_RX_SPLIT")) p.split = atoi(e) ? 1u : 0u;  // tuning
+    p.small = bytes_per_frame <= 96 ? 1u : 0u;
+    if (const char* e = getenv("DK_RX_SMALL")) p.small = atoi(e) ? 1u : 0u;  // tuning
+    if (p.small) p.split = p.stage = 0;
     p.sched = 0;
     if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
-    const uint32_t family = p.split ? dk::kFamilySplit : p.stage ? dk::kFamilyStaged : dk::kFamilyUnstaged;
+    const uint32_t family = p.small   ? dk::kFamilySmall
+                            : p.split ? dk::kFamilySplit
+                            : p.stage ? dk::kFamilyStaged
+                                      : dk::kFamilyUnstaged;
     if (c->occ_dyn != dyn || c->occ_family != family) {
         c->occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn, family), 1);
         c->occ_dyn = dyn;
         c->occ_family = family;
     }
-    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.split ? 1u : p.stage ? 3u : 4u);
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u);
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
     if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning

@@ -630,7 +630,8 @@ __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t fra
 // LE-half sum of frame bytes [34, E) on the fast path (IHL == 5), from what stream_chunk left: the register window
 // for small frames; for big frames sum(all granules) - sum[0, 34) - sum[E, 16 * nblk), the last granule being in
 // LDS; a direct byte sum when IPv4 total_length ends more than 32 bytes before the last block (rare; sets resum).
-__device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WaveLds& W, uint32_t lane, const uint8_t* f,
+template <class WL>
+__device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WL& W, uint32_t lane, const uint8_t* f,
                                                  int E, bool& resum) {
     const RegAcc& R = C.R;
     if (!C.big) {
@@ -684,8 +685,8 @@ constexpr int kStageK = DK_STAGE_K;
 
 // Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
 // results (stored, or handed back in rec for staging).
-template <bool kShift, bool kStage>
-__device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WaveLds& W,
+template <bool kShift, bool kStage, class WL>
+__device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
                                           uint32_t& fid_out, Rec& rec) {
 #ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
@@ -1007,6 +1008,153 @@ void dk_rx_kernel(RxParams P) {
     write_row(P, tid, kBlock, lds_flows, s_flow, s_vh);
 }
 
+// Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
+// probe -> stores is latency-bound at 64 bytes a frame, so this kernel drops the quarter-wave streaming machinery
+// (its 48 load registers and 27 KB of LDS per workgroup) for more resident waves, and loads the next chunk's frame
+// registers (descriptors two chunks ahead) while the current chunk is parsed. The rare frame whose span exceeds the
+// 64-byte register window is summed by the whole wave, one frame at a time, and hands the owner lane exactly what
+// stream_chunk would (header window, whole-granule sum, last granule in LDS), so phase C is shared code.
+struct SmallLds {
+    uint4 tail[64];  // the last granule of each big frame (seg_sum_fast)
+};
+#ifndef DK_SMALL_PF
+#define DK_SMALL_PF 0  // prefetch the next chunk's frame registers (measured: no gain)
+#endif
+#ifndef DK_MIN_WAVES_SMALL
+#define DK_MIN_WAVES_SMALL 6
+#endif
+template <bool kShift>
+__device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uint32_t lane, uint32_t off, const Blob& B,
+                                                 SmallLds& W, Chunk& C) {
+    RegAcc& R = C.R;
+    uint32_t x[4] = {0, 0, 0, 0};
+    C.fsum = 0;
+    uint64_t bm = __ballot(F.big);
+    if (bm) {
+        while (bm) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(bm);
+            bm &= bm - 1;
+            const uint32_t base = __builtin_amdgcn_readlane(off - F.sh, j);
+            const uint32_t nb = __builtin_amdgcn_readlane(F.nblk, j);
+            uint32_t acc = 0;
+            uint4 g0 = make_uint4(0, 0, 0, 0);  // granule `lane`: the header window is granules 0..4
+            for (uint32_t b0 = 0; b0 < nb; b0 += 128) {
+                const uint32_t b1 = b0 + lane, b2 = b1 + 64;
+                const uint4 q1 = B.template ld<DK_NT_LOADS != 0>(b1 < nb ? base + 16 * b1 : kOob);
+                const uint4 q2 = B.template ld<DK_NT_LOADS != 0>(b2 < nb ? base + 16 * b2 : kOob);
+                acc = block_sum(q2, block_sum(q1, acc));
+                if (b0 == 0) g0 = q1;
+                if (b1 + 1 == nb) W.tail[j] = q1;
+                if (b2 + 1 == nb) W.tail[j] = q2;
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) acc += (uint32_t)__shfl_xor((int)acc, o);
+            uint32_t h[20];
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                h[4 * k + 0] = (uint32_t)__shfl((int)g0.x, k);
+                h[4 * k + 1] = (uint32_t)__shfl((int)g0.y, k);
+                h[4 * k + 2] = (uint32_t)__shfl((int)g0.z, k);
+                h[4 * k + 3] = (uint32_t)__shfl((int)g0.w, k);
+            }
+            if (lane == j) {
+                C.fsum = acc;
+#pragma unroll
+                for (int k = 0; k < 16; k++) R.w[k] = h[k];
+#pragma unroll
+                for (int k = 0; k < 4; k++) x[k] = h[16 + k];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (kShift && __ballot(F.vec && F.sh != 0)) {
+        if (F.big && F.sh != 0) C.fsum -= block_sum_masked(R.w[0], R.w[1], R.w[2], R.w[3], 0, (int)F.sh, 0);
+        if (F.vec && F.sh != 0) realign(R.w, x, F.sh);
+    }
+    C.sh = F.sh;
+    C.inb = F.inb;
+    C.vec = F.vec;
+    C.big = F.big;
+    C.nblk = F.nblk;
+}
+
+template <bool kShift>
+__global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
+    __shared__ SmallLds s_wave[kWaves];
+    __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6;
+    const bool lds_flows = P.flow_mode == kFlowLds;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
+    __syncthreads();
+
+    const WaveRange r = wave_range(P.sched, P.n, wv, lane);
+    const Blob B(P.frames, P.frames_bytes);
+    SmallLds& W = s_wave[wv];
+    // Pipeline: chunk k is parsed while chunk k + 1's frame registers and chunk k + 2's descriptors load.
+    uint32_t c, lim, c1 = 0, lim1 = 0, c2 = 0, lim2 = 0;
+    bool have = r.chunk(0, c, lim);
+    bool have1 = have && r.chunk(1, c1, lim1);
+    uint32_t off = 0, len = 0, off1 = 0, len1 = 0;
+    if (have && c + r.lane_off < lim) {
+        off = P.off[c + r.lane_off];
+        len = P.len[c + r.lane_off];
+    }
+    if (have1 && c1 + r.lane_off < lim1) {
+        off1 = P.off[c1 + r.lane_off];
+        len1 = P.len[c1 + r.lane_off];
+    }
+    Chunk C;
+    FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
+    small_load(F, B, off, C.R);
+    for (uint32_t k = 0; have; k++) {
+        const uint32_t i = c + r.lane_off;
+        const bool live = i < lim;
+        const bool have2 = have1 && r.chunk(k + 2, c2, lim2);
+        uint32_t off2 = 0, len2 = 0;
+        if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead
+            off2 = P.off[c2 + r.lane_off];
+            len2 = P.len[c2 + r.lane_off];
+        }
+        const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + r.lane_off < lim1, off1, len1);
+#if DK_SMALL_PF
+        RegAcc R1;
+        small_load(F1, B, off1, R1);  // next chunk's frame registers, in flight during this chunk's phase C
+#endif
+        small_big_frames(F, lane, off, B, W, C);
+        uint32_t v, fid;
+        Rec rec;
+        rx_finish<kShift, false>(P, i, live, lane, W, off, len, C, v, fid, rec);
+        count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+        // rotate the pipeline
+        have = have1;
+        c = c1;
+        lim = lim1;
+        off = off1;
+        len = len1;
+        F = F1;
+#if DK_SMALL_PF
+        C.R = R1;
+#else
+        small_load(F, B, off, C.R);
+#endif
+        have1 = have2;
+        c1 = c2;
+        lim1 = lim2;
+        off1 = off2;
+        len1 = len2;
+    }
+    __syncthreads();
+    write_row(P, tid, kBlock, lds_flows, s_flow, s_vh);
+}
+
 // Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
 // chunk p into LDS buffer p % 2 (header windows, last granules, whole-frame sums) while finish waves 4..7 run phase C
 // of chunk p - 1 from the other buffer; one workgroup barrier per period. The streaming waves never stop for parse,
@@ -1290,6 +1438,9 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     if (family == dk::kFamilySplit)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
+    else if (family == dk::kFamilySmall)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true>, dk::kBlock,
+                                                          dyn_lds_bytes);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &blocks, family == dk::kFamilyStaged ? dk::dk_rx_kernel<true, true> : dk::dk_rx_kernel<true, false>,
@@ -1301,7 +1452,11 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
-    if (p.split && p.aligned16)
+    if (p.small && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+    else if (p.small)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+    else if (p.split && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<false>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<true>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);

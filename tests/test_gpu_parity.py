@@ -103,11 +103,13 @@ def test_random_batches(torch_cuda, mix, hint):
 
 @pytest.mark.parametrize("grid", [None, "2", "7"])
 @pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
-@pytest.mark.parametrize("family", ["unstaged", "staged", "split"])
+@pytest.mark.parametrize("family", ["unstaged", "staged", "split", "small"])
 def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
-    """Every kernel family (results stored per chunk / staged in registers / split stream+finish waves) under every
-    wave schedule, with grids small enough that each wave walks many chunks (staged results flushed mid-loop and at
-    exit) and with the default grid. The split kernel always walks sched 0."""
+    """Every kernel family (results stored per chunk / staged in registers / split stream+finish waves / small-frame
+    kernel, whose frames past the 64-byte window are summed wave-wide) under every wave schedule, with grids small
+    enough that each wave walks many chunks (staged results flushed mid-loop and at exit) and with the default grid.
+    The split kernel always walks sched 0."""
+    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
     monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
     monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
     monkeypatch.setenv("DK_RX_SCHED", sched)
@@ -134,6 +136,27 @@ def test_misaligned_and_offsets(torch_cuda):
     check(blob, off[perm], lens2[perm], flows, ctx="misaligned")
     # a wrong DK_RX_BATCH_ALIGNED16 hint costs speed only: misaligned frames then take the byte path
     check(blob, off[perm], lens2[perm], flows, ctx="misaligned, aligned16 hint", aligned16=True)
+
+
+def test_small_kernel_mixed(torch_cuda, monkeypatch):
+    """The small-frame kernel on what it is chosen for (minimum-size frames) with a few large frames mixed in, at
+    every even and odd offset mod 16: the wave-wide sum of frames past the register window, the realigned header
+    window and the last granule in LDS must give the oracle's result."""
+    monkeypatch.setenv("DK_RX_SMALL", "1")
+    flows = np.concatenate([synth.make_flows(64, kind="udp"), synth.make_flows(64)])
+    n = 4000
+    rng = np.random.default_rng(12)
+    ip_len = np.full(n, 50, np.uint16)
+    big = rng.random(n) < 0.03
+    ip_len[big] = rng.integers(51, 1500, int(big.sum()))
+    tr = synth.traffic(n, ip_len, flows, seed=13)
+    blob0, off0, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob0, off0, synth.corruption_plan(n, 0.05, tr))
+    frames = [blob0[o:o + L].tobytes() for o, L in zip(off0, lens)]
+    blob, off, lens2 = F.pack(frames, align=64, misalign=list(range(16)))
+    check(blob, off, lens2, flows, ctx="small kernel, misaligned")
+    blob, off, lens2 = F.pack(frames, align=64)
+    check(blob, off, lens2, flows, ctx="small kernel, aligned16 hint", aligned16=True)
 
 
 def test_fuzz_headers(torch_cuda):
