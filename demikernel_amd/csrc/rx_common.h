@@ -82,6 +82,7 @@ struct TxParams {
     const uint16_t* len;
     uint32_t n;
     uint32_t sched;  // as RxParams::sched
+    uint32_t split;  // launch the split (stream waves / finish waves) kernel: one 512-thread workgroup per CU
 };
 
 }  // namespace dk

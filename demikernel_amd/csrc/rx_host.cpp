@@ -467,8 +467,11 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
         occ = (uint32_t)std::max(dk_tx_resident_blocks(), 1);
         dev_cached = dev;
     }
-    dk::TxParams p{frames, frames_bytes, off, len, n, frames_bytes / n >= 1024 ? 1u : 0u};
-    uint32_t per_cu = std::min<uint32_t>(occ, p.sched ? 3u : 4u);
+    // Large frames: the split kernel (stream waves + finish waves, one 512-thread workgroup per CU, sched 0).
+    const bool big = frames_bytes / n >= 1024;
+    dk::TxParams p{frames, frames_bytes, off, len, n, big ? 1u : 0u, big ? 1u : 0u};
+    if (const char* e = getenv("DK_TX_SPLIT")) p.split = atoi(e) ? 1u : 0u;  // tuning
+    uint32_t per_cu = p.split ? 1u : std::min<uint32_t>(occ, p.sched ? 3u : 4u);
     if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
     if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);  // tuning
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);

@@ -1354,10 +1354,18 @@ __device__ __noinline__ void tx_slow(uint8_t* f, uint32_t len) {
     f[cs_at + 1] = (uint8_t)c;
 }
 
-__device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t lane, WaveLds& W, uint32_t off,
-                                        uint32_t len) {
-    Chunk C;
-    stream_chunk<true>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+// A frame's rewritten 64-byte header window, held in registers by the split TX kernel's finish waves until a burst.
+constexpr uint32_t kNoWin = 0xFFFFFFFFu;
+struct TxWin {
+    uint32_t d[16];
+    uint32_t off;  // frame offset in the blob; kNoWin: nothing staged
+};
+// Checksum computation and field writes of one lane's frame from what the streaming left in C and W. kStage: the
+// full-window rewrite is handed back in win instead of stored (other writes are stored at once).
+template <bool kStage>
+__device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, const WaveLds& W, uint32_t off,
+                                          uint32_t len, const Chunk& C, TxWin& win) {
+    win.off = kNoWin;
     if (!C.inb) return;
     uint8_t* f = P.frames + off;
     const RegAcc& R = C.R;
@@ -1391,9 +1399,28 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
         d[6] = (d[6] & 0xFFFF0000u) | bswap16(ipc);
         if (l4 && tcp) d[12] = (d[12] & 0xFFFFu) | (bswap16(c) << 16);
         if (l4 && !tcp) d[10] = (d[10] & 0xFFFF0000u) | bswap16(c);
+#ifdef DK_TX_ABL_NOSTORE  // ablation (tuning only): no window write
+        if ((d[6] ^ d[12] ^ d[10]) != 0x9E3779B1u) return;
+#endif
+        if (kStage) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) win.d[k] = d[k];
+            win.off = off;
+            return;
+        }
         uint4* q = reinterpret_cast<uint4*>(f);
+#if defined(DK_TX_ABL_NT)  // tuning: nontemporal window stores
+#pragma unroll
+        for (int k = 0; k < 16; k++) __builtin_nontemporal_store(d[k], reinterpret_cast<uint32_t*>(f) + k);
+        return;
+#endif
 #pragma unroll
         for (int k = 0; k < 4; k++) q[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+#ifdef DK_TX_ABL_W128  // ablation (tuning only, wrong bytes 64..127): whole 128-byte line writes
+        if (len >= 128)
+#pragma unroll
+            for (int k = 4; k < 8; k++) q[k] = make_uint4(d[0], d[1], d[2], d[3]);
+#endif
         return;
     }
 #endif
@@ -1402,6 +1429,96 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
         if (tcp) store_field<50>(f, R, len, C.sh, c);
         else store_field<40>(f, R, len, C.sh, c);
     }
+}
+
+__device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t lane, WaveLds& W, uint32_t off,
+                                        uint32_t len) {
+    Chunk C;
+    stream_chunk<true>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+    TxWin win;
+    tx_finish<false>(P, lane, W, off, len, C, win);
+}
+
+#ifndef DK_TX_STAGE_K
+#define DK_TX_STAGE_K 0  // measured: no gain at 4, 6 or 8; kept as a tuning option
+#endif
+#if DK_TX_STAGE_K > 0
+constexpr int kTxStageK = DK_TX_STAGE_K;  // chunks of header windows a finish wave holds before one burst of stores
+__device__ __forceinline__ void flush_tx(const TxParams& P, const TxWin (&stg)[kTxStageK], uint32_t nst) {
+#pragma unroll
+    for (int q = kTxStageK - 1; q >= 0; q--) {
+        if ((uint32_t)q >= nst || stg[q].off == kNoWin) continue;
+        uint4* p = reinterpret_cast<uint4*>(P.frames + stg[q].off);
+#pragma unroll
+        for (int k = 0; k < 4; k++) p[k] = make_uint4(stg[q].d[4 * k], stg[q].d[4 * k + 1], stg[q].d[4 * k + 2], stg[q].d[4 * k + 3]);
+    }
+}
+#endif
+
+// Split TX kernel (large frames), the receive split kernel's structure: stream waves 0..3 run phases A+B of chunk p
+// into LDS buffer p % 2, finish waves 4..7 compute chunk p - 1's checksums and rewrite its header windows; the
+// streaming waves never wait on the checksum arithmetic or the writes.
+__global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P) {
+    __shared__ WaveLds s_buf[2][kWaves];  // [period parity][stream wave]
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6, sw = wv & (kWaves - 1);
+    const bool finisher = wv >= (uint32_t)kWaves;
+    const WaveRange r = wave_range(0, P.n, sw, lane);
+    const WaveRange r0 = wave_range(0, P.n, 0, lane);
+    uint32_t nper = 0, c0, l0;
+    while (r0.chunk(nper, c0, l0)) nper++;
+    const Blob B(P.frames, P.frames_bytes);
+#if DK_TX_STAGE_K > 0
+    TxWin stg[kTxStageK];
+    uint32_t nstg = 0;  // wave-uniform
+#endif
+    for (uint32_t p = 0; p <= nper; p++) {
+        uint32_t c, lim;
+        if (!finisher) {
+            if (r.chunk(p, c, lim)) {
+                WaveLds& W = s_buf[p & 1][sw];
+                const uint32_t i = c + r.lane_off;
+                const bool live = i < lim;
+                const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+                const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
+                const CoopPlan pl = coop_plan(F, lane, off, W);
+                for (uint32_t rr = 0; rr * 4 < pl.ncoop; rr += kRoundsPerStep) {
+                    CoopStep S;
+                    coop_issue(pl, rr, lane, W, B, S, 0);
+                    coop_finish<true>(pl, rr, lane, W, B, S);
+                }
+            }
+        } else if (p > 0 && r.chunk(p - 1, c, lim)) {
+            WaveLds& W = s_buf[(p - 1) & 1][sw];
+            const uint32_t i = c + r.lane_off;
+            const bool live = i < lim;
+            const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+            const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
+            Chunk C;
+            small_load(F, B, off, C.R);
+            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 1};
+            coop_gather(F, pl, lane, W, C);
+#if DK_TX_STAGE_K > 0
+            TxWin win;
+            tx_finish<true>(P, lane, W, off, len, C, win);
+#pragma unroll
+            for (int q = kTxStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
+            stg[0] = win;
+            if (++nstg == (uint32_t)kTxStageK) {
+                flush_tx(P, stg, nstg);
+                nstg = 0;
+            }
+#else
+            TxWin win;
+            tx_finish<false>(P, lane, W, off, len, C, win);
+#endif
+        }
+        __syncthreads();
+    }
+#if DK_TX_STAGE_K > 0
+    if (finisher && nstg) flush_tx(P, stg, nstg);
+#endif
 }
 
 // Persistent, same schedule as dk_rx_kernel.
@@ -1487,6 +1604,9 @@ int dk_tx_resident_blocks() {
 
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
-    hipLaunchKernelGGL(dk::dk_tx_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, p);
+    if (p.split)
+        hipLaunchKernelGGL(dk::dk_tx_split_kernel, dim3(grid), dim3(dk::kSplitBlock), 0, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(dk::dk_tx_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

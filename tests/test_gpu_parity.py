@@ -255,7 +255,9 @@ def tx_check(blob, off, lens, ctx=""):
     assert bad.size == 0, f"{ctx}: {bad.size} bytes differ, first at blob offset {bad[:8]}"
 
 
-def test_tx_checksum_matches_oracle(torch_cuda):
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_tx_checksum_matches_oracle(torch_cuda, monkeypatch, split):
+    monkeypatch.setenv("DK_TX_SPLIT", split)  # both TX kernels (the split one is chosen for >= 1 KiB per frame)
     flows = synth.make_flows(64)
     n = 5000
     tr = synth.traffic(n, np.random.default_rng(8).integers(28, 3000, n).astype(np.uint16), flows)
@@ -265,9 +267,11 @@ def test_tx_checksum_matches_oracle(torch_cuda):
     tx_check(blob2, off2, lens2, "random lengths")
 
 
-def test_tx_checksum_malformed_and_options(torch_cuda):
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_tx_checksum_malformed_and_options(torch_cuda, monkeypatch, split):
     """Every corpus / fuzz / option frame (non-IPv4, bad lengths, bad data offsets, IHL > 5, short UDP): the TX fill
-    touches exactly what serialize_and_attach's restatement touches, at every alignment class."""
+    touches exactly what serialize_and_attach's restatement touches, at every alignment class, in both TX kernels."""
+    monkeypatch.setenv("DK_TX_SPLIT", split)
     rng = np.random.default_rng(77)
     base = [c[1] for c in F.verdict_corpus()]
     pl = bytes(range(200))
