@@ -265,6 +265,14 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
             "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (store in LDS)"}
 
 
+def rx_kernel_name(frame_bytes, n):
+    """The receive kernel family the host picks for a batch (rx_host.cpp launch_batch: mean blob bytes per frame; the
+    blob holds 64-byte-aligned slots, so its size is rounded up per frame)."""
+    per = frame_bytes // max(n, 1)
+    return ("dk_rx_small_kernel" if per <= 96 else "dk_rx_split_kernel" if per >= 1024 else
+            "dk_rx_kernel (staged)" if per >= 128 else "dk_rx_kernel")
+
+
 def tx_rate(eng, batch, frame_bytes, stream, iters=20):
     """dk_tx_checksum kernel time over an HBM-resident batch: frame bytes read, 2 checksum fields written per frame."""
     import torch
@@ -281,7 +289,8 @@ def tx_rate(eng, batch, frame_bytes, stream, iters=20):
     algo = frame_bytes + batch.n * (DESC_BYTES + 4)
     return {"gbps": round(frame_bytes / t / 1e9, 1), "kernel_ms_avg": round(t * 1e3, 4),
             "roofline_achieved_gbps": round(algo / t / 1e9, 1), "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4),
-            "algorithmic_bytes_per_launch": algo}
+            "algorithmic_bytes_per_launch": algo,
+            "kernel": "dk_tx_split_kernel" if frame_bytes // max(batch.n, 1) >= 1024 else "dk_tx_kernel"}
 
 
 def read_ceiling(batch, stream, iters=10):
@@ -414,7 +423,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms_avg": round(kern_avg * 1e3, 4),
-                     "algorithmic_bytes_per_launch": algo},
+                     "algorithmic_bytes_per_launch": algo, "kernel": rx_kernel_name(frame_bytes, batch.n)},
     }
     if not args.no_extras:
         ceil_gbs, ceil_cfg = read_ceiling(batch, stream)
@@ -442,8 +451,13 @@ def main():
         r3 = eng3.results(b3[0].n)
         w3, k3, _ = time_kernel(eng3, b3, r3, 40, 4, stream)
         n3 = b3[0].n
+        k3avg = float(np.mean(k3))
+        algo3 = n3 * (64 + DESC_BYTES + RESULT_BYTES)
         out["c3_udp64"] = {"gbps": round(n3 * 64 * 40 / w3 / 1e9, 2), "mpkt_s": round(n3 * 40 / w3 / 1e6, 1),
-                           "kernel_ms_avg": round(float(np.mean(k3)) * 1e3, 4)}
+                           "kernel_ms_avg": round(k3avg * 1e3, 4), "kernel": "dk_rx_small_kernel",
+                           "algorithmic_bytes_per_launch": algo3,
+                           "roofline_achieved_gbps": round(algo3 / k3avg / 1e9, 1),
+                           "roofline_frac": round(algo3 / k3avg / 1e9 / HBM_PEAK_GBS, 4)}
         del b3, r3, eng3
         # host-resident path (NIC ring / socket buffer in pinned host memory): H2D frames + descriptors, kernel,
         # D2H results, pipelined on 3 streams (dk_rx_process_host). Reported beside `value`, never as `value`.

@@ -1255,22 +1255,36 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
 
 // Adds the per-workgroup rows of flow_scratch[rows][row_words] into the caller's u64 counters: columns
 // [0, flow_words) are packed-u16 flow pairs (flow_counts), the next DK_V_COUNT are u32 verdict counts
-// (verdict_counts). Block (x, y) sums rows [y * kReduceRows, ...) of 256 consecutive columns (coalesced row reads,
-// loads independent) and adds its 64-bit partials with device-scope atomics: rows / kReduceRows adds per counter.
-constexpr uint32_t kReduceRows = 32;
+// (verdict_counts). Block (x, y) = 64 columns x kReduceRows rows: wave w sums every 4th row of the block's rows (lane =
+// column: 256-byte row pieces, 8 independent loads in flight per lane), the 4 waves combine in LDS and the block adds
+// its 64-bit partials with device-scope atomics: rows / kReduceRows adds per counter.
+constexpr uint32_t kReduceRows = 64;
+constexpr uint32_t kReduceCols = 64;
 __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* scratch, uint32_t rows,
                                                                 uint32_t row_words, uint32_t flow_words,
                                                                 uint32_t nflows, uint64_t* counts,
                                                                 uint64_t* verdicts) {
-    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
-    if (w >= row_words) return;
+    __shared__ uint64_t s_part[kWaves][2][kReduceCols];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t w = blockIdx.x * kReduceCols + lane;
     const uint32_t r0 = blockIdx.y * kReduceRows, r1 = min(rows, r0 + kReduceRows);
     uint64_t lo = 0, hi = 0;
+    if (w < row_words) {
 #pragma unroll 8
-    for (uint32_t r = r0; r < r1; r++) {
-        const uint32_t x = scratch[(size_t)r * row_words + w];
-        lo += x & 0xFFFFu;
-        hi += x >> 16;
+        for (uint32_t r = r0 + wv; r < r1; r += kWaves) {
+            const uint32_t x = scratch[(size_t)r * row_words + w];
+            lo += x & 0xFFFFu;
+            hi += x >> 16;
+        }
+    }
+    s_part[wv][0][lane] = lo;
+    s_part[wv][1][lane] = hi;
+    __syncthreads();
+    if (wv != 0 || w >= row_words) return;
+#pragma unroll
+    for (int k = 1; k < kWaves; k++) {
+        lo += s_part[k][0][lane];
+        hi += s_part[k][1][lane];
     }
     if (w >= flow_words) {  // verdict column: a plain u32 count
         const uint32_t v = w - flow_words;
@@ -1587,7 +1601,8 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
         hipLaunchKernelGGL((dk::dk_rx_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     if (hipGetLastError() != hipSuccess) return 5;
     if (p.row_words) {
-        const dim3 g2((p.row_words + dk::kBlock - 1) / dk::kBlock, (grid + dk::kReduceRows - 1) / dk::kReduceRows);
+        const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
+                      (grid + dk::kReduceRows - 1) / dk::kReduceRows);
         hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, (hipStream_t)stream,
                            p.flow_scratch, grid, p.row_words, p.flow_words, p.nflows, p.res.flow_counts,
                            p.res.verdict_counts);

@@ -15,11 +15,16 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d $OUT/bench -o run --out
   python3 $R/bench.py --steps 50 --warmup 5 --cpu-seconds 2 --no-extras > $OUT/bench.json 2> $OUT/bench.err || exit 11
 for WL in c2_tcp1500 c3_udp64 c4_imix c5_tcp1500_10k; do
   TX=""; [ $WL = c2_tcp1500 ] && TX=--tx
-  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "dk_rx_kernel|dk_rx_split_kernel|dk_tx_kernel|read_probe" -T -d $OUT/fetch_$WL -o run --output-format csv -- \
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "dk_rx_kernel|dk_rx_split_kernel|dk_rx_small_kernel|dk_tx_kernel|dk_tx_split_kernel|read_probe" -T -d $OUT/fetch_$WL -o run --output-format csv -- \
     python3 $R/tools/kbench.py --workload $WL --iters 5 --probe-one $TX > $OUT/fetch_$WL.log 2>&1 || exit 12
-  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "dk_rx_kernel|dk_rx_split_kernel|dk_tx_kernel|read_probe" -T -d $OUT/write_$WL -o run --output-format csv -- \
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "dk_rx_kernel|dk_rx_split_kernel|dk_rx_small_kernel|dk_tx_kernel|dk_tx_split_kernel|read_probe" -T -d $OUT/write_$WL -o run --output-format csv -- \
     python3 $R/tools/kbench.py --workload $WL --iters 5 --probe-one $TX > $OUT/write_$WL.log 2>&1 || exit 13
 done
+# kernel stats of the 64-byte-frame kernel (C3) and the TX checksum kernel (C2 batch)
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -T -d $OUT/c3 -o run --output-format csv -- \
+  python3 $R/tools/kbench.py --workload c3_udp64 --iters 20 > $OUT/c3.log 2>&1 || exit 15
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -T -d $OUT/tx -o run --output-format csv -- \
+  python3 $R/tools/kbench.py --workload c2_tcp1500 --iters 20 --tx > $OUT/tx.log 2>&1 || exit 16
 # the TCP receive pipeline's kernels (1M segments, 16k connections)
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -T -d $OUT/tcp -o run --output-format csv -- \
   python3 $R/tools/tcpbench.py --nconns 16384 --iters 10 --cpu-seconds 0.5 > $OUT/tcp.json 2> $OUT/tcp.err || exit 14

@@ -53,6 +53,10 @@ def main():
     stats = os.path.join(src, "bench", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+    for sub in ("c3", "tx"):
+        st = os.path.join(src, sub, "run_kernel_stats.csv")
+        if os.path.exists(st):
+            shutil.copy(st, os.path.join(dst, f"{tag}_{sub}_kernel_stats.csv"))
     tstats = os.path.join(src, "tcp", "run_kernel_stats.csv")
     if os.path.exists(tstats):
         shutil.copy(tstats, os.path.join(dst, f"{tag}_tcp_kernel_stats.csv"))
@@ -71,8 +75,8 @@ def main():
         rx, probe, tx = kbench_info(os.path.join(src, f"fetch_{wl}.log"))
         fk = {k[0]: v for k, v in fc.items() if k[1] == "FETCH_SIZE"}
         wk = {k[0]: v for k, v in wc.items() if k[1] == "WRITE_SIZE"}
-        rxk = next(k for k in fk if "dk_rx_kernel" in k or "dk_rx_split_kernel" in k)
-        rxname = "dk_rx_split_kernel" if "split" in rxk else "dk_rx_kernel"
+        rxk = next(k for k in fk if "dk_rx_kernel" in k or "dk_rx_split_kernel" in k or "dk_rx_small_kernel" in k)
+        rxname = next(nm for nm in ("dk_rx_split_kernel", "dk_rx_small_kernel", "dk_rx_kernel") if nm in rxk)
         pk = next(k for k in fk if "read_probe" in k)
         factor = probe["bytes"] / (fk[pk] * 1024.0)
         rd = fk[rxk] * 1024.0 * factor
@@ -85,14 +89,15 @@ def main():
         rows.append([wl, rxname, f"{fk[rxk]:.0f}", f"{wk.get(rxk, 0.0):.0f}", f"{factor:.4f}", f"{rd:.0f}",
                      f"{wr:.0f}", algo, f"{(rd + wr) / algo:.3f}"])
         rows.append([wl, "read_probe", f"{fk[pk]:.0f}", f"{wk.get(pk, 0.0):.0f}", "", probe["bytes"], "", "", ""])
-        txk = next((k for k in fk if "dk_tx_kernel" in k), None)
+        txk = next((k for k in fk if "dk_tx_kernel" in k or "dk_tx_split_kernel" in k), None)
+        txname = "dk_tx_split_kernel" if txk and "split" in txk else "dk_tx_kernel"
         if tx and txk:
             trd, twr = fk[txk] * 1024.0 * factor, wk.get(txk, 0.0) * 1024.0
             traffic[wl + "_tx"] = {"hbm_bytes_per_launch": int(trd + twr), "hbm_read_bytes": int(trd),
                                    "hbm_write_bytes": int(twr), "fetch_calibration_factor": round(factor, 4),
                                    "algorithmic_bytes_per_launch": tx["algo_bytes"],
-                                   "source": f"profiles/{tag}_pmc.csv (dk_tx_kernel)"}
-            rows.append([wl, "dk_tx_kernel", f"{fk[txk]:.0f}", f"{wk.get(txk, 0.0):.0f}", f"{factor:.4f}",
+                                   "kernel": txname, "source": f"profiles/{tag}_pmc.csv ({txname})"}
+            rows.append([wl, txname, f"{fk[txk]:.0f}", f"{wk.get(txk, 0.0):.0f}", f"{factor:.4f}",
                          f"{trd:.0f}", f"{twr:.0f}", tx["algo_bytes"], f"{(trd + twr) / tx['algo_bytes']:.3f}"])
     with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as f:
         csv.writer(f).writerows(rows)
