@@ -125,6 +125,28 @@ TCP_FUNCTIONS = [
 ]
 
 # include/dk_diag.h (diagnostics, not the receive ABI)
+# include/dk_demi.h: delivered frames as demi_sgarray_t (host-side, no GPU work)
+class DemiSgaseg(ctypes.Structure):
+    _pack_ = 1
+    _fields_ = [("sgaseg_buf", c_void_p), ("sgaseg_len", c_uint32)]
+
+
+class SockaddrIn(ctypes.Structure):
+    _fields_ = [("sin_family", ctypes.c_uint16), ("sin_port", ctypes.c_uint16), ("sin_addr", c_uint32),
+                ("sin_zero", ctypes.c_uint8 * 8)]
+
+
+class DemiSgarray(ctypes.Structure):
+    _pack_ = 1
+    _fields_ = [("sga_buf", c_void_p), ("sga_numsegs", c_uint32), ("sga_segs", DemiSgaseg * 1),
+                ("sga_addr", SockaddrIn)]
+
+
+DEMI_FUNCTIONS = [
+    ("dk_rx_into_sgarrays", c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    POINTER(DemiSgarray), c_void_p, c_uint32, POINTER(c_uint32)]),
+]
+
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
     ("dk_diag_path_stats_enable", c_int, [c_void_p, c_int]),
@@ -149,10 +171,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
-    for name, restype, argtypes in FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS:
+    for name, restype, argtypes in FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS + DEMI_FUNCTIONS:
         fn = getattr(lib, name, None)
         if fn is None:
-            if (name, restype, argtypes) in DIAG_FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS and path != LIB_PATH:
+            if (name, restype, argtypes) in DIAG_FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DEMI_FUNCTIONS and path != LIB_PATH:
                 continue  # older tuning builds may predate a diagnostic
             raise ImportError(f"{path}: missing {name}")
         fn.restype = restype
