@@ -1270,11 +1270,16 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
     const uint32_t r0 = blockIdx.y * kReduceRows, r1 = min(rows, r0 + kReduceRows);
     uint64_t lo = 0, hi = 0;
     if (w < row_words) {
-#pragma unroll 8
-        for (uint32_t r = r0 + wv; r < r1; r += kWaves) {
-            const uint32_t x = scratch[(size_t)r * row_words + w];
-            lo += x & 0xFFFFu;
-            hi += x >> 16;
+        uint32_t x[kReduceRows / kWaves];  // all of this lane's loads in flight at once: one memory round trip
+#pragma unroll
+        for (uint32_t k = 0; k < kReduceRows / kWaves; k++) {
+            const uint32_t r = r0 + wv + k * kWaves;
+            x[k] = r < r1 ? scratch[(size_t)r * row_words + w] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kReduceRows / kWaves; k++) {
+            lo += x[k] & 0xFFFFu;
+            hi += x[k] >> 16;
         }
     }
     s_part[wv][0][lane] = lo;
