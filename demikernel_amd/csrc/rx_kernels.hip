@@ -685,7 +685,7 @@ constexpr int kStageK = DK_STAGE_K;
 
 // Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
 // results (stored, or handed back in rec for staging).
-template <bool kShift, bool kStage, class WL>
+template <bool kShift, bool kStage, class WL, bool kOpt = true>
 __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
                                           uint32_t& fid_out, Rec& rec) {
@@ -800,11 +800,13 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
         st_res(P.res.flow_id + i, fid);
         }
         }
-        if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
-        if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
-        if (P.res.tcp_win) P.res.tcp_win[i] = win;
+        if (kOpt) {  // optional outputs (kOpt = false: the caller asked for none; fewer live SGPRs)
+            if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
+            if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
+            if (P.res.tcp_win) P.res.tcp_win[i] = win;
+        }
     }
-    if (P.path_stats) {  // diagnostics (dk_diag.h): one atomic per path per wave
+    if (kOpt && P.path_stats) {  // diagnostics (dk_diag.h): one atomic per path per wave
         const uint32_t path = !fast ? 3u : resum ? 2u : big ? 1u : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) {
@@ -1080,7 +1082,7 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
     C.nblk = F.nblk;
 }
 
-template <bool kShift>
+template <bool kShift, bool kOpt>
 __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
     __shared__ SmallLds s_wave[kWaves];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
@@ -1131,7 +1133,7 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
         small_big_frames(F, lane, off, B, W, C);
         uint32_t v, fid;
         Rec rec;
-        rx_finish<kShift, false>(P, i, live, lane, W, off, len, C, v, fid, rec);
+        rx_finish<kShift, false, SmallLds, kOpt>(P, i, live, lane, W, off, len, C, v, fid, rec);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         // rotate the pipeline
         have = have1;
@@ -1575,7 +1577,7 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
     else if (family == dk::kFamilySmall)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true>, dk::kBlock,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kBlock,
                                                           dyn_lds_bytes);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1588,10 +1590,13 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
+    const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.path_stats;
     if (p.small && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+    else if (p.small && opt)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     else if (p.small)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     else if (p.split && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<false>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split)

@@ -155,6 +155,10 @@ def test_small_kernel_mixed(torch_cuda, monkeypatch):
     frames = [blob0[o:o + L].tobytes() for o, L in zip(off0, lens)]
     blob, off, lens2 = F.pack(frames, align=64, misalign=list(range(16)))
     check(blob, off, lens2, flows, ctx="small kernel, misaligned")
+    # no optional outputs requested: the instantiation without the TCP-field / path-stats stores
+    got = run_gpu(blob, off, lens2, flows, tcp_fields=False)
+    assert "tcp_seq" not in got
+    assert_same(got, run_oracle(blob, off, lens2, flows), "small kernel, no optional outputs")
     blob, off, lens2 = F.pack(frames, align=64)
     check(blob, off, lens2, flows, ctx="small kernel, aligned16 hint", aligned16=True)
 
