@@ -18,6 +18,8 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
+#include <cstring>
 
 #include "../../include/dk_tcp.h"
 
@@ -107,6 +109,51 @@ struct Store {
         len(k) = v.len;
     }
     __device__ __forceinline__ void copy(uint32_t to, uint32_t from) { set(to, start(from), view(from)); }
+    // VecDeque::remove(at) / insert(at) over the n live entries (insert drops what falls past the cap)
+    __device__ __forceinline__ void remove(uint32_t at, uint32_t n) {
+        for (uint32_t k = at; k + 1 < n; k++) copy(k, k + 1);
+    }
+    __device__ __forceinline__ void insert(uint32_t at, uint32_t n, uint32_t st, dk_tcp_view v) {
+        for (uint32_t k = min(n, DK_TCP_OOO_MAX - 1); k > at; k--) copy(k, k - 1);
+        set(at, st, v);
+    }
+};
+
+// The wave walk's store: entry k in lane k's registers (lanes >= DK_TCP_OOO_MAX unused). Reads are lane reads of a
+// wave-uniform index, remove and insert one cross-lane shift each instead of an entry-by-entry copy loop.
+struct RegStore {
+    uint32_t st, rf, of, ln, lane;
+    __device__ __forceinline__ uint32_t start(uint32_t k) const { return __builtin_amdgcn_readlane(st, k); }
+    __device__ __forceinline__ uint32_t len(uint32_t k) const { return __builtin_amdgcn_readlane(ln, k); }
+    __device__ __forceinline__ dk_tcp_view view(uint32_t k) const {
+        return dk_tcp_view{(uint32_t)__builtin_amdgcn_readlane(rf, k), (uint32_t)__builtin_amdgcn_readlane(of, k),
+                           (uint32_t)__builtin_amdgcn_readlane(ln, k)};
+    }
+    __device__ __forceinline__ void remove(uint32_t at, uint32_t) {
+        const uint32_t a = __shfl_down(st, 1, 64), b = __shfl_down(rf, 1, 64), c = __shfl_down(of, 1, 64),
+                       d = __shfl_down(ln, 1, 64);
+        if (lane >= at) {
+            st = a;
+            rf = b;
+            of = c;
+            ln = d;
+        }
+    }
+    __device__ __forceinline__ void insert(uint32_t at, uint32_t, uint32_t s, dk_tcp_view v) {
+        const uint32_t a = __shfl_up(st, 1, 64), b = __shfl_up(rf, 1, 64), c = __shfl_up(of, 1, 64),
+                       d = __shfl_up(ln, 1, 64);
+        if (lane > at) {
+            st = a;
+            rf = b;
+            of = c;
+            ln = d;
+        } else if (lane == at) {
+            st = s;
+            rf = v.ref;
+            of = v.off;
+            ln = v.len;
+        }
+    }
 };
 
 struct Out {  // the connection's delivery slots
@@ -119,13 +166,15 @@ struct Out {  // the connection's delivery slots
     }
 };
 
-__device__ __forceinline__ void ooo_remove(Store& s, Walk& w, uint32_t at) {
-    for (uint32_t k = at; k + 1 < w.nooo; k++) s.copy(k, k + 1);
+template <class S>
+__device__ __forceinline__ void ooo_remove(S& s, Walk& w, uint32_t at) {
+    s.remove(at, w.nooo);
     w.nooo--;
 }
 
 // store_out_of_order_segment (ctrlblk.rs:844-941) on the fixed arrays.
-__device__ __forceinline__ uint32_t ooo_store(Store& s, Walk& w, uint32_t new_start, uint32_t new_end,
+template <class S>
+__device__ __forceinline__ uint32_t ooo_store(S& s, Walk& w, uint32_t new_start, uint32_t new_end,
                                               dk_tcp_view buf) {
     uint32_t at = w.nooo;
     bool again = true;
@@ -160,14 +209,14 @@ __device__ __forceinline__ uint32_t ooo_store(Store& s, Walk& w, uint32_t new_st
     }
     // VecDeque::insert at `at`, then pop_back while longer than the cap
     if (at >= DK_TCP_OOO_MAX) return DK_TCP_STORED;
-    for (uint32_t k = min(w.nooo, DK_TCP_OOO_MAX - 1); k > at; k--) s.copy(k, k - 1);
-    s.set(at, new_start, buf);
+    s.insert(at, w.nooo, new_start, buf);
     w.nooo = min(w.nooo + 1, DK_TCP_OOO_MAX);
     return DK_TCP_STORED;
 }
 
 // receive_data (ctrlblk.rs:951-1001): true if a stored FIN is now in order.
-__device__ __forceinline__ bool receive_data(Store& s, Walk& w, dk_tcp_view buf, Out& o) {
+template <class S>
+__device__ __forceinline__ bool receive_data(S& s, Walk& w, dk_tcp_view buf, Out& o) {
     uint32_t recv_next = w.rn + buf.len;
     o.push(buf, w);
     while (w.nooo > 0 && s.start(0) == recv_next) {
@@ -180,7 +229,8 @@ __device__ __forceinline__ bool receive_data(Store& s, Walk& w, dk_tcp_view buf,
 }
 
 // process_packet (ctrlblk.rs:403-440) for segment g = {seq, ack, meta, payload} of frame i.
-__device__ __forceinline__ uint32_t process(Store& s, Walk& w, uint4 g, uint32_t i, Out& o, dk_tcp_view& view) {
+template <class S>
+__device__ __forceinline__ uint32_t process(S& s, Walk& w, uint4 g, uint32_t i, Out& o, dk_tcp_view& view) {
     const uint32_t flags = (g.z >> 16) & 0xFFu;
     bool syn = flags & 0x02u, fin = flags & 0x01u;
     const bool rst = flags & 0x04u, ack = flags & 0x10u;
@@ -323,6 +373,161 @@ __global__ __launch_bounds__(kWalkBlock) void dk_tcp_walk_kernel(Params P) {
     P.out.deliv_count[c] = o.n;
 }
 
+// The same walk with one wave per connection, for batches with many segments per connection (lanes = connections
+// leaves the chip idle when there are few). The connection's state stays wave-uniform. Each window of 64 segments is
+// classified in parallel (see the loop below): segments whose process_packet outcome needs no state machine are
+// taken at once — in-order data with no SYN/FIN/RST that ends inside the window and does not end exactly at the
+// out-of-order store's first entry or a pending FIN (NO_ACK / ACK_UNSENT with no state change, else DELIVERED = one
+// push and RCV.NXT += length, nothing drained from the store, or NO_DATA), entirely old segments (DUPLICATE) and segments past the window (OUT_OF_WINDOW). The window end
+// RCV.NXT + buffer - (RCV.NXT - reader_next) is reader_next + buffer for the whole batch, since nothing reads during
+// it. The first other segment goes through process() with every lane executing it redundantly (same inputs; the
+// out-of-order store is a RegStore, entry k in lane k), then the parallel check resumes at the next lane.
+constexpr uint32_t kWave = 64;
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x, uint32_t lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, kWave);
+        if (lane >= d) x = max(x, y);
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    dk_tcp_conn* t = P.conns + c;
+    const uint32_t k0 = P.range[c], cnt = P.range[c + 1] - k0;
+    const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c;
+    Walk w{t->state, t->receive_next, t->reader_next, t->buffer_size, t->send_next, t->fin_pending, t->fin_seq,
+           min(t->ooo_count, DK_TCP_OOO_MAX)};
+    RegStore s{0u, 0u, 0u, 0u, lane};
+    if (lane < w.nooo) {
+        const dk_tcp_view v = t->ooo[lane];
+        s = RegStore{t->ooo_start[lane], v.ref, v.off, v.len, lane};
+    }
+    Out o{P.out.deliv + d0, 0, cnt + DK_TCP_DELIV_EXTRA};
+    const uint32_t wend = w.reader + w.bufsz;
+    uint32_t inext = lane < cnt ? P.svals[k0 + lane] : 0u;
+    for (uint32_t base = 0; base < cnt; base += kWave) {
+        const uint32_t lim = min(cnt - base, kWave);
+        const bool have = lane < lim;
+        const uint32_t i = inext;
+        const uint4 g = have ? P.rec[i] : make_uint4(0u, 0u, 0u, 0u);
+        inext = base + kWave + lane < cnt ? P.svals[k0 + base + kWave + lane] : 0u;  // next window's indices
+        const uint32_t flags = (g.z >> 16) & 0xFFu, off = g.w & 0xFFFFu, len = g.w >> 16;
+        const bool simple = have && !(flags & 0x07u);
+        const bool ack_ok = (flags & 0x10u) && le(g.y, w.snd);
+        const uint8_t fast_action = !(flags & 0x10u) ? DK_TCP_NO_ACK
+                                    : !ack_ok        ? DK_TCP_ACK_UNSENT
+                                    : len > 0        ? DK_TCP_DELIVERED
+                                                     : DK_TCP_NO_DATA;
+        uint32_t lo = 0;
+        while (lo < lim) {
+            if (w.state != DK_TCP_ESTABLISHED) {  // queued behind the close
+                if (lane >= lo && have) {
+                    P.out.action[i] = DK_TCP_UNPROCESSED;
+                    P.out.view[i] = dk_tcp_view{i, off, len};
+                }
+                break;
+            }
+            // Parallel classification of lanes lo.. against RCV.NXT as it stands before each: accepted in-order
+            // segments move it to their end, so it is the running
+            // maximum of the candidates' ends (relative to RCV.NXT at lo; drops end before it or lie past the
+            // window). Entirely old (DUPLICATE) and past-the-window (OUT_OF_WINDOW) segments change nothing and
+            // are taken with the store in any state; the first other segment goes through process().
+            const bool mine = lane >= lo;
+            // With the store full, a segment that starts after every stored entry is inserted at the end and popped
+            // again (ctrlblk.rs:933-940): STORED with no change (a stuck hole makes every later segment one)
+            bool beyond = false;
+            if (w.nooo == DK_TCP_OOO_MAX && mine && simple) {
+                beyond = true;
+                for (uint32_t k = 0; k < DK_TCP_OOO_MAX; k++) beyond = beyond && lt(s.start(k) + (s.len(k) - 1), g.x);
+            }
+            uint32_t rel = 0;
+            if (mine && simple && !beyond && ack_ok && len > 0 && ge(g.x, w.rn) && !ge(g.x + (len - 1), wend))
+                rel = (g.x - w.rn) + len;
+            const uint32_t mx = wave_incl_max(rel, lane);
+            const uint32_t mx_prev = __shfl_up(mx, 1, kWave);
+            const uint32_t rn = w.rn + (lane > 0 ? mx_prev : 0u);
+            // receive_data drains the store (and completes a pending FIN) only when a push ends exactly at the
+            // store's first entry (at fin_seq): such a push is left to process()
+            const uint32_t front = w.nooo ? s.start(0) : 0u;
+            const uint32_t full = len + ((flags >> 1) & 1u) + (flags & 1u);  // SYN and FIN take a number each
+            const uint32_t seg_end = full ? g.x + (full - 1) : g.x;
+            bool ok;
+            uint8_t act;
+            uint32_t vlen = len;
+            if (g.x == rn) {
+                ok = simple && !beyond && (len == 0 || !ge(g.x + (len - 1), wend)) &&
+                     !(ack_ok && len > 0 &&
+                       ((w.nooo && g.x + len == front) || (w.fin_pending && g.x + len == w.fin_seq)));
+                act = fast_action;
+            } else if (lt(g.x, rn)) {
+                ok = lt(seg_end, rn);
+                act = DK_TCP_DUPLICATE;
+            } else if (ge(g.x, wend)) {
+                ok = true;
+                act = DK_TCP_OUT_OF_WINDOW;
+            } else {
+                ok = beyond;
+                act = fast_action == DK_TCP_DELIVERED ? (uint8_t)DK_TCP_STORED : fast_action;
+                if (len > 0 && ge(g.x + (len - 1), wend)) vlen = wend - g.x;  // check_segment_in_window's end trim
+            }
+            ok = ok && mine && have;
+            const uint64_t bad = __ballot(mine && !ok);
+            uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
+            f = min(f, lim);
+            const bool taken = mine && lane < f;
+            const bool pushed = taken && act == DK_TCP_DELIVERED;
+            const uint64_t pm = __ballot(pushed);
+            const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+            if (taken) {
+                P.out.action[i] = act;
+                P.out.view[i] = dk_tcp_view{i, off, vlen};
+                if (pushed && o.n + before < o.cap) o.d[o.n + before] = dk_tcp_view{i, off, len};
+            }
+            o.n += (uint32_t)__builtin_popcountll(pm);
+            if (f > lo) w.rn += __shfl(mx, f - 1, kWave);
+            if (f >= lim) break;
+            const uint4 gf = make_uint4(__shfl(g.x, f, kWave), __shfl(g.y, f, kWave), __shfl(g.z, f, kWave),
+                                        __shfl(g.w, f, kWave));
+            const uint32_t i_f = __shfl(i, f, kWave);
+            dk_tcp_view v;
+            const uint32_t a_f = process(s, w, gf, i_f, o, v);
+            if (lane == 0) {
+                P.out.action[i_f] = (uint8_t)a_f;
+                P.out.view[i_f] = v;
+            }
+            lo = f + 1;
+        }
+    }
+    if (lane == 0) {
+        P.out.deliv_start[c] = d0;
+        t->state = w.state;
+        t->receive_next = w.rn;
+        t->fin_pending = w.fin_pending;
+        t->fin_seq = w.fin_seq;
+        t->ooo_count = w.nooo;
+        P.out.deliv_count[c] = o.n;
+    }
+    if (lane < DK_TCP_OOO_MAX) {
+        const bool live = lane < w.nooo;
+        t->ooo_start[lane] = live ? s.st : 0u;
+        t->ooo[lane] = live ? dk_tcp_view{s.rf, s.of, s.ln} : dk_tcp_view{0, 0, 0};
+    }
+}
+
+// Which walk runs: DK_TCP_WALK=lane|wave forces one; otherwise the wave walk when connections average at least
+// kWaveWalkMinSegs segments in the batch.
+constexpr uint32_t kWaveWalkMinSegs = 32;
+bool use_wave_walk(uint32_t n, uint32_t nconns) {
+    if (nconns > (1u << 24)) return false;  // grid of nconns waves
+    const char* e = getenv("DK_TCP_WALK");
+    if (e && !strcmp(e, "lane")) return false;
+    if (e && !strcmp(e, "wave")) return true;
+    return (uint64_t)n >= (uint64_t)kWaveWalkMinSegs * nconns;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -430,7 +635,12 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
             return EINVAL;
     }
     if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
-    if (nconns) hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
+    if (nconns) {
+        if (use_wave_walk(n, nconns))
+            hipLaunchKernelGGL(dk_tcp_wave_walk_kernel, dim3(nconns), dim3(kWave), 0, s, P);
+        else
+            hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
+    }
     return hipGetLastError() == hipSuccess ? 0 : EINVAL;
 }
 

@@ -17,14 +17,24 @@ from oracle.oracle import OraclePeer
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def tcp():
+@pytest.fixture(scope="module", params=["lane", "wave"])
+def tcp(request):
+    """Every test runs through both walks: lanes = connections, and one wave per connection with the parallel
+    in-order check (DK_TCP_WALK forces the choice the engine otherwise makes from segments per connection)."""
+    import os
+
     import torch
 
     assert torch.cuda.is_available()
+    old = os.environ.get("DK_TCP_WALK")
+    os.environ["DK_TCP_WALK"] = request.param
     r = TcpReceiver(0)
     yield r
     r.close()
+    if old is None:
+        os.environ.pop("DK_TCP_WALK", None)
+    else:
+        os.environ["DK_TCP_WALK"] = old
 
 
 def rx_device(rx: dict):
@@ -85,6 +95,17 @@ SCENARIOS = {
                                        (3, 1, 1, S.ACK, 10, 25), (7, 1, 1, S.ACK, 10), (3, 1, 1, S.FIN | S.ACK, 0)]),
     "closed": (S.conns(2, rn=1, state=N.DK_TCP_CLOSED), [(0, 1, 1, S.ACK, 10), (1, 1, 1, S.ACK, 0)]),
     "empty_batch": (S.conns(3, rn=1), []),
+    # store full, then segments after every entry (inserted and popped: STORED with no change), one without ACK, one
+    # trimmed at the window end, a retransmission inside the store, and the hole filled (the store drains)
+    "full_store_beyond": (S.conns(rn=1, bufsz=6000), [(0, 1001 + 200 * k, 1, S.ACK, 100) for k in range(16)] +
+                          [(0, 5001, 1, S.ACK, 100), (0, 5201, 1, S.PSH, 100), (0, 5950, 1, S.ACK, 100),
+                           (0, 5600, 9, S.ACK, 10), (0, 1201, 1, S.ACK, 50), (0, 1, 1, S.ACK, 1000),
+                           (0, 5401, 1, S.ACK, 100)]),
+    # long in-order runs (64-segment windows of the wave walk) with drops between and a stored segment whose front
+    # an in-order push does not reach exactly
+    "long_runs": (S.conns(rn=1), [(0, 1 + 10 * k, 1, S.ACK, 10) for k in range(150)] +
+                  [(0, 3001, 1, S.ACK, 10), (0, 1, 1, S.ACK, 10)] +
+                  [(0, 1501 + 10 * k, 1, S.ACK, 10) for k in range(149)] + [(0, 2991, 1, S.ACK, 20)]),
 }
 
 
@@ -117,7 +138,8 @@ def test_carried_out_of_order_store(tcp):
 
 
 @pytest.mark.parametrize("n,nconns,batches", [(1, 1, 1), (3000, 1, 2), (20000, 7, 2), (60000, 1000, 3),
-                                              (200000, 20000, 2), (100000, 300, 1)])
+                                              (200000, 20000, 2), (100000, 300, 1), (50000, 3, 1),
+                                              (262144, 64, 1)])
 def test_streams_through_rx(tcp, n, nconns, batches):
     """Frames -> dk_rx (verdicts, flow ids, seq/ack) -> dk_tcp on the GPU, against the oracle chain on the same
     frames, batch after batch with the connection table carried."""
