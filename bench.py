@@ -262,7 +262,10 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
     return {"mseg_s": round(nseg / t / 1e6, 1), "ms_avg": round(t * 1e3, 4), "segments": nseg, "connections": nconns,
             "delivered_frac": round(float(hist[1]) / nseg, 3),
             "cpu_baseline": {"mseg_s": round(nseg / tc / 1e6, 2), "cores": 1, "kind": "port", "reps": reps},
-            "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (store in LDS)"}
+            "walk": "wave" if nseg >= 32 * nconns else "lane",
+            "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (lanes = connections, "
+                        "store in LDS; one wave per connection with a parallel 64-segment check at >= 32 "
+                        "segments per connection)"}
 
 
 def rx_kernel_name(frame_bytes, n):
@@ -467,6 +470,8 @@ def main():
         out["tx_checksum"] = tx_rate(eng, batch, frame_bytes, stream)
         out["tx_checksum"]["traffic"] = load_traffic_profile(name + "_tx")
         out["tcp_rx"] = tcp_rate(stream)
+        # few connections with many segments each (the wave-per-connection walk)
+        out["tcp_rx_64conns"] = tcp_rate(stream, 1 << 20, 64, cpu_seconds=1.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

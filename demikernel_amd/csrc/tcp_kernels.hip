@@ -12,6 +12,8 @@
 //      state machine in order, reading each segment's record through the sorted frame index (pipelined: indices two
 //      batches of kBatch ahead, records one batch ahead). The walk is the only sequential part
 //      (latency-bound, lanes = connections); everything else is a pass over the batch.
+//   4'. dk_tcp_wave_walk_kernel instead, at >= kWaveWalkMinSegs segments per connection: one wave per connection,
+//      64 segments classified in parallel per step, the state machine only for the segments that need it.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -407,13 +409,18 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     }
     Out o{P.out.deliv + d0, 0, cnt + DK_TCP_DELIV_EXTRA};
     const uint32_t wend = w.reader + w.bufsz;
-    uint32_t inext = lane < cnt ? P.svals[k0 + lane] : 0u;
+    // Software pipeline over windows: frame indices two windows ahead, records one window ahead.
+    uint32_t icur = lane < cnt ? P.svals[k0 + lane] : 0u;
+    uint4 gnext = lane < cnt ? P.rec[icur] : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t inext = kWave + lane < cnt ? P.svals[k0 + kWave + lane] : 0u;
     for (uint32_t base = 0; base < cnt; base += kWave) {
         const uint32_t lim = min(cnt - base, kWave);
         const bool have = lane < lim;
-        const uint32_t i = inext;
-        const uint4 g = have ? P.rec[i] : make_uint4(0u, 0u, 0u, 0u);
-        inext = base + kWave + lane < cnt ? P.svals[k0 + base + kWave + lane] : 0u;  // next window's indices
+        const uint32_t i = icur;
+        const uint4 g = gnext;
+        icur = inext;
+        gnext = base + kWave + lane < cnt ? P.rec[icur] : make_uint4(0u, 0u, 0u, 0u);
+        inext = base + 2 * kWave + lane < cnt ? P.svals[k0 + base + 2 * kWave + lane] : 0u;
         const uint32_t flags = (g.z >> 16) & 0xFFu, off = g.w & 0xFFFFu, len = g.w >> 16;
         const bool simple = have && !(flags & 0x07u);
         const bool ack_ok = (flags & 0x10u) && le(g.y, w.snd);
