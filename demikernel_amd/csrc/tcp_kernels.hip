@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/warp/warp_scan.hpp>
 
 #include <algorithm>
 #include <cerrno>
@@ -386,16 +387,10 @@ __global__ __launch_bounds__(kWalkBlock) void dk_tcp_walk_kernel(Params P) {
 // out-of-order store is a RegStore, entry k in lane k), then the parallel check resumes at the next lane.
 constexpr uint32_t kWave = 64;
 
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x, uint32_t lane) {
-#pragma unroll
-    for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, kWave);
-        if (lane >= d) x = max(x, y);
-    }
-    return x;
-}
+using WaveScan = rocprim::warp_scan<uint32_t, kWave>;
 
 __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
+    __shared__ WaveScan::storage_type scan_tmp;
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     dk_tcp_conn* t = P.conns + c;
     const uint32_t k0 = P.range[c], cnt = P.range[c + 1] - k0;
@@ -453,9 +448,10 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
             uint32_t rel = 0;
             if (mine && simple && !beyond && ack_ok && len > 0 && ge(g.x, w.rn) && !ge(g.x + (len - 1), wend))
                 rel = (g.x - w.rn) + len;
-            const uint32_t mx = wave_incl_max(rel, lane);
-            const uint32_t mx_prev = __shfl_up(mx, 1, kWave);
-            const uint32_t rn = w.rn + (lane > 0 ? mx_prev : 0u);
+            uint32_t mx_prev;  // max over the lanes before this one (DPP scan)
+            WaveScan().exclusive_scan(rel, mx_prev, 0u, scan_tmp, rocprim::maximum<uint32_t>());
+            const uint32_t mx = max(mx_prev, rel);
+            const uint32_t rn = w.rn + mx_prev;
             // receive_data drains the store (and completes a pending FIN) only when a push ends exactly at the
             // store's first entry (at fin_seq): such a push is left to process()
             const uint32_t front = w.nooo ? s.start(0) : 0u;
@@ -494,11 +490,11 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
                 if (pushed && o.n + before < o.cap) o.d[o.n + before] = dk_tcp_view{i, off, len};
             }
             o.n += (uint32_t)__builtin_popcountll(pm);
-            if (f > lo) w.rn += __shfl(mx, f - 1, kWave);
+            if (f > lo) w.rn += (uint32_t)__builtin_amdgcn_readlane(mx, f - 1);
             if (f >= lim) break;
-            const uint4 gf = make_uint4(__shfl(g.x, f, kWave), __shfl(g.y, f, kWave), __shfl(g.z, f, kWave),
-                                        __shfl(g.w, f, kWave));
-            const uint32_t i_f = __shfl(i, f, kWave);
+            const uint4 gf = make_uint4(__builtin_amdgcn_readlane(g.x, f), __builtin_amdgcn_readlane(g.y, f),
+                                        __builtin_amdgcn_readlane(g.z, f), __builtin_amdgcn_readlane(g.w, f));
+            const uint32_t i_f = __builtin_amdgcn_readlane(i, f);
             dk_tcp_view v;
             const uint32_t a_f = process(s, w, gf, i_f, o, v);
             if (lane == 0) {
