@@ -262,9 +262,9 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
     return {"mseg_s": round(nseg / t / 1e6, 1), "ms_avg": round(t * 1e3, 4), "segments": nseg, "connections": nconns,
             "delivered_frac": round(float(hist[1]) / nseg, 3),
             "cpu_baseline": {"mseg_s": round(nseg / tc / 1e6, 2), "cores": 1, "kind": "port", "reps": reps},
-            "walk": "wave" if nseg >= 32 * nconns else "lane",
+            "walk": "wave" if nseg >= 8 * nconns else "lane",
             "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (lanes = connections, "
-                        "store in LDS; one wave per connection with a parallel 64-segment check at >= 32 "
+                        "store in LDS; one wave per connection with a parallel 64-segment check at >= 8 "
                         "segments per connection)"}
 
 

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
 
 // Which walk runs: DK_TCP_WALK=lane|wave forces one; otherwise the wave walk when connections average at least
 // kWaveWalkMinSegs segments in the batch.
-constexpr uint32_t kWaveWalkMinSegs = 32;
+constexpr uint32_t kWaveWalkMinSegs = 8;
 bool use_wave_walk(uint32_t n, uint32_t nconns) {
     if (nconns > (1u << 24)) return false;  // grid of nconns waves
     const char* e = getenv("DK_TCP_WALK");

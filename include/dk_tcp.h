@@ -20,7 +20,7 @@
  *
  * Conventions as dk_rx.h: 0 or a positive errno; device pointers; asynchronous on the caller's stream.
  * The engine picks its per-connection walk from the batch (one lane per connection, or one wave per connection at
- * >= 32 segments per connection); the environment variable DK_TCP_WALK=lane|wave forces one. Results are identical.
+ * >= 8 segments per connection); the environment variable DK_TCP_WALK=lane|wave forces one. Results are identical.
  */
 #ifndef DK_TCP_H
 #define DK_TCP_H
