@@ -395,8 +395,11 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     dk_tcp_conn* t = P.conns + c;
     const uint32_t k0 = P.range[c], cnt = P.range[c + 1] - k0;
     const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c;
-    Walk w{t->state, t->receive_next, t->reader_next, t->buffer_size, t->send_next, t->fin_pending, t->fin_seq,
-           min(t->ooo_count, DK_TCP_OOO_MAX)};
+    // the connection's scalar state, wave-uniform: held in scalar registers
+#define DK_U(x) (uint32_t) __builtin_amdgcn_readfirstlane((int)(x))
+    Walk w{DK_U(t->state), DK_U(t->receive_next), DK_U(t->reader_next), DK_U(t->buffer_size), DK_U(t->send_next),
+           DK_U(t->fin_pending), DK_U(t->fin_seq), DK_U(min(t->ooo_count, DK_TCP_OOO_MAX))};
+#undef DK_U
     RegStore s{0u, 0u, 0u, 0u, lane};
     if (lane < w.nooo) {
         const dk_tcp_view v = t->ooo[lane];
