@@ -5,8 +5,11 @@
 
 A step = one dk_rx_process pass over one HBM-resident batch of the workload (default: BASELINE config 2,
 1,048,576 x 1500 B IPv4/TCP frames over 1,024 flows, 1 % corrupted tail), plus, for N > 1, the RCCL all-reduce of the
-per-flow packet counts (the only collective on this path). Weak scaling: every rank owns one batch (its packet shard).
+per-flow packet counts (dk_rx_flow_counts_allreduce over a dk_comm.h communicator: the only collective on this path,
+on a side stream, overlapping the next step's kernel). Weak scaling: every rank owns one batch (its packet shard).
 `value` = sum of frame bytes processed by all ranks / max-over-ranks time.  Rank 0 prints one JSON line.
+At N = 1 the line also carries the other BASELINE configs as extras (C3 64 B UDP, C4 IMIX shard, C5 10k-flow shard
+kernel-only and end to end from pinned host memory, C1-shaped CPU baseline), each with its own roofline fields.
 """
 from __future__ import annotations
 
@@ -28,6 +31,8 @@ RESULT_BYTES = 24      # meta, src_ip, dst_ip, ports, payload, flow_id (u32 each
 
 WORKLOADS = {
     # name: (description, frames, ip_len spec, flow kind, nflows)
+    "c1_tcp1078": ("tcp-echo-shaped: 1078 B IPv4/TCP (1 KiB payload) on one 4-tuple to port 12345", 1 << 17, 1064,
+                   "tcp", 1),
     "c2_tcp1500": ("1M x 1500B IPv4/TCP, 1024 flows, device-resident", 1 << 20, 1486, "tcp", 1024),
     "c3_udp64": ("1M x 64B IPv4/UDP (min-size), device-resident, 8 rotating batches", 1 << 20, 50, "udp", 1024),
     "c4_imix": ("IMIX 40/576/1500 at 7:4:1, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, "imix", "tcp", 1024),
@@ -62,105 +67,111 @@ def make_batch(eng, name, rank, seed_base, world=1):
     return batch, flows, tr
 
 
-def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, counts_allreduce=False):
+def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
     """Run warmup + timed steps. A step = the receive pass over one batch (+ for N > 1 the all-reduce of this step's
-    per-flow counts). For N > 1 the counters are double-buffered and the all-reduce is issued asynchronously (RCCL runs
-    on its own stream), so step k's reduction overlaps step k+1's kernel.
-    Returns (wall seconds for `steps`, per-launch kernel seconds, per-step collective seconds measured unoverlapped)."""
+    counters over RCCL: ShardedReceiver, double-buffered counters, the collective on a side stream so step k's
+    reduction overlaps step k+1's kernel). Returns (wall seconds for `steps`, per-launch kernel seconds from HIP
+    events on the launch stream around the timed region, per-step collective seconds measured unoverlapped)."""
     import torch
 
-    gloo = dist is not None and dist.get_backend() == "gloo"
-    bufs = [res.t["flow_counts"], torch.zeros_like(res.t["flow_counts"])] if counts_allreduce else []
-    pending = [None, None]
+    from demikernel_amd.shard import ShardedReceiver
 
-    def reduce(buf, async_op):
-        if gloo:  # rehearsal only: gloo reduces a host copy, synchronously
-            h = buf.cpu()
-            dist.all_reduce(h)
-            buf.copy_(h)
-            return None
-        return dist.all_reduce(buf, async_op=async_op)
-
-    def step(k):
-        b = batches[k % len(batches)]
-        if counts_allreduce:
-            slot = k % 2
-            if pending[slot] is not None:
-                pending[slot].wait()  # stream dependency: the buffer's previous all-reduce has finished
-                pending[slot] = None
-            bufs[slot].zero_()
-            res.t["flow_counts"] = bufs[slot]
-        eng.receive_batch(b, res, stream=stream)
-        if counts_allreduce:
-            pending[k % 2] = reduce(bufs[k % 2], True)
-
-    def drain():
-        for slot in (0, 1):
-            if pending[slot] is not None:
-                pending[slot].wait()
-                pending[slot] = None
-
+    sr = ShardedReceiver(eng, res, comm, stream)
     for k in range(warmup):
-        step(k)
-    drain()
+        sr.step(batches[k % len(batches)])
+    sr.drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     # HIP events bracket the timed region only (an event pair around every launch adds a marker + cache writeback per
-    # step and perturbs the kernel it measures): per-launch time = region / steps, i.e. dk_rx_kernel plus the small
-    # dk_flow_reduce_kernel and launch gaps (rocprofv3 kernel stats in profiles/ split the two kernels).
+    # step and perturbs the kernel it measures): per-launch time = region / steps, on the stream the kernels run on.
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
     for k in range(steps):
-        step(k)
+        sr.step(batches[k % len(batches)])
     e1.record(stream)
-    drain()
+    sr.drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern = [e0.elapsed_time(e1) / 1e3 / steps]
+    kern = e0.elapsed_time(e1) / 1e3 / steps
     coll = []
-    if counts_allreduce:  # the collective alone, unoverlapped, for the report
+    if comm is not None:  # the collective alone, unoverlapped, for the report
+        r = sr.res[0]
         for _ in range(5):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            reduce(bufs[0], False)
-            e1.record(stream)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record(sr.side)
+            eng.counts_allreduce(r, comm.handle, stream=sr.side)
+            c1.record(sr.side)
             torch.cuda.synchronize()
-            coll.append(e0.elapsed_time(e1) / 1e3)
+            coll.append(c0.elapsed_time(c1) / 1e3)
     return wall, kern, coll
 
 
-def cpu_baseline(batch, flows, sample_frames, min_seconds, threads=1):
-    """Oracle (CPU restatement of the reference) on a bounded sample of the same workload, host cores."""
-    from demikernel_amd import ipv4, synth
-    from oracle.oracle import OraclePeer
+def cpu_info():
+    """What the CPU baseline ran on: model name, CPUs this process may use (affinity), cgroup CPU quota."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "cpus_usable": len(os.sched_getaffinity(0)), "cpu_logical": os.cpu_count(),
+            "cgroup_cpu_quota": quota}
 
+
+def host_sample(batch, sample_frames):
+    """The first `sample_frames` frames of a device batch, copied to host (blob, off, lens)."""
     n = min(sample_frames, batch.n)
     off = batch.off[:n].cpu().numpy().view(np.uint32).copy()
     lens = batch.len[:n].cpu().numpy().view(np.uint16).copy()
     end = int(off[-1]) + int(lens[-1])
-    blob = batch.blob[:end].cpu().numpy()
+    return batch.blob[:end].cpu().numpy(), off, lens
+
+
+def cpu_rate(blob, off, lens, flows, min_seconds, threads=1):
+    """Oracle (CPU restatement of the reference) over host arrays, repeated for >= min_seconds; median rates."""
+    from demikernel_amd import ipv4, synth
+    from oracle.oracle import OraclePeer
+
     peer = OraclePeer(ipv4(synth.BOB_IPV4))
     peer.set_flows(flows)
     nbytes = int(lens.astype(np.int64).sum())
-    rates, used, t_all = [], 1, time.perf_counter()
-    while time.perf_counter() - t_all < min_seconds or len(rates) < 3:
+    times, used, t_all = [], 1, time.perf_counter()
+    while time.perf_counter() - t_all < min_seconds or len(times) < 3:
         t = time.perf_counter()
         if threads == 1:
             peer.process(blob, off, lens)
         else:
             _, used = peer.process_mt(blob, off, lens, threads)
-        rates.append(nbytes / (time.perf_counter() - t) / 1e9)
-    return float(np.median(rates)), used, n, nbytes, len(rates)
+        times.append(time.perf_counter() - t)
+    t = float(np.median(times))
+    return {"gbps": nbytes / t / 1e9, "mpkt_s": len(off) / t / 1e6, "cores": used, "frames": len(off),
+            "bytes": nbytes, "reps": len(times)}
 
 
-def host_path_rate(eng, batch, flows, nframes, reps=3):
-    """End-to-end GB/s of frame bytes for a pinned host batch through dk_rx_process_host (PCIe-inclusive)."""
+def cpu_baseline(batch, flows, sample_frames, min_seconds, threads=1):
+    """Oracle on a bounded sample of the same workload, host cores (kept for tools that import it)."""
+    blob, off, lens = host_sample(batch, sample_frames)
+    r = cpu_rate(blob, off, lens, flows, min_seconds, threads)
+    return r["gbps"], r["cores"], r["frames"], r["bytes"], r["reps"]
+
+
+def host_path_rate(eng, batch, flows, nframes, reps=5):
+    """End-to-end GB/s of frame bytes for a pinned host batch through dk_rx_process_host (PCIe-inclusive): pinned
+    host frames + descriptors -> HBM -> kernel -> results back to pinned host arrays. Median of `reps`."""
     import torch
 
     from demikernel_amd import RxResults
@@ -180,11 +191,12 @@ def host_path_rate(eng, batch, flows, nframes, reps=3):
         t = time.perf_counter()
         eng.receive_batch_host(pinned.numpy(), off_p.numpy(), len_p.numpy(), res)
         rates.append(nbytes / (time.perf_counter() - t) / 1e9)
-    return {"gbps": round(max(rates), 2), "frames": n, "bytes": nbytes, "reps": reps,
+    return {"gbps": round(float(np.median(rates)), 2), "gbps_max": round(max(rates), 2), "frames": n, "bytes": nbytes,
+            "reps": reps, "stat": "median",
             "pipeline": "3 streams, 65536-frame chunks, pinned host memory (dk_rx_process_host)"}
 
 
-def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=3):
+def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=5):
     """end-to-end GB/s of frame bytes for frames sitting in a TPACKET_V3 receive ring (the
     layout AF_PACKET fills; page-locked with hipHostRegister): block scan on the host, H2D of the blocks' byte ranges,
     kernel, D2H of the results (dk_rx_process_tpacket3). PCIe-inclusive; reported beside `value`, never as `value`."""
@@ -209,8 +221,9 @@ def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=3):
             assert nf == n and nb == used
     finally:
         r.close()
-    return {"gbps": round(max(rates), 2), "frames": n, "bytes": nbytes, "blocks": used, "block_size": block_size,
-            "reps": reps, "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
+    return {"gbps": round(float(np.median(rates)), 2), "gbps_max": round(max(rates), 2), "frames": n, "bytes": nbytes,
+            "blocks": used, "block_size": block_size, "reps": reps, "stat": "median",
+            "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
 
 
 def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
@@ -342,25 +355,51 @@ def load_traffic_profile(workload):
         return None
 
 
+def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True):
+    """Device-resident kernel rate of another BASELINE config on this GPU (its own engine and batches; `rotate`
+    distinct batches when one would sit in the 256 MB MALL), with its roofline fields."""
+    from demikernel_amd import Config, RxEngine, synth
+
+    eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
+    made = [make_batch(eng, name, 0, synth.SEED + 1000 * k) for k in range(rotate)]
+    batches = [m[0] for m in made]
+    _, flows, tr = made[0]
+    n = batches[0].n
+    res = eng.results(n, dst_ip=dst_ip)
+    wall, kern, _ = time_kernel(eng, batches, res, steps, warmup, stream)
+    fb = int(tr.frame_len.astype(np.int64).sum())
+    rb = RESULT_BYTES if dst_ip else RESULT_BYTES - 4
+    algo = fb + n * (DESC_BYTES + rb)
+    out = {"workload": WORKLOADS[name][0], "frames": n, "flows": len(flows), "batches_rotated": rotate,
+           "gbps": round(fb * steps / wall / 1e9, 2), "mpkt_s": round(n * steps / wall / 1e6, 1),
+           "kernel_ms_avg": round(kern * 1e3, 4), "kernel": rx_kernel_name(int(batches[0].frames_bytes), n),
+           "result_bytes_per_frame": rb,
+           "roofline": {"bound": "hbm", "achieved": round(algo / kern / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo,
+                        "traffic": load_traffic_profile(name)}}
+    return out, eng, batches[0], flows
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2_tcp1500", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c2_tcp1500", choices=sorted(k for k in WORKLOADS if k != "c1_tcp1078"))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 17)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-frames", type=int, default=1 << 19)
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="collective backend for N > 1 (nccl = RCCL on ROCm; gloo only to rehearse on one GPU)")
+    ap.add_argument("--backend", default="gloo", choices=["nccl", "gloo"],
+                    help="N > 1: process group for the barrier and the max-over-ranks timing only (the counters are "
+                         "reduced by dk_rx_flow_counts_allreduce over RCCL either way)")
     args = ap.parse_args()
 
     import torch
 
     rank, local_rank, world = dist_env()
-    dist = None
+    dist, comm = None, None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
@@ -374,7 +413,11 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
-    from demikernel_amd import Config, RxEngine, synth
+    from demikernel_amd import Comm, Config, RxEngine, synth
+    from demikernel_amd.shard import broadcast_comm_id
+
+    if world > 1:  # the receive path's own RCCL communicator (include/dk_comm.h), bootstrapped over the process group
+        comm = Comm.init_rank(world, broadcast_comm_id(dist, Comm.unique_id), rank, dev)
 
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -386,8 +429,7 @@ def main():
     res = eng.results(batch.n)
     frame_bytes = int(tr.frame_len.astype(np.int64).sum())
 
-    wall, kern, coll = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist,
-                                   counts_allreduce=world > 1)
+    wall, kern_avg, coll = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist, comm)
     if dist is not None:
         cdev = "cuda" if args.backend == "nccl" else "cpu"
         t = torch.tensor([wall], dtype=torch.float64, device=cdev)
@@ -400,7 +442,6 @@ def main():
         total_bytes, total_frames = frame_bytes, batch.n
 
     value = total_bytes * args.steps / wall / 1e9
-    kern_avg = float(np.mean(kern))
     algo = frame_bytes + batch.n * (DESC_BYTES + RESULT_BYTES)
     achieved = algo / kern_avg / 1e9
     traffic = load_traffic_profile(name)
@@ -420,13 +461,14 @@ def main():
         "data": "synthetic (seeded frames generated on device; 1% corrupted tail)",
         "config": {"workload": WORKLOADS[name][0], "name": name, "frames_per_gpu": batch.n,
                    "global_frames": total_frames, "parallelism": f"packet-shard x{world}",
-                   "collective": ("all_reduce(flow_counts, u64) per step, async, double-buffered (overlaps the next "
-                                  "step's kernel)") if world > 1 else "none"},
+                   "collective": ("dk_rx_flow_counts_allreduce (RCCL all-reduce of u64 flow + verdict counters) per "
+                                  "step on a side stream, double-buffered (overlaps the next step's kernel)")
+                   if world > 1 else "none"},
         "mpkt_s": round(total_frames * args.steps / wall / 1e6, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms_avg": round(kern_avg * 1e3, 4),
-                     "algorithmic_bytes_per_launch": algo, "kernel": rx_kernel_name(frame_bytes, batch.n)},
+                     "algorithmic_bytes_per_launch": algo, "kernel": rx_kernel_name(int(batch.frames_bytes), batch.n)},
     }
     if not args.no_extras:
         ceil_gbs, ceil_cfg = read_ceiling(batch, stream)
@@ -434,36 +476,56 @@ def main():
                                                     "frac": round(achieved / ceil_gbs, 4)}
     if coll:
         out["collective_ms_avg"] = round(float(np.mean(coll)) * 1e3, 4)
+    host = cpu_info()
     if rank == 0 and world == 1 and not args.no_cpu:
-        gbs, used, n_s, nb_s, reps = cpu_baseline(batch, flows, args.cpu_sample, args.cpu_seconds)
-        out["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s", "cores": used, "kind": "port",
-                               "sample": f"first {n_s} frames of the same batch ({nb_s / 1e6:.0f} MB), "
-                                         f"{reps} reps over >= {args.cpu_seconds:.0f} s, median; oracle/dk_oracle.cpp "
-                                         f"(C++ restatement of the Rust path, clang -O3, 1 thread as the reference's "
-                                         f"single-threaded LibOS)"}
+        blob_s, off_s, lens_s = host_sample(batch, args.cpu_sample)
+        r = cpu_rate(blob_s, off_s, lens_s, flows, args.cpu_seconds)
+        out["cpu_baseline"] = {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": 1, "kind": "port",
+                               "mpkt_s": round(r["mpkt_s"], 2),
+                               "sample": f"first {r['frames']} frames of the same batch ({r['bytes'] / 1e6:.0f} MB), "
+                                         f"{r['reps']} reps over >= {args.cpu_seconds:.0f} s, median; "
+                                         f"oracle/dk_oracle.cpp (C++ restatement of the Rust path, clang -O3, 1 thread "
+                                         f"as the reference's single-threaded LibOS)", **host}
         if not args.no_extras:
-            # the same restatement on all host cores of this box's share (OpenMP packet shards), as a scaled figure
-            threads = min(os.cpu_count() or 1, 16)
-            gbs_mt, used_mt, _, _, _ = cpu_baseline(batch, flows, args.cpu_sample, max(args.cpu_seconds / 2, 1.0),
-                                                    threads=threads)
-            out["cpu_baseline_all_cores"] = {"value": round(gbs_mt, 3), "unit": "GB/s", "cores": used_mt}
+            # the reference's own config 1 shape (tcp-echo: 1 KiB payloads on one 4-tuple to port 12345,
+            # tools/ci/job/linux.py:145, examples/tcp-echo/client.rs:82) and config 3 (64 B UDP), 1 core each
+            e1 = RxEngine(Config(synth.BOB_IPV4), device=dev)
+            b1, f1, _ = make_batch(e1, "c1_tcp1078", 0, synth.SEED)
+            r1 = cpu_rate(*host_sample(b1, b1.n), f1, 3.0)
+            out["cpu_baseline"]["c1"] = {"gbps": round(r1["gbps"], 3), "mpkt_s": round(r1["mpkt_s"], 2), "cores": 1,
+                                         "sample": f"{r1['frames']} x 1078 B TCP frames, one Active 4-tuple, "
+                                                   f"{r1['reps']} reps, median"}
+            del e1, b1
+            e3 = RxEngine(Config(synth.BOB_IPV4), device=dev)
+            b3, f3, _ = make_batch(e3, "c3_udp64", 0, synth.SEED)
+            r3 = cpu_rate(*host_sample(b3, 1 << 20), f3, 3.0)
+            out["cpu_baseline"]["c3"] = {"gbps": round(r3["gbps"], 3), "mpkt_s": round(r3["mpkt_s"], 2), "cores": 1,
+                                         "sample": f"{r3['frames']} x 64 B UDP frames (the C3 batch), {r3['reps']} "
+                                                   f"reps, median"}
+            del e3, b3
+            # the same restatement on every CPU this process may use (OpenMP packet shards), as a scaled figure: the
+            # CPUs in its affinity mask, capped by its cgroup CPU quota (more threads than the quota only time-slice)
+            threads = host["cpus_usable"]
+            if host["cgroup_cpu_quota"]:
+                threads = max(1, min(threads, int(host["cgroup_cpu_quota"])))
+            rm = cpu_rate(blob_s, off_s, lens_s, flows, max(args.cpu_seconds / 2, 1.0), threads=threads)
+            out["cpu_baseline_all_cores"] = {"value": round(rm["gbps"], 3), "unit": "GB/s", "cores": rm["cores"],
+                                             "mpkt_s": round(rm["mpkt_s"], 2), **host}
     if rank == 0 and world == 1 and not args.no_extras and name == "c2_tcp1500":
-        # secondary: 64 B UDP Mpkt/s (config 3) on rotating batches
-        eng3 = RxEngine(Config(synth.BOB_IPV4), device=dev)
-        b3 = [make_batch(eng3, "c3_udp64", 0, synth.SEED + 1000 * k)[0] for k in range(8)]
-        r3 = eng3.results(b3[0].n)
-        w3, k3, _ = time_kernel(eng3, b3, r3, 40, 4, stream)
-        n3 = b3[0].n
-        k3avg = float(np.mean(k3))
-        algo3 = n3 * (64 + DESC_BYTES + RESULT_BYTES)
-        out["c3_udp64"] = {"gbps": round(n3 * 64 * 40 / w3 / 1e9, 2), "mpkt_s": round(n3 * 40 / w3 / 1e6, 1),
-                           "kernel_ms_avg": round(k3avg * 1e3, 4), "kernel": "dk_rx_small_kernel",
-                           "algorithmic_bytes_per_launch": algo3,
-                           "roofline_achieved_gbps": round(algo3 / k3avg / 1e9, 1),
-                           "roofline_frac": round(algo3 / k3avg / 1e9 / HBM_PEAK_GBS, 4)}
-        del b3, r3, eng3
-        # host-resident path (NIC ring / socket buffer in pinned host memory): H2D frames + descriptors, kernel,
-        # D2H results, pipelined on 3 streams (dk_rx_process_host). Reported beside `value`, never as `value`.
+        # the other BASELINE configs on this GPU (per-GPU shards of C4 / C5), each with its own roofline
+        c3, e, _, _ = rx_extra("c3_udp64", dev, stream, steps=40, warmup=4, rotate=8)
+        c3b, e, _, _ = rx_extra("c3_udp64", dev, stream, steps=40, warmup=4, rotate=8, dst_ip=False)
+        c3["compact_20B_results"] = {k: c3b[k] for k in ("gbps", "mpkt_s", "kernel_ms_avg", "roofline")}
+        out["c3_udp64"] = c3
+        del e
+        out["c4_imix"], e, _, _ = rx_extra("c4_imix", dev, stream)
+        del e
+        out["c5_device"], e5, b5, f5 = rx_extra("c5_tcp1500_10k", dev, stream)
+        # C5 end to end: the per-GPU shard in pinned host memory -> HBM -> kernel -> results to pinned host memory
+        out["c5_host_path"] = host_path_rate(e5, b5, f5, b5.n)
+        out["c5_host_path"]["workload"] = WORKLOADS["c5_tcp1500_10k"][0]
+        del e5, b5
+        # host-resident path (NIC ring / socket buffer in pinned host memory) on a C2 slice, and the TPACKET_V3 ring
         out["host_path"] = host_path_rate(eng, batch, flows, args.host_frames)
         out["ring_path"] = ring_path_rate(eng, batch, flows, args.host_frames)
         # TX checksum fill (dk_tx_checksum) over the same batch (rewrites its checksum fields)
@@ -474,6 +536,8 @@ def main():
         out["tcp_rx_64conns"] = tcp_rate(stream, 1 << 20, 64, cpu_seconds=1.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.destroy()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -5,6 +5,7 @@ the 4-tuple socket demux, run as hand-written HIP kernels over HBM-resident fram
 (include/dk_rx.h, libdk_rx.so). See DESIGN.md and INTEGRATION.md.
 """
 from .rx import (  # noqa: F401
+    Comm,
     Config,
     Fail,
     FrameBatch,
@@ -17,7 +18,8 @@ from .rx import (  # noqa: F401
     ipv4,
     ipv4_str,
     raise_for_verdict,
+    tx_tuning,
 )
 
-__all__ = ["Config", "Fail", "FrameBatch", "RxEngine", "RxResults", "SocketId", "V", "VERDICTS", "flow_array",
-           "ipv4", "ipv4_str", "raise_for_verdict"]
+__all__ = ["Comm", "Config", "Fail", "FrameBatch", "RxEngine", "RxResults", "SocketId", "V", "VERDICTS", "flow_array",
+           "ipv4", "ipv4_str", "raise_for_verdict", "tx_tuning"]

@@ -68,6 +68,7 @@ FUNCTIONS = [
     ("dk_rx_flow_table_size", c_uint32, [c_void_p]),
     ("dk_rx_process", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_void_p]),
     ("dk_rx_process_host", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_uint32]),
+    ("dk_rx_flow_counts_allreduce", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p]),
     ("dk_tx_checksum", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
     ("dk_rx_verdict_name", c_char_p, [c_int]),
     ("dk_rx_verdict_errno", c_int, [c_int]),
@@ -145,13 +146,30 @@ class DemiSgarray(ctypes.Structure):
 DEMI_FUNCTIONS = [
     ("dk_rx_into_sgarrays", c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     POINTER(DemiSgarray), c_void_p, c_uint32, POINTER(c_uint32)]),
+    ("dk_tcp_into_sgarrays", c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p, POINTER(DemiSgarray),
+                                     c_uint32, POINTER(c_uint32)]),
+]
+
+# include/dk_comm.h: RCCL communicator bootstrap (the receive path's one collective is dk_rx_flow_counts_allreduce)
+DK_COMM_ID_BYTES = 128
+COMM_FUNCTIONS = [
+    ("dk_comm_unique_id", c_int, [c_void_p]),
+    ("dk_comm_init_rank", c_int, [POINTER(c_void_p), c_int32, c_void_p, c_int32, c_int32]),
+    ("dk_comm_init_all", c_int, [c_void_p, c_int32, c_void_p]),
+    ("dk_comm_count", c_int, [c_void_p, POINTER(c_int32)]),
+    ("dk_comm_destroy", c_int, [c_void_p]),
 ]
 
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
     ("dk_diag_path_stats_enable", c_int, [c_void_p, c_int]),
     ("dk_diag_path_stats_read", c_int, [c_void_p, c_void_p]),
+    ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p]),
+    ("dk_diag_tx_set_tuning", c_int, [c_int32, c_int32, c_int32]),
 ]
+DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug"]
+
+ALL_FUNCTIONS = FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS + DEMI_FUNCTIONS + COMM_FUNCTIONS
 
 _lib = None
 
@@ -171,11 +189,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
-    for name, restype, argtypes in FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS + DEMI_FUNCTIONS:
+    for name, restype, argtypes in ALL_FUNCTIONS:
         fn = getattr(lib, name, None)
         if fn is None:
-            if (name, restype, argtypes) in DIAG_FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DEMI_FUNCTIONS and path != LIB_PATH:
-                continue  # older tuning builds may predate a diagnostic
+            if path != LIB_PATH:
+                continue  # tuning builds (older sources) may predate a function
             raise ImportError(f"{path}: missing {name}")
         fn.restype = restype
         fn.argtypes = argtypes

@@ -111,11 +111,15 @@ int dk_ring_scan_tpacket3(const void* ring, uint64_t ring_bytes, uint32_t block_
         __atomic_load(status_word(r, base), &status, __ATOMIC_ACQUIRE);  // pairs with the kernel's block close
         if (!(status & TP_STATUS_USER)) break;                            // still the kernel's
         rc = scan_block(r, base, block_size, off, len, cap, n);
-        if (rc == ENOSPC && k > 0) {  // the blocks before it are complete: stop there
+        if (rc && k > 0) {  // the blocks before it are complete: return them; the next call starts at this block
             rc = 0;
             break;
         }
-        if (rc) break;
+        if (rc == EBADMSG) {  // the first block is malformed: report it, consumed (the caller hands it back)
+            k++;
+            break;
+        }
+        if (rc) break;  // ENOSPC with the first block: it alone holds more than cap frames, nothing consumed
         if (n == cap) {  // full: the next block cannot fit
             k++;
             break;

@@ -41,11 +41,26 @@ DK_HD uint32_t flow_hash(uint32_t kind, uint32_t lip, uint32_t rip, uint32_t por
 
 // Per-flow counting strategy (chosen per launch by the host).
 constexpr uint32_t kFlowNone = 0;    // no flow_counts requested
-constexpr uint32_t kFlowLds = 1;     // per-workgroup packed-u16 LDS histogram + scratch rows + reduce kernel
+constexpr uint32_t kFlowLds = 1;     // per-workgroup packed-u16 LDS histogram + scratch rows, combined per launch
 constexpr uint32_t kFlowGlobal = 2;  // per-frame u64 global atomics (tables too large for LDS)
 constexpr uint32_t kMaxLdsFlowWords = 16384;  // 64 KiB of LDS -> up to 32768 flows on the LDS path
 constexpr uint32_t kVerdictWords = (DK_V_COUNT + 3) & ~3u;  // verdict histogram columns of a scratch row
 constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
+// Counter rows are combined inside the launch (flush_counters, rx_kernels.hip): workgroups are grouped kCountGroup at a
+// time, each group has one arrival ticket, and the group's last arriver sums the group's rows into the caller's u64
+// counters. Rows are padded to whole 128-byte lines.
+// In-launch combining pays per workgroup (its row store drain and ticket round trip at exit); a second launch pays a
+// kernel boundary. Measured: in-launch is faster up to ~768 workgroups (C2 -1.3 us, IMIX -1 us), the
+// second launch at 1536 (C3 +2.3 us in-launch). The host picks per launch: in-launch when grid <= kFusedMaxGrid.
+#ifndef DK_FUSED_MAX_GRID
+#define DK_FUSED_MAX_GRID 1024
+#endif
+constexpr uint32_t kFusedMaxGrid = DK_FUSED_MAX_GRID;
+#ifndef DK_COUNT_GROUP
+#define DK_COUNT_GROUP 16
+#endif
+constexpr uint32_t kCountGroup = DK_COUNT_GROUP;
+constexpr uint32_t kRowAlignWords = 32;
 
 // Kernel parameters (passed by value).
 struct RxParams {
@@ -63,8 +78,11 @@ struct RxParams {
     uint32_t flow_mode;      // kFlow*
     uint32_t flow_words;     // kFlowLds: ceil(nflows / 2), else 0
     uint32_t row_words;      // words per workgroup row of flow_scratch: flow_words + (verdict_counts ? kVerdictWords : 0)
-    uint32_t* flow_scratch;  // [grid][row_words]: the packed-u16 flow histogram (kFlowLds), then the u32 verdict
+    uint32_t row_stride;     // row_words rounded up to kRowAlignWords
+    uint32_t* flow_scratch;  // [grid][row_stride]: the packed-u16 flow histogram (kFlowLds), then the u32 verdict
                              // histogram; nullptr when row_words == 0
+    uint32_t* tickets;       // [ceil(grid / kCountGroup)] arrival tickets, 0 between launches (the last arriver resets)
+    uint32_t fused;          // 1: rows combined in-launch (flush_counters); 0: plain rows + dk_flow_reduce_kernel
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
     uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave
     uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path

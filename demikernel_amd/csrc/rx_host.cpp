@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -20,10 +21,25 @@ namespace {
 constexpr int kPipeStreams = 3;
 constexpr uint32_t kDefaultChunkFrames = 1u << 16;
 constexpr uint64_t kMaxChunkBytes = 256ull << 20;
+constexpr size_t kMaxStreamSlots = 8;
 
-struct FlowScratch {  // per-workgroup flow-count rows for the kFlowLds path (one per concurrent launch)
-    uint32_t* p = nullptr;
-    size_t words = 0;
+// Counter scratch of one stream's launches: per-workgroup rows and the group arrival tickets of flush_counters
+// (rx_kernels.hip). Tickets are zeroed once at allocation; each launch's last arrivers reset theirs.
+struct CountScratch {
+    uint32_t* rows = nullptr;
+    size_t rows_words = 0;
+    uint32_t* tickets = nullptr;
+    uint32_t ntickets = 0;
+};
+
+// A context's scratch is keyed by stream: calls on different streams never share counter rows or tickets, so their
+// launches may run concurrently. Past kMaxStreamSlots streams the least recently used slot is taken over, and the new
+// stream first waits for the slot's last launch (its event).
+struct StreamSlot {
+    hipStream_t stream = nullptr;
+    CountScratch cs;
+    hipEvent_t last = nullptr;  // non-null once the slot is in use; ordering event for a takeover
+    uint64_t stamp = 0;
 };
 
 struct Stage {  // device staging for one pipeline stream
@@ -34,7 +50,13 @@ struct Stage {  // device staging for one pipeline stream
     uint16_t* desc_len = nullptr;
     uint32_t* res = nullptr;  // 9 result arrays of chunk_cap entries
     uint32_t cap = 0;
-    FlowScratch scratch;
+};
+
+// Tuning overrides (-1 = the host rule). Read once from the environment at dk_rx_ctx_create (DK_RX_STAGE, DK_RX_SPLIT,
+// DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID, DK_RX_GRID_PER_CU, DK_RX_DEBUG) or set by dk_diag_rx_set_tuning; never read on
+// the launch path.
+struct Tuning {
+    int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
 };
 
 }  // namespace
@@ -49,7 +71,9 @@ struct dk_rx_ctx {
     uint64_t* d_flow_counts = nullptr;
     uint32_t d_flow_cap = 0;
     uint64_t* d_verdict_counts = nullptr;
-    FlowScratch scratch;      // for dk_rx_process (device-resident path)
+    StreamSlot slots[kMaxStreamSlots];
+    uint64_t clock = 0;
+    Tuning tune;
     uint32_t cu_count = 0;
     uint32_t occ_dyn = ~0u;   // occupancy cache: dynamic LDS bytes -> resident blocks per CU
     uint32_t occ_blocks = 0;
@@ -76,6 +100,11 @@ uint32_t next_pow2(uint32_t x) {
     return p;
 }
 
+int32_t env_knob(const char* name) {
+    const char* e = getenv(name);
+    return e ? (int32_t)atoi(e) : -1;
+}
+
 int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask) {
     uint32_t* d = nullptr;
     if (hipMalloc(&d, slots.size() * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
@@ -89,29 +118,86 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
     return 0;
 }
 
-int ensure_scratch(FlowScratch& f, size_t words) {
-    if (f.words >= words) return 0;
-    if (f.p) (void)hipFree(f.p);
-    f.p = nullptr;
-    f.words = 0;
-    if (hipMalloc(&f.p, words * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
-    f.words = words;
+void free_slot(StreamSlot& s) {  // the caller has synchronised the device
+    if (s.cs.rows) (void)hipFree(s.cs.rows);
+    if (s.cs.tickets) (void)hipFree(s.cs.tickets);
+    if (s.last) (void)hipEventDestroy(s.last);
+    s = StreamSlot{};
+}
+
+// The slot of `stream`. Past kMaxStreamSlots streams the least recently used slot is taken over: an event recorded on
+// its stream now completes after every launch that used the slot, and the new stream waits for it.
+#ifndef DK_SLOT_EVENTS
+#define DK_SLOT_EVENTS 0  // 1: record the slot's event after every launch (measured: costs the launch gap)
+#endif
+int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
+    StreamSlot* pick = nullptr;
+    for (StreamSlot& s : c->slots)
+        if (s.last && s.stream == stream) pick = &s;
+    if (!pick)
+        for (StreamSlot& s : c->slots)
+            if (!s.last) {
+                if (hipEventCreateWithFlags(&s.last, hipEventDisableTiming) != hipSuccess) {
+                    s.last = nullptr;
+                    return EIO;
+                }
+                s.stream = stream;
+                pick = &s;
+                break;
+            }
+    if (!pick) {  // every slot belongs to another stream: take over the least recently used one, behind its work
+        pick = &c->slots[0];
+        for (StreamSlot& s : c->slots)
+            if (s.stamp < pick->stamp) pick = &s;
+#if !DK_SLOT_EVENTS
+        if (hipEventRecord(pick->last, pick->stream) != hipSuccess) return EIO;
+#endif
+        if (hipStreamWaitEvent(stream, pick->last, 0) != hipSuccess) return EIO;
+        pick->stream = stream;
+    }
+    pick->stamp = ++c->clock;
+    *out = pick;
     return 0;
 }
 
-void free_scratch(FlowScratch& f) {
-    if (f.p) (void)hipFree(f.p);
-    f = FlowScratch{};
+// Rows for `grid` workgroups and their group tickets. Growing waits for the slot's last launch before freeing.
+int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride) {
+    CountScratch& cs = s.cs;
+    const size_t words = (size_t)grid * row_stride;
+    const uint32_t nt = (grid + dk::kCountGroup - 1) / dk::kCountGroup;
+    if (cs.rows_words >= words && cs.ntickets >= nt) return 0;
+    if (hipStreamSynchronize(s.stream) != hipSuccess) return EIO;  // launches still using the old buffers
+    if (cs.rows_words < words) {
+        if (cs.rows) (void)hipFree(cs.rows);
+        cs.rows = nullptr;
+        cs.rows_words = 0;
+        if (hipMalloc(&cs.rows, words * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+        cs.rows_words = words;
+    }
+    if (cs.ntickets < nt) {
+        if (cs.tickets) (void)hipFree(cs.tickets);
+        cs.tickets = nullptr;
+        cs.ntickets = 0;
+        if (hipMalloc(&cs.tickets, nt * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+        if (hipMemset(cs.tickets, 0, nt * sizeof(uint32_t)) != hipSuccess) return EIO;
+        cs.ntickets = nt;
+    }
+    return 0;
 }
 
-// Choose the flow-count mode and the persistent grid, then launch (main kernel + flow reduce).
-int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
+// Choose the flow-count mode and the persistent grid, then launch on `stream` with that stream's counter scratch.
+// size_hint = bytes of blob the batch covers (the family and grid follow the mean bytes per frame).
+int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t stream) {
     if (p.n == 0) return 0;
+    const Tuning& T = c->tune;
     const uint32_t ntiles = (p.n + 255) / 256;
     p.flow_mode = dk::kFlowNone;
     p.flow_words = 0;
     p.row_words = 0;
+    p.row_stride = 0;
     p.flow_scratch = nullptr;
+    p.tickets = nullptr;
+    p.fused = 0;
     uint32_t dyn = 0;
     if (p.res.flow_counts && c->nflows) {
         const uint32_t words = (c->nflows + 1) / 2;
@@ -124,22 +210,21 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         }
     }
     // Kernel instantiation, schedule and resident workgroups per CU (measured, DESIGN.md §8 "Tuning log"):
-    //  - frames of >= 128 bytes of blob on average: the result-staging kernel (stores leave in one burst per 6 chunks
-    //    instead of between the frame reads; -11 % at C2, -4 % IMIX; no gain for 64-byte frames, which are
-    //    issue-bound and want 4 WG/CU);
-    //  - round-robin 256-frame tiles (sched 0) for every frame size (contiguous per-wave shares, sched 1, measured
-    //    1-3 % slower once stores are staged).
+    //  - >= 1 KiB of blob per frame: the split kernel (stream waves + finish waves, one 512-thread workgroup per CU);
+    //  - >= 128 bytes: the result-staging kernel (stores leave in one burst per 6 chunks instead of between the frame
+    //    reads; -11 % at C2 before the split kernel, -4 % IMIX);
+    //  - <= 96 bytes: the small-frame kernel (issue/latency-bound, wants occupancy);
+    //  - round-robin 256-frame tiles (sched 0) for every frame size.
     // Never more workgroups per CU than the occupancy admits (large socket tables take LDS).
-    const uint64_t bytes_per_frame = p.frames_bytes / p.n;
+    const uint64_t bytes_per_frame = size_hint / p.n;
     p.stage = bytes_per_frame >= 128 ? 1u : 0u;
     p.split = bytes_per_frame >= 1024 ? 1u : 0u;
-    if (const char* e = getenv("DK_RX_STAGE")) p.stage = atoi(e) ? 1u : 0u;  // tuning
-    if (const char* e = getenv("DK_RX_SPLIT")) p.split = atoi(e) ? 1u : 0u;  // tuning
     p.small = bytes_per_frame <= 96 ? 1u : 0u;
-    if (const char* e = getenv("DK_RX_SMALL")) p.small = atoi(e) ? 1u : 0u;  // tuning
+    if (T.stage >= 0) p.stage = T.stage ? 1u : 0u;
+    if (T.split >= 0) p.split = T.split ? 1u : 0u;
+    if (T.small >= 0) p.small = T.small ? 1u : 0u;
     if (p.small) p.split = p.stage = 0;
-    p.sched = 0;
-    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
+    p.sched = T.sched >= 0 ? (uint32_t)std::min(T.sched, 3) : 0u;
     const uint32_t family = p.small   ? dk::kFamilySmall
                             : p.split ? dk::kFamilySplit
                             : p.stage ? dk::kFamilyStaged
@@ -150,26 +235,36 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, FlowScratch& fs, void* stream) {
         c->occ_family = family;
     }
     uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u);
-    if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);
+    if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
-    if (const char* e = getenv("DK_RX_GRID")) grid = std::min(ntiles, (uint32_t)std::max(atoi(e), 1));  // tests/tuning
+    if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
-    // Per-workgroup histogram rows (flow pairs, then verdicts), added up by dk_flow_reduce_kernel.
+    StreamSlot* slot = nullptr;
+    int rc = acquire_slot(c, stream, &slot);
+    if (rc) return rc;
+    // Per-workgroup histogram rows (flow pairs, then verdicts), combined in-launch per group of workgroups.
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
     if (p.row_words) {
-        int rc = ensure_scratch(fs, (size_t)grid * p.row_words);
-        if (rc) return rc;
-        p.flow_scratch = fs.p;
+        p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
+        if ((rc = ensure_counts(*slot, grid, p.row_stride))) return rc;
+        p.flow_scratch = slot->cs.rows;
+        p.tickets = slot->cs.tickets;
+        p.fused = grid <= dk::kFusedMaxGrid ? 1u : 0u;
     }
-    if (getenv("DK_RX_DEBUG"))
-        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u\n",
-                p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split);
-    return dk_launch_rx(p, grid, stream);
+    if (T.debug > 0)
+        fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
+                        "small=%u\n",
+                p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
+                p.small);
+    rc = dk_launch_rx(p, grid, stream);
+#if DK_SLOT_EVENTS
+    if (rc == 0 && hipEventRecord(slot->last, stream) != hipSuccess) rc = EIO;
+#endif
+    return rc;
 }
 
 void free_stage(Stage& s) {
-    free_scratch(s.scratch);
     if (s.frames) (void)hipFree(s.frames);
     if (s.desc_off) (void)hipFree(s.desc_off);
     if (s.desc_len) (void)hipFree(s.desc_len);
@@ -197,6 +292,17 @@ int ensure_stage(Stage& s, uint32_t cap, uint64_t bytes) {
         s.frames_cap = bytes;
     }
     return 0;
+}
+
+// TX tuning overrides (-1 = host rule): DK_TX_SPLIT, DK_RX_SCHED, DK_RX_GRID_PER_CU read once per process, or set by
+// dk_diag_tx_set_tuning; never read from the environment on the launch path.
+struct TxTuning {
+    std::atomic<int32_t> split{-1}, sched{-1}, grid_per_cu{-1};
+    TxTuning() : split(env_knob("DK_TX_SPLIT")), sched(env_knob("DK_RX_SCHED")), grid_per_cu(env_knob("DK_RX_GRID_PER_CU")) {}
+};
+TxTuning& tx_tuning() {
+    static TxTuning t;
+    return t;
 }
 
 dk::RxParams base_params(const dk_rx_ctx* c) {
@@ -235,6 +341,14 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || cus <= 0)
         cus = 256;
     c->cu_count = (uint32_t)cus;
+    Tuning& t = c->tune;  // tuning overrides: read once here, never on the launch path
+    t.stage = env_knob("DK_RX_STAGE");
+    t.split = env_knob("DK_RX_SPLIT");
+    t.small = env_knob("DK_RX_SMALL");
+    t.sched = env_knob("DK_RX_SCHED");
+    t.grid = env_knob("DK_RX_GRID");
+    t.grid_per_cu = env_knob("DK_RX_GRID_PER_CU");
+    t.debug = env_knob("DK_RX_DEBUG");
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4, 0u);
     int rc = upload_table(c, slots, dk::kMinTableSlots - 1);
@@ -253,7 +367,8 @@ void dk_rx_ctx_destroy(dk_rx_ctx* c) {
     for (Stage& s : c->stages) free_stage(s);
     if (c->d_flow_counts) (void)hipFree(c->d_flow_counts);
     if (c->d_verdict_counts) (void)hipFree(c->d_verdict_counts);
-    free_scratch(c->scratch);
+    (void)hipDeviceSynchronize();  // launches still using the context's scratch (streams may be gone)
+    for (StreamSlot& s : c->slots) free_slot(s);
     if (c->d_path_stats) (void)hipFree(c->d_path_stats);
     delete c;
 }
@@ -296,7 +411,7 @@ uint32_t dk_rx_flow_table_size(const dk_rx_ctx* c) { return c ? c->nflows : 0; }
 int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, void* stream) {
     if (!c || !b || !r) return EINVAL;
     if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
-    if (b->n && (!r->meta || !r->src_ip || !r->dst_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
+    if (b->n && (!r->meta || !r->src_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
     if (b->frames_bytes > DK_RX_MAX_BLOB) return EINVAL;
     DeviceGuard g(c->cfg.device);
     dk::RxParams p = base_params(c);
@@ -307,13 +422,13 @@ int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, vo
     p.n = b->n;
     p.aligned16 = (b->flags & DK_RX_BATCH_ALIGNED16) ? 1u : 0u;
     p.res = *r;
-    return launch_batch(c, p, c->scratch, stream);
+    return launch_batch(c, p, b->frames_bytes, (hipStream_t)stream);
 }
 
 int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, uint32_t chunk_frames) {
     if (!c || !b || !r) return EINVAL;
     if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
-    if (b->n && (!r->meta || !r->src_ip || !r->dst_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
+    if (b->n && (!r->meta || !r->src_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
     if (b->frames_bytes > DK_RX_MAX_BLOB) return EINVAL;
     if (b->n == 0) return 0;
     DeviceGuard g(c->cfg.device);
@@ -390,7 +505,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         uint32_t* R = st.res;
         p.res.meta = R;
         p.res.src_ip = R + (size_t)st.cap;
-        p.res.dst_ip = R + 2 * (size_t)st.cap;
+        p.res.dst_ip = r->dst_ip ? R + 2 * (size_t)st.cap : nullptr;
         p.res.ports = R + 3 * (size_t)st.cap;
         p.res.payload = R + 4 * (size_t)st.cap;
         p.res.flow_id = R + 5 * (size_t)st.cap;
@@ -399,7 +514,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         p.res.tcp_win = r->tcp_win ? R + 8 * (size_t)st.cap : nullptr;
         p.res.flow_counts = r->flow_counts ? c->d_flow_counts : nullptr;
         p.res.verdict_counts = r->verdict_counts ? c->d_verdict_counts : nullptr;
-        rc = launch_batch(c, p, st.scratch, st.stream);
+        rc = launch_batch(c, p, ch.hi - ch.lo, st.stream);
         if (rc) break;
         uint32_t* outs[9] = {r->meta, r->src_ip, r->dst_ip, r->ports, r->payload, r->flow_id,
                              r->tcp_seq, r->tcp_ack, r->tcp_win};
@@ -449,6 +564,21 @@ int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
     return hipMemcpy(out, c->d_path_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : EIO;
 }
 
+int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t knobs[DK_DIAG_RX_KNOBS]) {
+    if (!c || !knobs) return EINVAL;
+    c->tune = Tuning{knobs[0], knobs[1], knobs[2], knobs[3], knobs[4], knobs[5], knobs[6]};
+    c->occ_family = ~0u;
+    return 0;
+}
+
+int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu) {
+    TxTuning& t = tx_tuning();
+    t.split = split;
+    t.sched = sched;
+    t.grid_per_cu = grid_per_cu;
+    return 0;
+}
+
 int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
                    void* stream) {
     if (n && (!frames || !off || !len)) return EINVAL;
@@ -470,10 +600,11 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
     // Large frames: the split kernel (stream waves + finish waves, one 512-thread workgroup per CU, sched 0).
     const bool big = frames_bytes / n >= 1024;
     dk::TxParams p{frames, frames_bytes, off, len, n, big ? 1u : 0u, big ? 1u : 0u};
-    if (const char* e = getenv("DK_TX_SPLIT")) p.split = atoi(e) ? 1u : 0u;  // tuning
+    const TxTuning& T = tx_tuning();
+    if (T.split >= 0) p.split = T.split ? 1u : 0u;
     uint32_t per_cu = p.split ? 1u : std::min<uint32_t>(occ, p.sched ? 3u : 4u);
-    if (const char* e = getenv("DK_RX_SCHED")) p.sched = (uint32_t)std::min(std::max(atoi(e), 0), 3);  // tuning
-    if (const char* e = getenv("DK_RX_GRID_PER_CU")) per_cu = (uint32_t)std::max(atoi(e), 1);  // tuning
+    if (T.sched >= 0) p.sched = (uint32_t)std::min<int32_t>(T.sched, 3);
+    if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
     return dk_launch_tx(p, grid, stream);
 }

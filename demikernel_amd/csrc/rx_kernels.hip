@@ -794,7 +794,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
 #endif
         {
         st_res(P.res.src_ip + i, src);
-        st_res(P.res.dst_ip + i, dst);
+        if (P.res.dst_ip) st_res(P.res.dst_ip + i, dst);
         st_res(P.res.ports + i, ports);
         st_res(P.res.payload + i, pay);
         st_res(P.res.flow_id + i, fid);
@@ -892,7 +892,7 @@ __device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)
         const uint32_t i = c + r.lane_off;
         st_res(P.res.meta + i, stg[q].meta);
         st_res(P.res.src_ip + i, stg[q].src);
-        st_res(P.res.dst_ip + i, stg[q].dst);
+        if (P.res.dst_ip) st_res(P.res.dst_ip + i, stg[q].dst);
         st_res(P.res.ports + i, stg[q].ports);
         st_res(P.res.payload + i, stg[q].pay);
         st_res(P.res.flow_id + i, stg[q].fid);
@@ -928,24 +928,88 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
     }
 }
 
-// Workgroup exit: the LDS histograms go to this workgroup's scratch row with plain stores — flow words (kFlowLds),
-// then the verdict words — and dk_flow_reduce_kernel adds the rows into the caller's u64 counters. (A u64 device-scope
-// atomic per workgroup on the same few verdict addresses serialises at the memory side: 1024 workgroups cost ~14 us, a
-// third of a 64-byte-frame batch)
-__device__ __forceinline__ void write_row(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
-                                          const uint32_t* s_flow, const uint32_t* s_vh) {
+// Workgroup exit: the LDS histograms (flow words in kFlowLds mode, then the verdict words) reach the caller's u64
+// counters. Two forms, picked by the host per launch (P.fused, rx_common.h kFusedMaxGrid):
+// * in-launch (grids up to ~1k workgroups), no second kernel (a dependent launch costs a ~1.5-1.9 us boundary plus its
+//   own run):
+//   1. each workgroup writes its row write-through (sc1 stores: the line goes to memory and leaves this XCD's L2),
+//      every storing wave drains (s_waitcnt vmcnt(0)), then one lane adds 1 to its group's arrival ticket (agent
+//      scope);
+//   2. the workgroup whose add returns kCountGroup - 1 (the group's last) reads the group's rows with sc1 loads (L1
+//      bypassed; no other XCD has the lines cached: sc1 stores drop them) and adds the column sums to the caller's
+//      counters with device-scope atomics (kCountGroup rows per add: no same-address pile-up of every workgroup, which
+//      cost ~14 us at 1024 workgroups), then resets the ticket for the next launch.
+//   This is MI355X_MICROARCH.md §"inter-workgroup visibility", Valid forms row 1 (write-through payload, drained, one
+//   agent-scope add per storing workgroup, the last adder told by the returned value, sc1 loads): no release or
+//   acquire fence.
+// * larger grids (1536 workgroups of the small-frame kernel): plain row stores, dk_flow_reduce_kernel adds them up
+//   (measured faster there: every workgroup's exit drain and ticket round trip cost more than one boundary).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
+    return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
+                                               const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
     if (!P.row_words) return;
-    uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_words;
+    uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_stride;
+    if (!P.fused) {  // rows with plain stores; dk_flow_reduce_kernel (a second launch) adds them up
+        if (lds_flows)
+            for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
+        if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
+        return;
+    }
     if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
-    if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
+        for (uint32_t k = tid; k < P.flow_words; k += nthreads) st_wt(row + k, s_flow[k]);
+    if (P.res.verdict_counts && tid < kVerdictWords) st_wt(row + P.flow_words + tid, tid < DK_V_COUNT ? s_vh[tid] : 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its row stores have reached memory
+    __syncthreads();
+    const uint32_t g = blockIdx.x / kCountGroup, r0 = g * kCountGroup;
+    const uint32_t gn = min(kCountGroup, gridDim.x - r0);
+    if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add((gu32*)(P.tickets + g), 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = old == gn - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    const uint32_t* rows = P.flow_scratch + (size_t)r0 * P.row_stride;
+    for (uint32_t w = tid; w < P.row_words; w += nthreads) {
+        uint32_t x[kCountGroup];
+#pragma unroll
+        for (uint32_t k = 0; k < kCountGroup; k++)  // all loads in flight (a short group re-reads its last row)
+            x[k] = ld_wt(rows + (size_t)min(k, gn - 1) * P.row_stride + w);
+#pragma unroll
+        for (uint32_t k = 0; k < kCountGroup; k++) x[k] = k < gn ? x[k] : 0u;
+        uint64_t lo = 0, hi = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kCountGroup; k++) {
+            lo += x[k] & 0xFFFFu;
+            hi += x[k] >> 16;
+        }
+        if (w >= P.flow_words) {  // verdict column: a plain u32 count
+            const uint32_t v = w - P.flow_words;
+            const uint64_t t = lo + (hi << 16);
+            if (t && v < DK_V_COUNT)
+                atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + v), (unsigned long long)t);
+        } else {
+            if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + 2 * w), (unsigned long long)lo);
+            if (hi && 2 * w + 1 < P.nflows)
+                atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + 2 * w + 1), (unsigned long long)hi);
+        }
+    }
+    if (tid == 0) __hip_atomic_store((gu32*)(P.tickets + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
 // per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
-// wraps). At exit both histograms are written with plain stores to flow_scratch[b][*] (write_row) and
-// dk_flow_reduce_kernel adds the rows into the caller's u64 counters. kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
+// wraps). At exit both histograms reach the caller's u64 counters through flush_counters (in-launch, per group of
+// kCountGroup workgroups). kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
@@ -954,6 +1018,7 @@ __global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_
 void dk_rx_kernel(RxParams P) {
     __shared__ WaveLds s_wave[kWaves];        // per-wave phase B/C exchange
     __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
+    __shared__ uint32_t s_last;               // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
     const uint32_t tid = threadIdx.x;
@@ -1007,7 +1072,7 @@ void dk_rx_kernel(RxParams P) {
 
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     __syncthreads();
-    write_row(P, tid, kBlock, lds_flows, s_flow, s_vh);
+    flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh, &s_last);
 }
 
 // Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
@@ -1086,6 +1151,7 @@ template <bool kShift, bool kOpt>
 __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
     __shared__ SmallLds s_wave[kWaves];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
+    __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
     const uint32_t tid = threadIdx.x;
@@ -1154,7 +1220,7 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
         len1 = len2;
     }
     __syncthreads();
-    write_row(P, tid, kBlock, lds_flows, s_flow, s_vh);
+    flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh, &s_last);
 }
 
 // Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
@@ -1179,7 +1245,7 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
         const uint32_t i = c + r.lane_off;
         st_res(P.res.meta + i, stg[q].meta);
         st_res(P.res.src_ip + i, stg[q].src);
-        st_res(P.res.dst_ip + i, stg[q].dst);
+        if (P.res.dst_ip) st_res(P.res.dst_ip + i, stg[q].dst);
         st_res(P.res.ports + i, stg[q].ports);
         st_res(P.res.payload + i, stg[q].pay);
         st_res(P.res.flow_id + i, stg[q].fid);
@@ -1190,6 +1256,7 @@ template <bool kShift>
 __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P) {
     __shared__ WaveLds s_buf[2][kWaves];   // [period parity][stream wave]
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
+    __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
     const uint32_t tid = threadIdx.x;
@@ -1252,7 +1319,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
         __syncthreads();
     }
     if (finisher && nstg) flush_split(P, stg, nstg, r, klast);
-    write_row(P, tid, kSplitBlock, lds_flows, s_flow, s_vh);
+    flush_counters(P, tid, kSplitBlock, lds_flows, s_flow, s_vh, &s_last);
 }
 
 // Adds the per-workgroup rows of flow_scratch[rows][row_words] into the caller's u64 counters: columns
@@ -1263,7 +1330,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
 constexpr uint32_t kReduceRows = 64;
 constexpr uint32_t kReduceCols = 64;
 __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* scratch, uint32_t rows,
-                                                                uint32_t row_words, uint32_t flow_words,
+                                                                uint32_t row_words, uint32_t row_stride, uint32_t flow_words,
                                                                 uint32_t nflows, uint64_t* counts,
                                                                 uint64_t* verdicts) {
     __shared__ uint64_t s_part[kWaves][2][kReduceCols];
@@ -1276,7 +1343,7 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
 #pragma unroll
         for (uint32_t k = 0; k < kReduceRows / kWaves; k++) {
             const uint32_t r = r0 + wv + k * kWaves;
-            x[k] = r < r1 ? scratch[(size_t)r * row_words + w] : 0u;
+            x[k] = r < r1 ? scratch[(size_t)r * row_stride + w] : 0u;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kReduceRows / kWaves; k++) {
@@ -1302,6 +1369,7 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
     if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2 * w), (unsigned long long)lo);
     if (hi && 2 * w + 1 < nflows) atomicAdd(reinterpret_cast<unsigned long long*>(counts + 2 * w + 1), (unsigned long long)hi);
 }
+
 
 // ---------------------------------------------------------------------------------------------------------------------
 // TX checksum fill: Ipv4Header::serialize_and_attach (ipv4/header.rs:229-266),
@@ -1610,12 +1678,11 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     else
         hipLaunchKernelGGL((dk::dk_rx_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     if (hipGetLastError() != hipSuccess) return 5;
-    if (p.row_words) {
+    if (p.row_words && !p.fused) {
         const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
                       (grid + dk::kReduceRows - 1) / dk::kReduceRows);
-        hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, (hipStream_t)stream,
-                           p.flow_scratch, grid, p.row_words, p.flow_words, p.nflows, p.res.flow_counts,
-                           p.res.verdict_counts);
+        hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, s, p.flow_scratch, grid, p.row_words,
+                           p.row_stride, p.flow_words, p.nflows, p.res.flow_counts, p.res.verdict_counts);
         if (hipGetLastError() != hipSuccess) return 5;
     }
     return 0;

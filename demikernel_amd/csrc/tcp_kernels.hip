@@ -523,14 +523,12 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     }
 }
 
-// Which walk runs: DK_TCP_WALK=lane|wave forces one; otherwise the wave walk when connections average at least
-// kWaveWalkMinSegs segments in the batch.
+// Which walk runs: `force` (DK_TCP_WALK=lane|wave, read once at dk_tcp_ctx_create: 0 lane, 1 wave, -1 the rule);
+// otherwise the wave walk when connections average at least kWaveWalkMinSegs segments in the batch.
 constexpr uint32_t kWaveWalkMinSegs = 8;
-bool use_wave_walk(uint32_t n, uint32_t nconns) {
+bool use_wave_walk(uint32_t n, uint32_t nconns, int force) {
     if (nconns > (1u << 24)) return false;  // grid of nconns waves
-    const char* e = getenv("DK_TCP_WALK");
-    if (e && !strcmp(e, "lane")) return false;
-    if (e && !strcmp(e, "wave")) return true;
+    if (force >= 0) return force == 1;
     return (uint64_t)n >= (uint64_t)kWaveWalkMinSegs * nconns;
 }
 
@@ -559,8 +557,15 @@ int grow(T*& p, size_t& cap, size_t n) {
 }  // namespace
 }  // namespace dk_tcp
 
+// One scratch set per context (sort keys, sorted pairs, records, ranges, sort temp). Calls are ordered on their
+// streams; a call on a different stream than the previous one first waits for the previous call's work (`last`), so
+// two streams never overlap on the scratch, and growing it waits for that work before freeing.
 struct dk_tcp_ctx {
     int device = 0;
+    int walk = -1;  // DK_TCP_WALK at creation: 0 lane, 1 wave, -1 the engine's rule
+    hipEvent_t last = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool used = false;
     uint32_t *keys = nullptr, *skeys = nullptr, *svals = nullptr, *range = nullptr;
     size_t keys_cap = 0, skeys_cap = 0, svals_cap = 0, range_cap = 0;
     uint4* rec = nullptr;
@@ -576,8 +581,14 @@ int dk_tcp_ctx_create(int32_t device, dk_tcp_ctx** out) {
     *out = nullptr;
     int nd = 0;
     if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return EINVAL;
+    dk_tcp::DeviceGuard g(device);
     dk_tcp_ctx* t = new dk_tcp_ctx();
     t->device = device;
+    if (const char* e = getenv("DK_TCP_WALK")) t->walk = !strcmp(e, "wave") ? 1 : !strcmp(e, "lane") ? 0 : -1;
+    if (hipEventCreateWithFlags(&t->last, hipEventDisableTiming) != hipSuccess) {
+        delete t;
+        return EINVAL;
+    }
     *out = t;
     return 0;
 }
@@ -585,8 +596,10 @@ int dk_tcp_ctx_create(int32_t device, dk_tcp_ctx** out) {
 void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     if (!t) return;
     dk_tcp::DeviceGuard g(t->device);
+    if (t->used) (void)hipEventSynchronize(t->last);
     for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp})
         if (p) (void)hipFree(p);
+    (void)hipEventDestroy(t->last);
     delete t;
 }
 
@@ -604,6 +617,9 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     DeviceGuard g(t->device);
     const hipStream_t s = (hipStream_t)stream;
     int rc = 0;
+    if (t->used && t->last_stream != s && hipStreamWaitEvent(s, t->last, 0) != hipSuccess) return EINVAL;
+    const bool grows = t->keys_cap < n || t->rec_cap < n || t->range_cap < (size_t)nconns + 1;
+    if (t->used && grows && hipEventSynchronize(t->last) != hipSuccess) return EINVAL;  // in-flight work on the scratch
     if ((rc = grow(t->keys, t->keys_cap, n)) || (rc = grow(t->skeys, t->skeys_cap, n)) ||
         (rc = grow(t->svals, t->svals_cap, n)) || (rc = grow(t->rec, t->rec_cap, n)) ||
         (rc = grow(t->range, t->range_cap, (size_t)nconns + 1)))
@@ -615,6 +631,7 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     if (rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, t->keys, t->skeys, index, t->svals, n, 0, bits,
                                               s) != hipSuccess)
         return EINVAL;
+    if (t->used && t->temp_cap < sort_bytes && hipEventSynchronize(t->last) != hipSuccess) return EINVAL;
     if ((rc = grow(t->temp, t->temp_cap, sort_bytes))) return rc;
 
     Params P{};
@@ -642,12 +659,16 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     }
     if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
     if (nconns) {
-        if (use_wave_walk(n, nconns))
+        if (use_wave_walk(n, nconns, t->walk))
             hipLaunchKernelGGL(dk_tcp_wave_walk_kernel, dim3(nconns), dim3(kWave), 0, s, P);
         else
             hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
     }
-    return hipGetLastError() == hipSuccess ? 0 : EINVAL;
+    if (hipGetLastError() != hipSuccess) return EINVAL;
+    if (hipEventRecord(t->last, s) != hipSuccess) return EINVAL;
+    t->last_stream = s;
+    t->used = true;
+    return 0;
 }
 
 }  // extern "C"

@@ -14,13 +14,21 @@ from typing import Optional
 import numpy as np
 
 from . import _native as N
-from .rx import RxResults, _check
+from .rx import Fail, RxResults, _check
 
 TP_STATUS_KERNEL, TP_STATUS_USER = 0, 1
 TPACKET_V3 = 2
 BLOCK_DESC_BYTES = 48  # sizeof(struct tpacket_block_desc)
 PKT_HDR_BYTES = 48  # sizeof(struct tpacket3_hdr)
 TP_MAC, TP_NET = 82, 96
+
+
+def _check_blocks(rc: int, what: str, blocks: int) -> None:
+    """Fail with the blocks the call consumed (a malformed first block counts as consumed: release it too)."""
+    if rc != 0:
+        e = Fail(rc, what)
+        e.blocks = blocks
+        raise e
 
 
 def page_aligned_empty(nbytes: int) -> np.ndarray:
@@ -112,9 +120,10 @@ class TpacketRing:
         off = np.zeros(max(cap, 1), np.uint32)
         ln = np.zeros(max(cap, 1), np.uint16)
         nf, nb = ctypes.c_uint32(), ctypes.c_uint32()
-        _check(self.lib.dk_ring_scan_tpacket3(self.ring.ctypes.data, self.ring.nbytes, self.block_size, first_block,
-                                              nblocks, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(nf),
-                                              ctypes.byref(nb)), "dk_ring_scan_tpacket3")
+        rc = self.lib.dk_ring_scan_tpacket3(self.ring.ctypes.data, self.ring.nbytes, self.block_size, first_block,
+                                            nblocks, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(nf),
+                                            ctypes.byref(nb))
+        _check_blocks(rc, "dk_ring_scan_tpacket3", nb.value)
         return off[:nf.value], ln[:nf.value], nb.value
 
     def release(self, first_block: int, nblocks: int) -> None:
@@ -126,7 +135,70 @@ class TpacketRing:
         Returns (frames, blocks consumed)."""
         nf, nb = ctypes.c_uint32(), ctypes.c_uint32()
         r = results.c_struct()
-        _check(self.lib.dk_rx_process_tpacket3(engine._ctx, self.ring.ctypes.data, self.ring.nbytes, self.block_size,
-                                               first_block, nblocks, ctypes.byref(r), results.n, ctypes.byref(nf),
-                                               ctypes.byref(nb)), "dk_rx_process_tpacket3")
+        rc = self.lib.dk_rx_process_tpacket3(engine._ctx, self.ring.ctypes.data, self.ring.nbytes, self.block_size,
+                                             first_block, nblocks, ctypes.byref(r), results.n, ctypes.byref(nf),
+                                             ctypes.byref(nb))
+        _check_blocks(rc, "dk_rx_process_tpacket3", nb.value)
         return nf.value, nb.value
+
+
+class PacketSocketRing:
+    """A live Linux receive ring: an AF_PACKET / SOCK_RAW socket (ETH_P_ALL) with PACKET_RX_RING in TPACKET_V3 mode,
+    mmap'd, bound to one interface — catpowder's RawSocket::new (catpowder/linux/rawsocket/rawsocket.rs:27-39: AF_PACKET,
+    SOCK_RAW | SOCK_NONBLOCK, ETH_P_ALL) with the kernel's block ring in place of one recvfrom per frame. `ring` is the
+    mapping as a u8 array, for TpacketRing. Needs CAP_NET_RAW (PermissionError otherwise)."""
+
+    SOL_PACKET, PACKET_RX_RING, PACKET_VERSION, PACKET_IGNORE_OUTGOING = 263, 5, 10, 23
+    ETH_P_ALL = 3
+
+    def __init__(self, ifname: str = "lo", block_size: int = 1 << 16, nblocks: int = 64, retire_ms: int = 4):
+        import mmap
+        import socket
+        import struct
+
+        s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(self.ETH_P_ALL))
+        try:
+            s.setsockopt(self.SOL_PACKET, self.PACKET_VERSION, TPACKET_V3)
+            try:  # only what the interface receives (a loopback send is seen again as outgoing otherwise)
+                s.setsockopt(self.SOL_PACKET, self.PACKET_IGNORE_OUTGOING, 1)
+            except OSError:
+                pass
+            frame_size = 2048
+            # struct tpacket_req3: block_size, block_nr, frame_size, frame_nr, retire_blk_tov, sizeof_priv,
+            # feature_req_word
+            req = struct.pack("7I", block_size, nblocks, frame_size, block_size * nblocks // frame_size, retire_ms, 0, 0)
+            s.setsockopt(self.SOL_PACKET, self.PACKET_RX_RING, req)
+            self.mm = mmap.mmap(s.fileno(), block_size * nblocks, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+            s.bind((ifname, self.ETH_P_ALL))
+        except Exception:
+            s.close()
+            raise
+        self.sock = s
+        self.ifname = ifname
+        self.block_size = block_size
+        self.nblocks = nblocks
+        self.ring = np.frombuffer(self.mm, np.uint8)
+
+    def block_ready(self, k: int) -> bool:
+        return bool(int(self.ring[k * self.block_size + 8: k * self.block_size + 12].view(np.uint32)[0]) & TP_STATUS_USER)
+
+    def close(self) -> None:
+        self.ring = None
+        try:
+            self.mm.close()
+        except BufferError:  # a numpy view is still alive; the mapping goes with the socket
+            pass
+        self.sock.close()
+
+
+def inject(ifname: str, frames: list) -> None:
+    """Send raw Ethernet frames out of `ifname` (loopback: they come back in as received frames)."""
+    import socket
+
+    s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(PacketSocketRing.ETH_P_ALL))
+    try:
+        s.bind((ifname, 0))
+        for f in frames:
+            s.send(f)
+    finally:
+        s.close()

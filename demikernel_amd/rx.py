@@ -124,13 +124,15 @@ class RxResults:
     TCP_ARRAYS = ["tcp_seq", "tcp_ack", "tcp_win"]
 
     def __init__(self, n: int, nflows: int, *, device=None, tcp_fields: bool = False, counts: bool = True,
-                 host: bool = False):
+                 host: bool = False, dst_ip: bool = True):
+        """dst_ip=False: the 20-byte-per-frame layout (dk_rx.h ABI 3: dst_ip not written)."""
         import torch
 
         kw = dict(device=device) if not host else dict(pin_memory=torch.cuda.is_available())
         self.n = n
         self.t = {}
-        for name in self.ARRAYS + (self.TCP_ARRAYS if tcp_fields else []):
+        names = [a for a in self.ARRAYS if dst_ip or a != "dst_ip"]
+        for name in names + (self.TCP_ARRAYS if tcp_fields else []):
             self.t[name] = torch.zeros(n, dtype=torch.int32, **kw)
         if counts:
             self.t["flow_counts"] = torch.zeros(max(nflows, 1), dtype=torch.int64, **kw)
@@ -182,11 +184,11 @@ class RxEngine:
         _check(self.lib.dk_rx_flow_table_set(self._ctx, flows.ctypes.data, len(flows)), "dk_rx_flow_table_set")
         self.nflows = len(flows)
 
-    def results(self, n: int, *, tcp_fields: bool = False, counts: bool = True) -> RxResults:
+    def results(self, n: int, *, tcp_fields: bool = False, counts: bool = True, dst_ip: bool = True) -> RxResults:
         import torch
 
         return RxResults(n, self.nflows, device=torch.device("cuda", self.device), tcp_fields=tcp_fields,
-                         counts=counts)
+                         counts=counts, dst_ip=dst_ip)
 
     def receive_batch(self, batch: FrameBatch, results: RxResults, stream=None) -> None:
         """Asynchronous on `stream` (a torch.cuda.Stream; default: the current stream)."""
@@ -219,6 +221,24 @@ class RxEngine:
         _check(self.lib.dk_diag_path_stats_read(self._ctx, out.ctypes.data), "dk_diag_path_stats_read")
         return out
 
+    def set_tuning(self, **knobs) -> None:
+        """Diagnostics (dk_diag.h): override the engine's kernel family / schedule / grid choices (-1 = its rule);
+        unnamed knobs go back to the rule. Names: stage, split, small, sched, grid, grid_per_cu, debug."""
+        bad = set(knobs) - set(N.DK_DIAG_RX_KNOBS)
+        assert not bad, bad
+        arr = (ctypes.c_int32 * len(N.DK_DIAG_RX_KNOBS))(*[int(knobs.get(k, -1)) for k in N.DK_DIAG_RX_KNOBS])
+        _check(self.lib.dk_diag_rx_set_tuning(self._ctx, arr), "dk_diag_rx_set_tuning")
+
+    def counts_allreduce(self, results: RxResults, comm: int, stream=None) -> None:
+        """dk_rx_flow_counts_allreduce: sum this batch's device counters over every rank of `comm` (an RCCL
+        communicator from dk_comm.h), in place, on `stream`."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        r = results.c_struct()
+        _check(self.lib.dk_rx_flow_counts_allreduce(self._ctx, ctypes.byref(r), ctypes.c_void_p(comm),
+                                                    ctypes.c_void_p(s.cuda_stream)), "dk_rx_flow_counts_allreduce")
+
     def tx_checksum(self, batch: FrameBatch, stream=None) -> None:
         """Fill IPv4/TCP/UDP checksums in place (serialize_and_attach with tx offload off)."""
         import torch
@@ -226,6 +246,48 @@ class RxEngine:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(self.lib.dk_tx_checksum(_ptr(batch.blob), batch.frames_bytes, _ptr(batch.off), _ptr(batch.len),
                                        batch.n, ctypes.c_void_p(s.cuda_stream)), "dk_tx_checksum")
+
+
+def tx_tuning(split: int = -1, sched: int = -1, grid_per_cu: int = -1) -> None:
+    """Diagnostics (dk_diag.h): TX kernel overrides for the process (-1 = the engine's rule)."""
+    _check(N.load_library().dk_diag_tx_set_tuning(split, sched, grid_per_cu), "dk_diag_tx_set_tuning")
+
+
+class Comm:
+    """An RCCL communicator (include/dk_comm.h) for the receive path's one collective."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * N.DK_COMM_ID_BYTES)()
+        _check(N.load_library().dk_comm_unique_id(buf), "dk_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def init_rank(cls, nranks: int, uid: bytes, rank: int, device: int) -> "Comm":
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * N.DK_COMM_ID_BYTES).from_buffer_copy(uid)
+        _check(N.load_library().dk_comm_init_rank(ctypes.byref(h), nranks, buf, rank, device), "dk_comm_init_rank")
+        return cls(h.value)
+
+    @classmethod
+    def init_all(cls, devices) -> list:
+        hs = (ctypes.c_void_p * len(devices))()
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        _check(N.load_library().dk_comm_init_all(hs, len(devices), devs), "dk_comm_init_all")
+        return [cls(h) for h in hs]
+
+    def count(self) -> int:
+        n = ctypes.c_int32()
+        _check(N.load_library().dk_comm_count(ctypes.c_void_p(self.handle), ctypes.byref(n)), "dk_comm_count")
+        return n.value
+
+    def destroy(self) -> None:
+        if self.handle:
+            _check(N.load_library().dk_comm_destroy(ctypes.c_void_p(self.handle)), "dk_comm_destroy")
+            self.handle = 0
 
 
 def verdict_errno(v: int) -> int:

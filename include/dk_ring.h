@@ -33,8 +33,12 @@ int dk_ring_unregister(void* ring);
 /* Walk blocks first_block .. first_block + nblocks - 1 (modulo ring_bytes / block_size) in order and write one
  * descriptor per frame: off = byte offset of the frame (tp_mac) from the ring base, len = tp_snaplen. Stops at the
  * first block that is not TP_STATUS_USER (still the kernel's). *n_frames = descriptors written, *n_blocks = blocks
- * consumed. A block whose packet chain leaves the block, or a frame longer than 65535 bytes, is EBADMSG; more frames
- * than cap is ENOSPC (nothing is consumed from the block that did not fit). */
+ * consumed. A block whose packet chain leaves the block, or a frame longer than 65535 bytes, is malformed; a block
+ * whose frames do not fit in the cap left is not consumed. Either stops the walk; then:
+ *   - after at least one complete block: returns 0 with those blocks (the next call starts at the stopping block);
+ *   - malformed first block: returns EBADMSG with *n_frames = 0 and *n_blocks = 1 (the block counts as consumed, so the
+ *     caller hands it back with dk_ring_release_tpacket3 and the ring does not stall on it);
+ *   - first block alone holds more than cap frames: returns ENOSPC with *n_blocks = 0 (retry with a larger cap). */
 int dk_ring_scan_tpacket3(const void* ring, uint64_t ring_bytes, uint32_t block_size, uint32_t first_block,
                           uint32_t nblocks, uint32_t* off, uint16_t* len, uint32_t cap, uint32_t* n_frames,
                           uint32_t* n_blocks);
@@ -45,7 +49,8 @@ int dk_ring_release_tpacket3(void* ring, uint64_t ring_bytes, uint32_t block_siz
 
 /* Scan up to nblocks ready blocks and process their frames through the receive engine (dk_rx_process_host pipeline;
  * results are host arrays of at least `cap` entries, in ring order). *n_frames / *n_blocks as dk_ring_scan_tpacket3.
- * Synchronous. Does not release the blocks. */
+ * Synchronous. Does not release the blocks (a malformed first block comes back as EBADMSG with *n_blocks = 1: release
+ * it too). */
 int dk_rx_process_tpacket3(dk_rx_ctx* ctx, const void* ring, uint64_t ring_bytes, uint32_t block_size,
                            uint32_t first_block, uint32_t nblocks, const dk_rx_results* res, uint32_t cap,
                            uint32_t* n_frames, uint32_t* n_blocks);

@@ -28,7 +28,11 @@
  *   - IPv4 addresses are uint32_t whose in-memory bytes are the address octets (s_addr / Ipv4Addr::octets order).
  *     Ports are host-order uint16_t values (the reference's u16 port).
  *   - Not re-entrant per context; one host thread per context (demikernel/bindings.rs:33-35). GPU work is
- *     ordered on the caller's stream.
+ *     ordered on the caller's stream. A context keeps its launch scratch per stream (up to 8 streams; past that the
+ *     least recently used stream's scratch is taken over behind that stream's last launch), so batches issued on
+ *     different streams of one context may run concurrently; counters they share are added atomically.
+ *   - Tuning: the engine's choices (kernel family, grid) follow the batch; overrides are diagnostics (dk_diag.h),
+ *     read from the environment once, when the context is created.
  *   - No torch / HIP types in signatures: streams are passed as void* (a hipStream_t, NULL = default stream).
  */
 #ifndef DK_RX_H
@@ -41,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DK_RX_ABI_VERSION 2u
+#define DK_RX_ABI_VERSION 3u
 
 /* Frames at an address that is a multiple of this take the vectorised path (16-byte aligned frames directly, other
  * even addresses — e.g. NIC buffers with the Ethernet header at 2 mod 16 — through a realigned header window); any
@@ -144,8 +148,11 @@ typedef struct dk_rx_batch {
     uint32_t flags;           /* DK_RX_BATCH_* hints, 0 = none                                         */
 } dk_rx_batch;
 
-/* Per-frame results, struct-of-arrays, one element per frame. Required arrays: meta, src_ip, dst_ip, ports,
- * payload, flow_id. Optional (NULL = not written): tcp_seq, tcp_ack, tcp_win, flow_counts, verdict_counts.
+/* Per-frame results, struct-of-arrays, one element per frame. Required arrays: meta, src_ip, ports, payload, flow_id
+ * (20 bytes per frame). Optional (NULL = not written): dst_ip, tcp_seq, tcp_ack, tcp_win, flow_counts,
+ * verdict_counts. (ABI 3: dst_ip became optional. What a delivered frame goes on to, socket.receive, never sees the
+ * destination address — tcp/peer.rs:254 passes (src_ip, header, payload), udp/peer.rs:167 (remote, payload) — and
+ * it is the configured local address or 255.255.255.255 for every delivered frame, layer3/mod.rs:91-95.)
  *
  *  TCP / UDP (DK_V_OK_*, DK_V_*_NOSOCK):
  *  meta     = verdict | ip_protocol << 8 | tcp byte 13 (CWR..FIN) << 16 | tcp byte 12 (data offset, NS) << 24
@@ -196,6 +203,13 @@ int dk_rx_process(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results*
  * batch/res pointers are host pointers (pinned for full PCIe rate). flow/verdict counts are host arrays too.
  * chunk_frames = frames per pipeline stage (0 = default). Returns 0, EINVAL, ENOMEM or EIO. */
 int dk_rx_process_host(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results* res, uint32_t chunk_frames);
+
+/* Multi-GPU packet shards: sum res->flow_counts[0 .. flow table size) and
+ * res->verdict_counts[0 .. DK_V_COUNT) (device arrays; either may be NULL) over every rank of `nccl_comm` (an
+ * ncclComm_t, e.g. from dk_comm.h), in place, as one grouped ncclAllReduce(ncclUint64, ncclSum) on `stream` — the only
+ * collective of the receive path (RCCL over xGMI; per-frame results stay on their GPU). Every rank must call it with
+ * the same flow table size. Asynchronous. Returns 0, EINVAL or EIO. */
+int dk_rx_flow_counts_allreduce(dk_rx_ctx* ctx, const dk_rx_results* res, void* nccl_comm, void* stream);
 
 /* TX side: compute and store the IPv4 header checksum and the TCP/UDP checksum of every
  * frame in place, as Ipv4Header/TcpHeader/UdpHeader::serialize_and_attach do (ipv4/header.rs:229-266,

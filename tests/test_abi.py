@@ -10,7 +10,7 @@ import pytest
 from demikernel_amd import _native as N
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("dk_rx.h", "dk_diag.h", "dk_ring.h", "dk_tcp.h", "dk_demi.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("dk_rx.h", "dk_diag.h", "dk_ring.h", "dk_tcp.h", "dk_demi.h", "dk_comm.h")]
 
 
 def declared_functions(path):
@@ -31,11 +31,12 @@ def test_every_declared_function_is_exported():
     for h in HEADERS:
         names |= set(declared_functions(h))
     assert {"dk_rx_process", "dk_rx_ctx_create", "dk_tx_checksum", "dk_diag_read_probe", "dk_rx_process_tpacket3",
-            "dk_tcp_rx_process", "dk_rx_into_sgarrays"} <= names
+            "dk_tcp_rx_process", "dk_rx_into_sgarrays", "dk_tcp_into_sgarrays", "dk_rx_flow_counts_allreduce",
+            "dk_comm_init_rank"} <= names
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
     assert names <= exported, names - exported
-    bound = {f[0] for f in N.FUNCTIONS + N.RING_FUNCTIONS + N.TCP_FUNCTIONS + N.DIAG_FUNCTIONS + N.DEMI_FUNCTIONS}
+    bound = {f[0] for f in N.ALL_FUNCTIONS}
     assert bound == names, (names ^ bound)
     for n in names:
         getattr(lib, n)
@@ -81,7 +82,7 @@ def test_tcp_header_constants():
 
 def test_verdict_tables():
     lib = N.load_library()
-    assert lib.dk_rx_abi_version() == 2
+    assert lib.dk_rx_abi_version() == 3
     for i, name in enumerate(N.VERDICTS):
         assert lib.dk_rx_verdict_name(i).decode() == name
     assert lib.dk_rx_verdict_name(N.DK_V_COUNT).decode() == "UNKNOWN"
@@ -135,9 +136,10 @@ def test_demi_sgarray_layout_is_the_reference_abi():
 
 
 def test_into_sgarrays_matches_pop_semantics():
-    """dk_rx_into_sgarrays over the oracle's results of a mixed batch: one array per delivered frame in frame order,
-    one segment over the payload window, sga_buf = token, UDP arrays carry (AF_INET, sport, src_ip) in network order
-    (libos.rs:495-499, pal/mod.rs:154-160), TCP arrays a zero address; ENOSPC past cap. Host-only call."""
+    """dk_rx_into_sgarrays over the oracle's results of a mixed batch: one array per delivered UDP datagram in frame
+    order, one segment over the payload window, sga_buf = token, sga_addr = (AF_INET, sport, src_ip) in network order
+    (libos.rs:495-499, pal/mod.rs:154-160); delivered TCP frames are not pops (dk_tcp_into_sgarrays); ENOSPC past cap.
+    Host-only call."""
     import numpy as np
 
     from demikernel_amd import ipv4, synth
@@ -163,20 +165,17 @@ def test_into_sgarrays_matches_pop_semantics():
                                  pay.ctypes.data, tokens, out, idx.ctypes.data, n, ctypes.byref(nout))
     assert rc == 0
     v = meta & 0xFF
-    deliv = np.nonzero((v == 0) | (v == 1))[0]
-    assert nout.value == len(deliv) > 0 and (v == 1).any() and (v == 0).any()
+    deliv = np.nonzero(v == 1)[0]
+    assert nout.value == len(deliv) > 0 and (v == 0).any()
     assert (idx[: nout.value] == deliv).all()
     for k, i in enumerate(deliv):
         s = out[k]
         assert s.sga_buf == 0x1000 + 16 * i and s.sga_numsegs == 1
         assert s.sga_segs[0].sgaseg_buf == base + int(off32[i]) + int(pay[i] & 0xFFFF)
         assert s.sga_segs[0].sgaseg_len == pay[i] >> 16
-        if v[i] == 1:
-            assert s.sga_addr.sin_family == 2  # AF_INET
-            assert s.sga_addr.sin_port == int.from_bytes(int(ports[i] & 0xFFFF).to_bytes(2, "big"), "little")
-            assert s.sga_addr.sin_addr == src[i]
-        else:
-            assert bytes(s.sga_addr) == bytes(16)
+        assert s.sga_addr.sin_family == 2  # AF_INET
+        assert s.sga_addr.sin_port == int.from_bytes(int(ports[i] & 0xFFFF).to_bytes(2, "big"), "little")
+        assert s.sga_addr.sin_addr == src[i]
     # the delivered payload is what the frame carries after the strip (bytes S + hlen .. E)
     i = deliv[0]
     o, p = int(off32[i]), int(pay[i])
@@ -188,3 +187,60 @@ def test_into_sgarrays_matches_pop_semantics():
     assert lib.dk_rx_into_sgarrays(None, None, 0, None, None, None, None, None, None, None, 0, ctypes.byref(nout)) == 0
     assert lib.dk_rx_into_sgarrays(None, off32.ctypes.data, n, meta.ctypes.data, src.ctypes.data, ports.ctypes.data,
                                    pay.ctypes.data, None, out, None, n, ctypes.byref(nout)) == 22
+
+
+def test_tcp_into_sgarrays_are_the_receive_queue():
+    """dk_tcp_into_sgarrays over the oracle's dk_tcp results of a reordered stream with duplicates, strays and FINs
+    (the GPU's are bit-exact to these, tests/test_gpu_tcp.py): per connection, one array per pushed buffer in queue
+    order over exactly that buffer's bytes, zero address; FIN's EOF buffer is an empty segment; retransmitted and
+    out-of-window bytes never appear (the delivered bytes add up to RCV.NXT's advance). Host-only call."""
+    import numpy as np
+
+    from demikernel_amd import ipv4, synth
+    from oracle import oracle as O
+    from oracle.oracle import OraclePeer
+
+    lib = N.load_library()
+    flows, tr, table = synth.tcp_streams(4000, 5, buffer_size=1 << 22, seed=77)
+    blob, off, lens = synth.build_numpy(tr)
+    peer = OraclePeer(ipv4(synth.BOB_IPV4))
+    peer.set_flows(flows)
+    rx = peer.process(blob, off, lens)
+    t0 = table.copy()
+    out = O.tcp_process(table, rx)
+    n = len(off)
+    off32 = np.ascontiguousarray(off, np.uint32)
+    base = blob.ctypes.data
+    arrs = (N.DemiSgarray * (n + 64))()
+    nout = ctypes.c_uint32()
+    dupes = 0
+    for c in range(len(table)):
+        if t0["state"][c] != N.DK_TCP_ESTABLISHED:
+            continue
+        a, k = int(out["deliv_start"][c]), int(out["deliv_count"][c])
+        dv = np.ascontiguousarray(out["deliv"][a:a + k])
+        rc = lib.dk_tcp_into_sgarrays(base, off32.ctypes.data, n, dv.ctypes.data, k, None, arrs, n + 64,
+                                      ctypes.byref(nout))
+        assert rc == 0 and nout.value == k
+        total = 0
+        for j in range(k):
+            s, v = arrs[j], dv[j]
+            assert s.sga_numsegs == 1 and bytes(s.sga_addr) == bytes(16)
+            if v["ref"] == N.DK_TCP_REF_EOF:
+                assert s.sga_buf is None and s.sga_segs[0].sgaseg_len == 0
+                continue
+            assert s.sga_buf == base + int(off32[v["ref"]])
+            assert s.sga_segs[0].sgaseg_buf == base + int(off32[v["ref"]]) + int(v["off"])
+            assert s.sga_segs[0].sgaseg_len == v["len"]
+            total += int(v["len"])
+        fin = int(np.any(dv["ref"] == N.DK_TCP_REF_EOF))
+        assert (int(table["receive_next"][c]) - int(t0["receive_next"][c])) % 2**32 == total + fin, c
+        dupes += int(((out["action"] == N.A["DUPLICATE"]) & (rx["flow_id"] == c)).sum())
+    assert dupes > 0  # the stream had retransmissions, and none of their bytes were handed out
+    # errors: a ref outside the batch, capacity
+    dv = np.zeros(2, N.VIEW_DTYPE)
+    dv["ref"] = [0, n]
+    assert lib.dk_tcp_into_sgarrays(base, off32.ctypes.data, n, dv.ctypes.data, 2, None, arrs, 4, ctypes.byref(nout)) == 22
+    dv["ref"] = [0, 1]
+    assert lib.dk_tcp_into_sgarrays(base, off32.ctypes.data, n, dv.ctypes.data, 2, None, arrs, 1, ctypes.byref(nout)) == 28
+    assert nout.value == 1

@@ -23,7 +23,7 @@ def torch_cuda():
     return torch
 
 
-def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None, aligned16=None):
+def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None, aligned16=None, dst_ip=True):
     import torch
 
     eng = RxEngine(cfg or Config(LOCAL), device=0)
@@ -33,7 +33,7 @@ def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None
         b.aligned16 = aligned16
     if frames_bytes is not None:
         b.frames_bytes = frames_bytes
-    r = eng.results(len(off), tcp_fields=tcp_fields)
+    r = eng.results(len(off), tcp_fields=tcp_fields, dst_ip=dst_ip)
     eng.receive_batch(b, r)
     torch.cuda.synchronize()
     out = r.to_numpy()
@@ -60,8 +60,8 @@ def assert_same(got, exp, ctx=""):
             raise AssertionError(f"{ctx}: '{k}' differs at {bad}: got {v[bad]} exp {e[bad]}{extra}")
 
 
-def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None):
-    got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes, aligned16=aligned16)
+def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None, dst_ip=True):
+    got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes, aligned16=aligned16, dst_ip=dst_ip)
     exp = run_oracle(blob, off, lens, flows, cfg, frames_bytes=frames_bytes)
     assert_same(got, exp, ctx)
     return got
@@ -108,7 +108,7 @@ def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
     """Every kernel family (results stored per chunk / staged in registers / split stream+finish waves / small-frame
     kernel, whose frames past the 64-byte window are summed wave-wide) under every wave schedule, with grids small
     enough that each wave walks many chunks (staged results flushed mid-loop and at exit) and with the default grid.
-    The split kernel always walks sched 0."""
+    The split kernel always walks sched 0. Under sched 1 every family writes the 20-byte layout (no dst_ip, ABI 3)."""
     monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
     monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
     monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
@@ -121,7 +121,8 @@ def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.05, tr))
     perm = np.random.default_rng(8).permutation(n)
-    check(blob, off[perm], lens[perm], flows, ctx=f"{family} sched={sched} grid={grid}")
+    got = check(blob, off[perm], lens[perm], flows, ctx=f"{family} sched={sched} grid={grid}", dst_ip=sched != "1")
+    assert ("dst_ip" in got) == (sched != "1")
 
 
 def test_misaligned_and_offsets(torch_cuda):
@@ -259,9 +260,19 @@ def tx_check(blob, off, lens, ctx=""):
     assert bad.size == 0, f"{ctx}: {bad.size} bytes differ, first at blob offset {bad[:8]}"
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_tx_checksum_matches_oracle(torch_cuda, monkeypatch, split):
-    monkeypatch.setenv("DK_TX_SPLIT", split)  # both TX kernels (the split one is chosen for >= 1 KiB per frame)
+@pytest.fixture
+def tx_split(request):
+    """Force one TX kernel for the test (dk_diag_tx_set_tuning), back to the engine's rule afterwards."""
+    from demikernel_amd import tx_tuning
+
+    tx_tuning(split=int(request.param))
+    yield request.param
+    tx_tuning()
+
+
+@pytest.mark.parametrize("tx_split", ["0", "1"], indirect=True)
+def test_tx_checksum_matches_oracle(torch_cuda, tx_split):
+    # both TX kernels (the split one is chosen for >= 1 KiB per frame)
     flows = synth.make_flows(64)
     n = 5000
     tr = synth.traffic(n, np.random.default_rng(8).integers(28, 3000, n).astype(np.uint16), flows)
@@ -271,11 +282,10 @@ def test_tx_checksum_matches_oracle(torch_cuda, monkeypatch, split):
     tx_check(blob2, off2, lens2, "random lengths")
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_tx_checksum_malformed_and_options(torch_cuda, monkeypatch, split):
+@pytest.mark.parametrize("tx_split", ["0", "1"], indirect=True)
+def test_tx_checksum_malformed_and_options(torch_cuda, tx_split):
     """Every corpus / fuzz / option frame (non-IPv4, bad lengths, bad data offsets, IHL > 5, short UDP): the TX fill
     touches exactly what serialize_and_attach's restatement touches, at every alignment class, in both TX kernels."""
-    monkeypatch.setenv("DK_TX_SPLIT", split)
     rng = np.random.default_rng(77)
     base = [c[1] for c in F.verdict_corpus()]
     pl = bytes(range(200))
@@ -365,32 +375,161 @@ def test_tpacket3_ring_path_matches_oracle(torch_cuda):
         eng.close()
 
 
-def test_full_size_c2_properties(torch_cuda):
-    """BASELINE config 2 at full size (1M x 1500 B, device-generated): every valid frame is delivered to its flow,
-    counters add up, and a 20k-frame sample is bit-exact against the oracle."""
+def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, sample=20000):
+    """A device-generated batch at a BASELINE config's full size with a `corrupt` tail (synth.corruption_plan): every
+    intact frame is delivered to its own flow, every corrupted frame gets the oracle's verdict and fields, a random
+    sample is bit-exact against the oracle on every field, and both counter arrays are exactly the histograms of the
+    results. Returns (engine, batch, traffic, results as numpy, host copy of the blob)."""
     import torch
 
-    flows = synth.make_flows(1024)
-    n = 1 << 20
-    tr = synth.traffic(n, 1486, flows)
+    tr = synth.traffic(n, ip_len, flows, seed=seed)
     eng = RxEngine(Config(LOCAL))
     eng.set_sockets(flows)
-    batch = synth.build_device(tr, eng)
-    r = eng.results(n)
+    batch = synth.build_device(tr, eng, seed=seed)
+    off = np.asarray(batch.off.cpu().numpy().view(np.uint32))
+    lens = np.asarray(batch.len.cpu().numpy().view(np.uint16))
+    plan = synth.corruption_plan(n, corrupt, tr, seed)
+    synth.corrupt_device(batch, off, plan)
+    r = eng.results(n, tcp_fields=True)
     eng.receive_batch(batch, r)
     torch.cuda.synchronize()
     got = r.to_numpy()
-    assert (got["meta"] & 0xFF == V["OK_TCP"]).all()
-    assert np.array_equal(got["flow_id"], tr.flow.astype(np.uint32))
-    assert int(got["verdict_counts"].sum()) == n
-    assert np.array_equal(got["flow_counts"], np.bincount(tr.flow, minlength=len(flows)).astype(np.uint64))
-    sample = np.random.default_rng(0).choice(n, 20000, replace=False)
-    off = np.asarray(batch.off.cpu().numpy().view(np.uint32))
-    lens = np.asarray(batch.len.cpu().numpy().view(np.uint16))
     blob = batch.blob.cpu().numpy()
-    exp = run_oracle(blob, off[sample], lens[sample], flows)
-    for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id"):
-        assert np.array_equal(got[k][sample], exp[k]), k
+    bad = np.array(sorted({i for i, _, _ in plan}), np.int64)
+    good = np.ones(n, bool)
+    good[bad] = False
+    v = got["meta"] & 0xFF
+    assert np.array_equal(v[good], np.where(tr.proto[good] == 6, V["OK_TCP"], V["OK_UDP"]).astype(np.uint32))
+    assert np.array_equal(got["flow_id"][good], tr.flow[good].astype(np.uint32))
+    for idx, what in ((bad, "corrupted"), (np.random.default_rng(seed).choice(n, sample, replace=False), "sample")):
+        exp = run_oracle(blob, off[idx], lens[idx], flows)
+        for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win"):
+            assert np.array_equal(got[k][idx], exp[k]), (what, k)
+    assert (v[bad] > 1).mean() > 0.8  # the corruptions really are rejected
+    assert np.array_equal(got["verdict_counts"], np.bincount(v, minlength=len(VERDICTS)).astype(np.uint64))
+    deliv = v <= 1
+    assert np.array_equal(got["flow_counts"],
+                          np.bincount(got["flow_id"][deliv], minlength=len(flows)).astype(np.uint64))
+    return eng, batch, tr, got, blob
+
+
+def test_full_size_c2_properties(torch_cuda):
+    """BASELINE config 2 at full size (1M x 1500 B TCP, 1,024 flows) with the 1 % corrupted tail the bench times."""
+    full_size(1 << 20, 1486, synth.make_flows(1024))
+
+
+def test_full_size_c3_properties(torch_cuda):
+    """BASELINE config 3 at full size (1M x 64 B UDP, the small-frame kernel) with a 1 % corrupted tail."""
+    full_size(1 << 20, 50, synth.make_flows(1024, kind="udp"), seed=synth.SEED + 1)
+
+
+def test_full_size_c4_imix_shard(torch_cuda):
+    """BASELINE config 4's per-GPU shard (2M IMIX frames, 40/576/1500 B at 7:4:1) with a 1 % corrupted tail."""
+    n = 1 << 21
+    full_size(n, synth.imix_ip_lengths(n, seed=5), synth.make_flows(1024), seed=5)
+
+
+def test_c5_host_pipeline_10k_flows(torch_cuda):
+    """BASELINE config 5's per-GPU shard end to end: 2M x 1500 B TCP over 10,000 Active flows plus a Passive listener,
+    1 % corrupted, from pinned host memory through dk_rx_process_host (chunked H2D, kernel, D2H on 3 streams): every
+    result word and both counter arrays equal the HBM-resident call's (itself checked by full_size against the
+    oracle: intact frames, every corrupted frame and a 20k sample), frames of the Passive listener included."""
+    import torch
+
+    from demikernel_amd import RxResults
+
+    n = 1 << 21
+    flows = synth.make_flows(10000)
+    eng, batch, tr, got, _ = full_size(n, 1486, flows, seed=55)
+    assert (got["flow_counts"][:10000] > 0).all()
+    pinned = torch.empty(batch.blob.numel(), dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(batch.blob)
+    off = np.ascontiguousarray(batch.off.cpu().numpy().view(np.uint32))
+    lens = np.ascontiguousarray(batch.len.cpu().numpy().view(np.uint16))
+    del batch
+    rh = RxResults(n, len(flows), tcp_fields=True, host=True)
+    eng.receive_batch_host(pinned.numpy(), off, lens, rh)
+    h = rh.to_numpy()
+    for k, v in got.items():
+        assert np.array_equal(h[k], v), k
+    # a frame for the Passive listener (no Active entry: demuxes to Passive(local), tcp/peer.rs:241-251)
+    lis = FrameBatch.from_numpy(*F.pack([F.tcp_frame(b"syn", sport=4242, src="10.9.9.9", dport=synth.LOCAL_PORT)]))
+    rl = eng.results(1)
+    eng.receive_batch(lis, rl)
+    torch.cuda.synchronize()
+    assert int(rl.to_numpy()["flow_id"][0]) == 10000
+
+
+def test_two_streams_one_context(torch_cuda):
+    """One context, batches issued alternately on two streams (and then over more streams than the context keeps
+    scratch for): per-frame results equal the oracle's and the shared counters add up exactly."""
+    import torch
+
+    flows = np.concatenate([synth.make_flows(700), synth.make_flows(40, kind="udp")])
+    mk = []
+    for k, (nn, ip) in enumerate(((20000, 1486), (30000, "imix"), (25000, 50))):
+        tr = synth.traffic(nn, synth.imix_ip_lengths(nn, seed=k) if ip == "imix" else ip, flows, seed=30 + k)
+        blob, off, lens = synth.build_numpy(tr)
+        synth.corrupt_numpy(blob, off, synth.corruption_plan(nn, 0.03, tr, seed=k))
+        mk.append((blob, off, lens))
+    exps = [run_oracle(*m, flows) for m in mk]
+    eng = RxEngine(Config(LOCAL))
+    eng.set_sockets(flows)
+    batches = [FrameBatch.from_numpy(*m) for m in mk]
+    res = [eng.results(b.n, tcp_fields=True) for b in batches]
+    for r in res[1:]:  # one set of counters shared by every launch
+        r.t["flow_counts"], r.t["verdict_counts"] = res[0].t["flow_counts"], res[0].t["verdict_counts"]
+    streams = [torch.cuda.Stream() for _ in range(12)]
+    reps = 6
+    for it in range(reps):  # two streams, interleaved
+        for j, b in enumerate(batches):
+            eng.receive_batch(b, res[j], stream=streams[(it + j) % 2])
+    for it, s in enumerate(streams):  # 12 streams: more than the context's 8 scratch slots
+        for j, b in enumerate(batches):
+            eng.receive_batch(b, res[j], stream=streams[(it + 3 * j) % len(streams)])
+    torch.cuda.synchronize()
+    total = reps + len(streams)
+    for j, (r, e) in enumerate(zip(res, exps)):
+        got = r.to_numpy()
+        for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win"):
+            assert np.array_equal(got[k], e[k]), (j, k)
+    got = res[0].to_numpy()
+    assert np.array_equal(got["verdict_counts"], total * sum(e["verdict_counts"] for e in exps))
+    assert np.array_equal(got["flow_counts"], total * sum(e["flow_counts"][: len(flows)] for e in exps))
+
+
+def test_counts_allreduce_one_rank(torch_cuda):
+    """dk_rx_flow_counts_allreduce through a 1-rank RCCL communicator (ncclCommInitAll over device 0): the counters
+    come back unchanged (the sum over one rank), per-frame results untouched."""
+    import torch
+
+    from demikernel_amd import Comm
+
+    c2 = Comm.init_rank(1, Comm.unique_id(), 0, 0)  # the bench's bootstrap (dk_comm_unique_id + dk_comm_init_rank)
+    assert c2.count() == 1
+    c2.destroy()
+    comm = Comm.init_all([0])[0]
+    try:
+        assert comm.count() == 1
+        flows = synth.make_flows(3000)
+        tr = synth.traffic(40000, synth.imix_ip_lengths(40000), flows, seed=8)
+        blob, off, lens = synth.build_numpy(tr)
+        synth.corrupt_numpy(blob, off, synth.corruption_plan(40000, 0.02, tr))
+        eng = RxEngine(Config(LOCAL))
+        eng.set_sockets(flows)
+        r = eng.results(len(off))
+        eng.receive_batch(FrameBatch.from_numpy(blob, off, lens), r)
+        torch.cuda.synchronize()
+        before = r.to_numpy()
+        eng.counts_allreduce(r, comm.handle)
+        torch.cuda.synchronize()
+        after = r.to_numpy()
+        for k in before:
+            assert np.array_equal(before[k], after[k]), k
+        exp = run_oracle(blob, off, lens, flows)
+        assert np.array_equal(after["flow_counts"], exp["flow_counts"][: len(flows)])
+    finally:
+        comm.destroy()
 
 
 @pytest.mark.parametrize("name", ["verdict_corpus", "mixed_batch"])

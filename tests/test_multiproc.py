@@ -36,11 +36,14 @@ def _worker(rank, world, port, out_path):
     import torch
     import torch.distributed as dist
 
-    from demikernel_amd.shard import allreduce_counts
+    from demikernel_amd.shard import allreduce_counts, broadcast_comm_id
     from oracle.oracle import OraclePeer
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    # the RCCL bootstrap id travels the way bench.py hands it out (rank 0 makes it; a stand-in id here: no GPU)
+    uid = broadcast_comm_id(dist, lambda: bytes(range(128)))
+    assert uid == bytes(range(128))
     flows = np.concatenate([synth.make_flows(200), synth.make_flows(20, kind="udp")])
     n = 6000
     tr = synth.traffic(n, synth.imix_ip_lengths(n), flows, seed=3)

@@ -91,3 +91,23 @@ def test_malformed_blocks_rejected():
     with pytest.raises(Fail) as e:
         RG.TpacketRing(ring, bs, register=False).scan(used + 100, 1, 10)  # first block outside the ring
     assert e.value.errno == EINVAL
+
+
+def test_malformed_later_block_returns_good_prefix_then_is_consumed():
+    """A malformed block after good ones: the good prefix comes back (rc 0) and is consumed; the next scan starting at
+    the bad block reports EBADMSG with that block counted as consumed, so releasing it unblocks the ring."""
+    blob, off, lens = frames(2000)
+    bs = 1 << 16
+    ring, used, eoff, _ = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+    assert used >= 4
+    first_pkt = bs + RG.BLOCK_DESC_BYTES  # first packet of block 1
+    ring[first_pkt:first_pkt + 4] = 0     # tp_next_offset 0 on a packet that is not the block's last
+    r = RG.TpacketRing(ring, bs, register=False)
+    o, _, nb = r.scan(0, used, len(off))
+    assert nb == 1 and np.array_equal(o, eoff[eoff // bs == 0])
+    with pytest.raises(Fail) as e:
+        r.scan(1, used - 1, len(off))
+    assert e.value.errno == EBADMSG and e.value.blocks == 1
+    r.release(1, 1)
+    o3, _, nb3 = r.scan(2, used - 2, len(off))
+    assert nb3 == used - 2 and np.array_equal(o3, eoff[eoff // bs >= 2])

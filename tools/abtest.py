@@ -30,6 +30,7 @@ def main():
 
     import bench
     from demikernel_amd import Config, RxEngine, synth
+    from demikernel_amd import _native as N
 
     base = RxEngine(Config(synth.BOB_IPV4))
     batch, flows, tr = bench.make_batch(base, args.workload, 0, synth.SEED, 1)
@@ -49,12 +50,22 @@ def main():
     for rep in range(args.reps):
         for g, cf in [(g, cf) for g in grids for cf in configs]:
             sc, kv = cf
-            os.environ["DK_RX_GRID_PER_CU"] = str(g)
+            if g > 0:  # builds that read the knobs per launch (round 1); 0 = the engine's own grid rule
+                os.environ["DK_RX_GRID_PER_CU"] = str(g)
+            else:
+                os.environ.pop("DK_RX_GRID_PER_CU", None)
             if sc is not None:
                 os.environ["DK_RX_SCHED"] = sc
             if kv is not None:
                 os.environ[kname] = kv
+            knobs = {"grid_per_cu": g if g > 0 else -1}
+            if sc is not None:
+                knobs["sched"] = int(sc)
+            if kv is not None and kname.startswith("DK_RX_") and kname[6:].lower() in N.DK_DIAG_RX_KNOBS:
+                knobs[kname[6:].lower()] = int(kv)
             for k, (e, r) in engines.items():
+                if hasattr(e.lib, "dk_diag_rx_set_tuning"):  # later builds read them once per context
+                    e.set_tuning(**knobs)
                 run = (lambda: e.tx_checksum(batch)) if args.tx else (lambda: e.receive_batch(batch, r))  # noqa: E731
                 run()
                 ev0.record()
