@@ -53,7 +53,21 @@ class DkRxBatch(ctypes.Structure):
 
 
 RESULT_FIELDS = ["meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win",
-                 "flow_counts", "verdict_counts"]
+                 "flow_counts", "verdict_counts", "tcp_opts"]
+
+# numpy mirror of struct dk_tcp_opts (96 bytes): the parsed [TcpOptions2; 5] list of one segment.
+TCP_OPT_DTYPE = np.dtype([("kind", "u1"), ("u8", "u1"), ("u16", "<u2"), ("v0", "<u4"), ("v1", "<u4")])
+TCP_OPTS_DTYPE = np.dtype([("num", "<u4"), ("opt", TCP_OPT_DTYPE, (5,)), ("sack", "<u4", (4, 2))])
+assert TCP_OPT_DTYPE.itemsize == 12 and TCP_OPTS_DTYPE.itemsize == 96
+DK_TCPOPT_MSS, DK_TCPOPT_WS, DK_TCPOPT_SACK_OK, DK_TCPOPT_SACK, DK_TCPOPT_TS = 2, 3, 4, 5, 8
+
+
+class DkTcpOpt(ctypes.Structure):
+    _fields_ = [("kind", c_uint8), ("u8", c_uint8), ("u16", c_uint16), ("v0", c_uint32), ("v1", c_uint32)]
+
+
+class DkTcpOpts(ctypes.Structure):
+    _fields_ = [("num", c_uint32), ("opt", DkTcpOpt * 5), ("sack", (c_uint32 * 2) * 4)]
 
 
 class DkRxResults(ctypes.Structure):

@@ -146,11 +146,41 @@ __global__ __launch_bounds__(kBlock) void read_probe_frames(const uint4* __restr
     if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
 }
 
+// modes 9-11: the small-frame (64-byte slot) access pattern, buffer loads (nt), grid-strided 4 KiB wave chunks:
+// 9: lane l reads the 4 granules of slot l (lane stride 64 B), one chunk (4 loads per lane) in flight per wave step;
+// 10: as 9 with 4 chunks (16 loads per lane) in flight; 11: one chunk read lane-contiguously (1 KiB per load).
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void read_probe_small(const uint4* __restrict__ p, uint64_t n16, uint32_t* out) {
+    constexpr int C = kMode == 10 ? 4 : 1;  // chunks per wave step
+    uint32_t acc = 0;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t piece = 256 * C;  // granules per wave step
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0xFFFFFFFF, 0x00020000);
+    for (uint64_t base = w * piece; base < n16; base += nwaves * piece) {
+        uint4 v[4 * C];
+#pragma unroll
+        for (int c = 0; c < C; c++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint64_t g = kMode == 11 ? base + 64 * k + lane : base + 256 * c + 4 * lane + k;
+                const uint64_t i = min(g, n16 - 1);
+                const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 2);
+                v[4 * c + k] = make_uint4(r[0], r[1], r[2], r[3]);
+            }
+#pragma unroll
+        for (int u = 0; u < 4 * C; u++) acc ^= v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    acc = __reduce_add_sync(~0ull, acc);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
+}
+
 }  // namespace
 
 extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode,
                                   void* stream) {
-    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 8) return 22;
+    if (!buf || !scratch || grid == 0 || mode < 0 || mode > 11) return 22;
     if (mode >= 6 && bytes > 0xFFFFFFFFull) return 22;  // buffer offsets are 32-bit
     const uint4* p = (const uint4*)buf;
     const hipStream_t s = (hipStream_t)stream;
@@ -163,5 +193,8 @@ extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scr
     if (mode == 6) hipLaunchKernelGGL(read_probe16<6>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 7) hipLaunchKernelGGL(read_probe16<7>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     if (mode == 8) hipLaunchKernelGGL(read_probe_frames, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 9) hipLaunchKernelGGL(read_probe_small<9>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 10) hipLaunchKernelGGL(read_probe_small<10>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
+    if (mode == 11) hipLaunchKernelGGL(read_probe_small<11>, dim3(grid), dim3(kBlock), 0, s, p, bytes / 16, scratch);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

@@ -112,5 +112,6 @@ constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFa
 }
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
+uint32_t dk_rx_small_block_waves();  // waves per workgroup of the small-frame kernel
 int dk_tx_resident_blocks();  // occupancy of dk_tx_kernel per CU (0 on error)
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream);

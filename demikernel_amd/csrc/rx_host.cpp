@@ -16,6 +16,8 @@
 
 #include "rx_common.h"
 
+static_assert(sizeof(dk_tcp_opt) == 12 && sizeof(dk_tcp_opts) == 96, "dk_rx.h tcp option record layout");
+
 namespace {
 
 constexpr int kPipeStreams = 3;
@@ -50,6 +52,8 @@ struct Stage {  // device staging for one pipeline stream
     uint16_t* desc_len = nullptr;
     uint32_t* res = nullptr;  // 9 result arrays of chunk_cap entries
     uint32_t cap = 0;
+    dk_tcp_opts* opts = nullptr;  // tcp_opts records of chunk_cap entries (allocated when a call asks for them)
+    uint32_t opts_cap = 0;
 };
 
 // Tuning overrides (-1 = the host rule). Read once from the environment at dk_rx_ctx_create (DK_RX_STAGE, DK_RX_SPLIT,
@@ -236,7 +240,9 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     }
     uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u);
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
-    uint32_t grid = std::min(ntiles, per_cu * c->cu_count);
+    // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
+    const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
+    uint32_t grid = std::min((ntiles + tiles_per_wg - 1) / tiles_per_wg, per_cu * c->cu_count);
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
@@ -254,9 +260,9 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     }
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
-                        "small=%u\n",
+                        "small=%u fused=%u\n",
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
-                p.small);
+                p.small, p.fused);
     rc = dk_launch_rx(p, grid, stream);
 #if DK_SLOT_EVENTS
     if (rc == 0 && hipEventRecord(slot->last, stream) != hipSuccess) rc = EIO;
@@ -265,6 +271,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
 }
 
 void free_stage(Stage& s) {
+    if (s.opts) (void)hipFree(s.opts);
     if (s.frames) (void)hipFree(s.frames);
     if (s.desc_off) (void)hipFree(s.desc_off);
     if (s.desc_len) (void)hipFree(s.desc_len);
@@ -273,8 +280,15 @@ void free_stage(Stage& s) {
     s = Stage{};
 }
 
-int ensure_stage(Stage& s, uint32_t cap, uint64_t bytes) {
+int ensure_stage(Stage& s, uint32_t cap, uint64_t bytes, bool opts) {
     if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return EIO;
+    if (opts && s.opts_cap < cap) {
+        if (s.opts) (void)hipFree(s.opts);
+        s.opts = nullptr;
+        s.opts_cap = 0;
+        if (hipMalloc(&s.opts, (size_t)cap * sizeof(dk_tcp_opts)) != hipSuccess) return ENOMEM;
+        s.opts_cap = cap;
+    }
     if (s.cap < cap) {
         if (s.desc_off) (void)hipFree(s.desc_off);
         if (s.desc_len) (void)hipFree(s.desc_len);
@@ -459,7 +473,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
     uint32_t cap = 0;
     for (auto& ch : chunks) cap = std::max(cap, ch.e - ch.a);
     for (Stage& s : c->stages) {
-        int rc = ensure_stage(s, cap, std::max<uint64_t>(max_bytes, 16));
+        int rc = ensure_stage(s, cap, std::max<uint64_t>(max_bytes, 16), r->tcp_opts != nullptr);
         if (rc) return rc;
     }
     const uint32_t nfl = std::max(c->nflows, 1u);
@@ -512,6 +526,11 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         p.res.tcp_seq = r->tcp_seq ? R + 6 * (size_t)st.cap : nullptr;
         p.res.tcp_ack = r->tcp_ack ? R + 7 * (size_t)st.cap : nullptr;
         p.res.tcp_win = r->tcp_win ? R + 8 * (size_t)st.cap : nullptr;
+        p.res.tcp_opts = r->tcp_opts ? st.opts : nullptr;
+        if (r->tcp_opts && hipMemsetAsync(st.opts, 0, (size_t)m * sizeof(dk_tcp_opts), st.stream) != hipSuccess) {
+            rc = EIO;
+            break;
+        }
         p.res.flow_counts = r->flow_counts ? c->d_flow_counts : nullptr;
         p.res.verdict_counts = r->verdict_counts ? c->d_verdict_counts : nullptr;
         rc = launch_batch(c, p, ch.hi - ch.lo, st.stream);
@@ -526,6 +545,10 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
                 break;
             }
         }
+        if (rc == 0 && r->tcp_opts &&
+            hipMemcpyAsync(r->tcp_opts + ch.a, st.opts, m * sizeof(dk_tcp_opts), hipMemcpyDeviceToHost, st.stream) !=
+                hipSuccess)
+            rc = EIO;
     }
     for (Stage& s : c->stages)
         if (s.stream && hipStreamSynchronize(s.stream) != hipSuccess) rc = rc ? rc : EIO;

@@ -298,17 +298,25 @@ __device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const 
 }
 
 // TCP option walk (tcp/header.rs:215-302), over the option bytes in global memory. Returns 0 (ok), DK_V_TCP_OPT
-// (EBADMSG) or DK_V_TCP_OPT_EIO (truncated read: std::io::Cursor::read_exact -> io::Error -> EIO).
-__device__ __noinline__ uint32_t tcp_options(const uint8_t* o, uint32_t n) {
-    uint32_t pos = 0, nopt = 0;
+// (EBADMSG) or DK_V_TCP_OPT_EIO (truncated read: std::io::Cursor::read_exact -> io::Error -> EIO). With `out`, the
+// parsed list (the reference's [TcpOptions2; 5]) is written there when the walk succeeds.
+__device__ __forceinline__ uint32_t opt_be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+__device__ __noinline__ uint32_t tcp_options(const uint8_t* o, uint32_t n, dk_tcp_opts* out) {
+    dk_tcp_opts r;
+    uint32_t* rw = reinterpret_cast<uint32_t*>(&r);
+    for (int k = 0; k < 24; k++) rw[k] = 0;
+    uint32_t pos = 0, nopt = 0, nsack = 0;
     while (pos < n) {
         const uint32_t kind = o[pos++];
         if (kind == 0) break;
         if (kind == 1) continue;
-        uint32_t body;
+        dk_tcp_opt e{(uint8_t)kind, 0, 0, 0, 0};
         if (kind == 2 || kind == 3 || kind == 4 || kind == 5 || kind == 8) {
             if (pos >= n) return DK_V_TCP_OPT_EIO;
             const uint32_t l = o[pos++];
+            uint32_t body;
             if (kind == 2) { if (l != 4) return DK_V_TCP_OPT; body = 2; }
             else if (kind == 3) { if (l != 3) return DK_V_TCP_OPT; body = 1; }
             else if (kind == 4) { if (l != 2) return DK_V_TCP_OPT; body = 0; }
@@ -317,12 +325,31 @@ __device__ __noinline__ uint32_t tcp_options(const uint8_t* o, uint32_t n) {
                 body = l - 2;  // num_sacks * 8, read in 4-byte pieces
             } else { if (l != 10) return DK_V_TCP_OPT; body = 8; }
             if (n - pos < body) return DK_V_TCP_OPT_EIO;
+            const uint8_t* b = o + pos;
+            if (kind == 2) e.u16 = (uint16_t)((b[0] << 8) | b[1]);
+            else if (kind == 3) e.u8 = b[0];
+            else if (kind == 8) { e.v0 = opt_be32(b); e.v1 = opt_be32(b + 4); }
+            else if (kind == 5) {
+                const uint32_t ns = body / 8;
+                e.u8 = (uint8_t)ns;
+                e.u16 = (uint16_t)nsack;
+                for (uint32_t k = 0; k < ns && nsack < 4; k++, nsack++) {
+                    r.sack[nsack][0] = opt_be32(b + 8 * k);
+                    r.sack[nsack][1] = opt_be32(b + 8 * k + 4);
+                }
+            }
             pos += body;
         } else {
             return DK_V_TCP_OPT;
         }
         if (nopt >= 5) return DK_V_TCP_OPT;  // "too many TCP options provided"
+        r.opt[nopt] = e;
         nopt++;
+    }
+    if (out) {
+        r.num = nopt;
+        uint32_t* ow = reinterpret_cast<uint32_t*>(out);
+        for (int k = 0; k < 24; k++) ow[k] = rw[k];
     }
     return 0;
 }
@@ -455,13 +482,15 @@ struct FrameDesc {
     }
 };
 
-// Phase A, small frames (<= 64 bytes from the granule base): straight into the register window.
+// Phase A, small frames (<= 64 bytes from the granule base): straight into the register window. Granules the frame
+// does not reach (and every granule of other frames) load at kOob, i.e. zeros from the buffer range check: no branch
+// around a load (an exec-masked load per granule made the compiler drain vmcnt after each frame's first load).
 template <bool kShift>
 __device__ __forceinline__ void small_load(const FrameDesc<kShift>& F, const Blob& B, uint32_t off, RegAcc& R) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        uint4 q = make_uint4(0, 0, 0, 0);
-        if (F.vec && !F.big && (uint32_t)(16 * k) < F.span) q = B.template ld<false>(off - F.sh + 16 * k);
+        const bool use = F.vec && !F.big && (uint32_t)(16 * k) < F.span;
+        const uint4 q = B.template ld<false>(use ? off - F.sh + 16 * k : kOob);
         R.w[4 * k + 0] = q.x;
         R.w[4 * k + 1] = q.y;
         R.w[4 * k + 2] = q.z;
@@ -751,7 +780,8 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
             if (c != L.stored) L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
         }
         if (L.v == kPendTcp && L.hlen > 20) {
-            const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20);
+            const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20,
+                                           kOpt && live && P.res.tcp_opts ? P.res.tcp_opts + i : nullptr);
             if (e) L.v = e;
         }
         const uint32_t dport = L.ports >> 16;
@@ -849,9 +879,10 @@ struct WaveRange {
         return c < f1;
     }
 };
+template <uint32_t kW = kWaves>  // waves per workgroup
 __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint32_t wv, uint32_t lane) {
     WaveRange r;
-    const uint32_t nw = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
+    const uint32_t nw = gridDim.x * kW, gw = blockIdx.x * kW + wv;
     r.lane_off = lane;
     r.tail = false;
     r.nfull = r.t0 = r.t1 = 0;
@@ -1077,19 +1108,84 @@ void dk_rx_kernel(RxParams P) {
 
 // Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
 // probe -> stores is latency-bound at 64 bytes a frame, so this kernel drops the quarter-wave streaming machinery
-// (its 48 load registers and 27 KB of LDS per workgroup) for more resident waves, and loads the next chunk's frame
-// registers (descriptors two chunks ahead) while the current chunk is parsed. The rare frame whose span exceeds the
-// 64-byte register window is summed by the whole wave, one frame at a time, and hands the owner lane exactly what
-// stream_chunk would (header window, whole-granule sum, last granule in LDS), so phase C is shared code.
+// (its 48 load registers and 27 KB of LDS per workgroup) for more resident waves; descriptors are loaded two chunks
+// ahead. The rare frame whose span exceeds the 64-byte register window is summed by the whole wave, one frame at a
+// time, and hands the owner lane exactly what stream_chunk would (header window, whole-granule sum, last granule in
+// LDS), so phase C is shared code. Measured and not kept: the next chunk's window or registers in
+// flight during this chunk (no gain at 5 waves/SIMD, spills at 6), one generation of waves each taking 2-8 chunks
+// at once (+35-120 %: every wave then loads, computes and stores in lockstep).
+// Packed small frames are read as one contiguous window per chunk. Each lane reading its own 64-byte frame (4
+// dwordx4 loads at a 64-byte lane stride, every load touching 32 lines) caps at ~3.8 TB/s on gfx950 whatever the
+// occupancy, while the same bytes read lane-contiguously stream at ~7 TB/s (dk_diag_read_probe modes 9-11). So when
+// the chunk's frames lie in one window of <= kWinGran granules, ceil(G / 64) LDS-DMA loads
+// (buffer_load_dwordx4 ... lds, 1 KiB each, lane-contiguous) bring the window into the wave's LDS slot and every lane
+// reads its frame's 64 bytes back; scattered frames (e.g. one per 2 KiB mbuf) keep the per-lane loads.
+constexpr uint32_t kWinGran = 288;                    // 4.5 KiB: 64 packed 64-byte frames at any even offset
+constexpr uint32_t kWinLoads = (kWinGran + 63) / 64;  // DMA loads for a full window
 struct SmallLds {
-    uint4 tail[64];  // the last granule of each big frame (seg_sum_fast)
+    uint4 tail[64];              // the last granule of each big frame (seg_sum_fast)
+    uint4 win[kWinLoads * 64];   // the chunk's frame window (whole 1 KiB DMA pieces)
 };
-#ifndef DK_SMALL_PF
-#define DK_SMALL_PF 0  // prefetch the next chunk's frame registers (measured: no gain)
-#endif
 #ifndef DK_MIN_WAVES_SMALL
 #define DK_MIN_WAVES_SMALL 6
 #endif
+#ifndef DK_SMALL_WAVES
+#define DK_SMALL_WAVES 4  // waves per workgroup of the small-frame kernel
+#endif
+constexpr uint32_t kSmallWaves = DK_SMALL_WAVES;
+constexpr int kSmallBlock = 64 * DK_SMALL_WAVES;
+// Window plan of one chunk (wave-uniform): DMA'd into the wave's LDS slot, or per-lane loads.
+struct WinPlan {
+    bool win;
+    uint32_t lo;  // blob offset of the window's first granule
+};
+// Issue the chunk's window DMA if its frames lie in one window (the wave's window slot must no longer be read).
+template <bool kShift>
+__device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F, const Blob& B, uint32_t off,
+                                                      uint32_t len, bool live, uint32_t lane, SmallLds& W) {
+    WinPlan pl{false, 0};
+#ifndef DK_SMALL_NOWIN
+    const bool use = F.vec && !F.big;
+    const uint32_t a = off - F.sh;  // the frame's first granule
+    const uint64_t lm = __ballot(live);
+    if (!(lm & 1u)) return pl;  // lane 0 starts every chunk
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(a);
+    const uint32_t last = 63u - (uint32_t)__builtin_clzll(lm);
+    const uint32_t hi = __builtin_amdgcn_readlane(off + len, last);
+    const bool inwin = !use || (a >= lo && off + len <= hi);
+    if (hi > lo && hi - lo <= kWinGran * 16 && !__ballot(live && !inwin)) {
+        const uint32_t G = (hi - lo + 15) >> 4;  // wave-uniform
+        for (uint32_t k = 0; k * 64 < G; k++) {
+            const uint32_t g = 64 * k + lane;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(B.rs, (lds_void*)&W.win[64 * k], 16, g < G ? lo + 16 * g : kOob,
+                                                     0, 0, DK_NT_LOADS ? 2 : 0);
+        }
+        pl.win = true;
+        pl.lo = lo;
+    }
+#endif
+    return pl;
+}
+// The chunk's register windows: from the DMA'd window in LDS, or by per-lane loads (scattered frames).
+template <bool kShift>
+__device__ __forceinline__ void small_window_read(const WinPlan& pl, const FrameDesc<kShift>& F, const Blob& B,
+                                                  uint32_t off, SmallLds& W, RegAcc& R) {
+    if (pl.win) {
+        const uint32_t b = F.vec && !F.big ? (off - F.sh - pl.lo) >> 4 : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 q = W.win[b + k];
+            R.w[4 * k + 0] = q.x;
+            R.w[4 * k + 1] = q.y;
+            R.w[4 * k + 2] = q.z;
+            R.w[4 * k + 3] = q.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next chunk's DMA reuses the slot
+        return;
+    }
+    small_load(F, B, off, R);
+}
+
 template <bool kShift>
 __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uint32_t lane, uint32_t off, const Blob& B,
                                                  SmallLds& W, Chunk& C) {
@@ -1148,8 +1244,8 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
 }
 
 template <bool kShift, bool kOpt>
-__global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
-    __shared__ SmallLds s_wave[kWaves];
+__global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
+    __shared__ SmallLds s_wave[kSmallWaves];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
     __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
@@ -1158,12 +1254,12 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6;
     const bool lds_flows = P.flow_mode == kFlowLds;
-    for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
+        for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
     __syncthreads();
 
-    const WaveRange r = wave_range(P.sched, P.n, wv, lane);
+    const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
     const Blob B(P.frames, P.frames_bytes);
     SmallLds& W = s_wave[wv];
     // Pipeline: chunk k is parsed while chunk k + 1's frame registers and chunk k + 2's descriptors load.
@@ -1181,7 +1277,6 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
     }
     Chunk C;
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
-    small_load(F, B, off, C.R);
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1192,13 +1287,11 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
             len2 = P.len[c2 + r.lane_off];
         }
         const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + r.lane_off < lim1, off1, len1);
-#if DK_SMALL_PF
-        RegAcc R1;
-        small_load(F1, B, off1, R1);  // next chunk's frame registers, in flight during this chunk's phase C
-#endif
-        small_big_frames(F, lane, off, B, W, C);
         uint32_t v, fid;
         Rec rec;
+        rec.meta = kNoRec;
+        small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
+        small_big_frames(F, lane, off, B, W, C);
         rx_finish<kShift, false, SmallLds, kOpt>(P, i, live, lane, W, off, len, C, v, fid, rec);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         // rotate the pipeline
@@ -1208,11 +1301,6 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
         off = off1;
         len = len1;
         F = F1;
-#if DK_SMALL_PF
-        C.R = R1;
-#else
-        small_load(F, B, off, C.R);
-#endif
         have1 = have2;
         c1 = c2;
         lim1 = lim2;
@@ -1220,7 +1308,7 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel
         len1 = len2;
     }
     __syncthreads();
-    flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh, &s_last);
+    flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh, &s_last);
 }
 
 // Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
@@ -1645,7 +1733,7 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
     else if (family == dk::kFamilySmall)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kBlock,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kSmallBlock,
                                                           dyn_lds_bytes);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1654,17 +1742,19 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     return e == hipSuccess ? blocks : 0;
 }
 
+uint32_t dk_rx_small_block_waves() { return dk::kSmallWaves; }
+
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
-    const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.path_stats;
+    const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
     if (p.small && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.split && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<false>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split)

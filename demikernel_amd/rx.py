@@ -124,8 +124,9 @@ class RxResults:
     TCP_ARRAYS = ["tcp_seq", "tcp_ack", "tcp_win"]
 
     def __init__(self, n: int, nflows: int, *, device=None, tcp_fields: bool = False, counts: bool = True,
-                 host: bool = False, dst_ip: bool = True):
-        """dst_ip=False: the 20-byte-per-frame layout (dk_rx.h ABI 3: dst_ip not written)."""
+                 host: bool = False, dst_ip: bool = True, tcp_opts: bool = False):
+        """dst_ip=False: the 20-byte-per-frame layout (dk_rx.h ABI 3: dst_ip not written). tcp_opts: the per-frame
+        dk_tcp_opts records (written for option-bearing TCP segments only; zero-initialised here)."""
         import torch
 
         kw = dict(device=device) if not host else dict(pin_memory=torch.cuda.is_available())
@@ -137,6 +138,8 @@ class RxResults:
         if counts:
             self.t["flow_counts"] = torch.zeros(max(nflows, 1), dtype=torch.int64, **kw)
             self.t["verdict_counts"] = torch.zeros(DK_V_COUNT, dtype=torch.int64, **kw)
+        if tcp_opts:
+            self.t["tcp_opts"] = torch.zeros(max(n, 1) * N.TCP_OPTS_DTYPE.itemsize, dtype=torch.uint8, **kw)
 
     def c_struct(self) -> N.DkRxResults:
         return N.DkRxResults(*[_ptr(self.t.get(name)) for name in N.RESULT_FIELDS])
@@ -150,7 +153,10 @@ class RxResults:
         out = {}
         for k, v in self.t.items():
             a = v.cpu().numpy()
-            out[k] = a.view(np.uint64) if a.dtype == np.int64 else a.view(np.uint32)
+            if k == "tcp_opts":
+                out[k] = a.view(N.TCP_OPTS_DTYPE)[: self.n]
+            else:
+                out[k] = a.view(np.uint64) if a.dtype == np.int64 else a.view(np.uint32)
         return out
 
 
@@ -184,11 +190,12 @@ class RxEngine:
         _check(self.lib.dk_rx_flow_table_set(self._ctx, flows.ctypes.data, len(flows)), "dk_rx_flow_table_set")
         self.nflows = len(flows)
 
-    def results(self, n: int, *, tcp_fields: bool = False, counts: bool = True, dst_ip: bool = True) -> RxResults:
+    def results(self, n: int, *, tcp_fields: bool = False, counts: bool = True, dst_ip: bool = True,
+                tcp_opts: bool = False) -> RxResults:
         import torch
 
         return RxResults(n, self.nflows, device=torch.device("cuda", self.device), tcp_fields=tcp_fields,
-                         counts=counts, dst_ip=dst_ip)
+                         counts=counts, dst_ip=dst_ip, tcp_opts=tcp_opts)
 
     def receive_batch(self, batch: FrameBatch, results: RxResults, stream=None) -> None:
         """Asynchronous on `stream` (a torch.cuda.Stream; default: the current stream)."""

@@ -148,9 +148,31 @@ typedef struct dk_rx_batch {
     uint32_t flags;           /* DK_RX_BATCH_* hints, 0 = none                                         */
 } dk_rx_batch;
 
+/* TCP options of one segment: the reference's option list [TcpOptions2; 5] (tcp/header.rs:26-41, filled in header
+ * order by parse_and_strip :215-302; NoOperation and EndOfOptionsList are not entries). */
+enum dk_tcp_opt_kind {
+    DK_TCPOPT_MSS = 2,      /* MaximumSegmentSize(u16)                                   */
+    DK_TCPOPT_WS = 3,       /* WindowScale(u8)                                           */
+    DK_TCPOPT_SACK_OK = 4,  /* SelectiveAcknowlegementPermitted                          */
+    DK_TCPOPT_SACK = 5,     /* SelectiveAcknowlegement { num_sacks, sacks: [_; 4] }       */
+    DK_TCPOPT_TS = 8        /* Timestamp { sender_timestamp, echo_timestamp }             */
+};
+typedef struct dk_tcp_opt {
+    uint8_t kind;   /* enum dk_tcp_opt_kind                                                              */
+    uint8_t u8;     /* WS: the shift count; SACK: num_sacks (1..4)                                         */
+    uint16_t u16;   /* MSS: the segment size; SACK: index of its first block in dk_tcp_opts.sack            */
+    uint32_t v0;    /* TS: sender_timestamp                                                                */
+    uint32_t v1;    /* TS: echo_timestamp                                                                  */
+} dk_tcp_opt;       /* 12 bytes */
+typedef struct dk_tcp_opts {
+    uint32_t num;          /* entries in opt[] (0..5)                                                       */
+    dk_tcp_opt opt[5];
+    uint32_t sack[4][2];   /* SACK blocks (begin, end) of every SACK entry, in order (40 option bytes hold <= 4) */
+} dk_tcp_opts;             /* 96 bytes; unused entries and blocks are zero */
+
 /* Per-frame results, struct-of-arrays, one element per frame. Required arrays: meta, src_ip, ports, payload, flow_id
  * (20 bytes per frame). Optional (NULL = not written): dst_ip, tcp_seq, tcp_ack, tcp_win, flow_counts,
- * verdict_counts. (ABI 3: dst_ip became optional. What a delivered frame goes on to, socket.receive, never sees the
+ * verdict_counts, tcp_opts. (ABI 3: dst_ip became optional. What a delivered frame goes on to, socket.receive, never sees the
  * destination address — tcp/peer.rs:254 passes (src_ip, header, payload), udp/peer.rs:167 (remote, payload) — and
  * it is the configured local address or 255.255.255.255 for every delivered frame, layer3/mod.rs:91-95.)
  *
@@ -179,6 +201,11 @@ typedef struct dk_rx_results {
     uint32_t* tcp_win;
     uint64_t* flow_counts;     /* [number of flows in the table] */
     uint64_t* verdict_counts;  /* [DK_V_COUNT]                   */
+    dk_tcp_opts* tcp_opts;     /* [n], optional: written only for frames whose TCP segment carries options (data
+                                  offset > 5) and parses (verdict DK_V_OK_TCP or DK_V_TCP_NOSOCK); every other
+                                  frame's record is left untouched (dk_rx_process_host: zeroed). Saves the LibOS a
+                                  CPU re-parse of SYN / SYN-ACK option lists (active_open.rs / passive_open.rs
+                                  consume them). */
 } dk_rx_results;
 
 typedef struct dk_rx_ctx dk_rx_ctx;

@@ -18,7 +18,7 @@ int dko_peer_set_flows(dko_peer* p, const dk_flow* flows, uint32_t n);
 void dko_process(const dko_peer* p, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* off,
                  const uint16_t* len, uint32_t n, uint32_t* meta, uint32_t* src, uint32_t* dst, uint32_t* ports,
                  uint32_t* payload, uint32_t* flow, uint32_t* seq, uint32_t* ack, uint32_t* win,
-                 uint64_t* flow_counts, uint64_t* verdict_counts);
+                 uint64_t* flow_counts, uint64_t* verdict_counts, dk_tcp_opts* opts);
 }
 
 template <class T>
@@ -59,8 +59,9 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> a[9];
     for (auto& v : a) v.assign(n, 0);
     std::vector<uint64_t> fc(nf ? nf : 1, 0), vc(DK_V_COUNT, 0);
+    std::vector<dk_tcp_opts> opts(n ? n : 1);
     dko_process(p, blob, blob_len, off.data(), len.data(), n, a[0].data(), a[1].data(), a[2].data(), a[3].data(),
-                a[4].data(), a[5].data(), a[6].data(), a[7].data(), a[8].data(), fc.data(), vc.data());
+                a[4].data(), a[5].data(), a[6].data(), a[7].data(), a[8].data(), fc.data(), vc.data(), opts.data());
     FILE* out = fopen(argv[2], "wb");
     if (!out) return 2;
     for (auto& v : a) fwrite(v.data(), 4, n, out);

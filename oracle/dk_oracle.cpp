@@ -147,6 +147,7 @@ struct TcpHeader {
     uint16_t window, urgent;
     uint32_t data_offset;
     int num_options;
+    dk_tcp_opts opts;  // the option list (tcp/header.rs:212-302) in the dk_rx.h record layout
 };
 
 // tcp/header.rs:433-509, restated word for word.
@@ -219,56 +220,75 @@ int tcp_parse_and_strip(uint32_t local_ipv4_addr, uint32_t remote_ipv4_addr, Buf
     }
     out->urgent = be16(hdr + 18);
     int num_options = 0;
+    std::memset(&out->opts, 0, sizeof out->opts);
+    uint32_t nsack = 0;
     if (data_offset > 20) {                                           // :215-302
         Cursor rdr{hdr + 20, data_offset - 20, 0};
         while (rdr.pos < data_offset - 20) {
             uint8_t kind;
             if (!rdr.read_exact(&kind, 1)) return DK_V_TCP_OPT_EIO;
             uint8_t t1, t2[2], t4[4];
+            dk_tcp_opt e{kind, 0, 0, 0, 0};
             switch (kind) {
                 case 0: goto done;                                    // EndOfOptionsList: break
                 case 1: continue;                                     // NoOperation: not counted
-                case 2:                                               // MSS
+                case 2:                                               // MaximumSegmentSize(mss)
                     if (!rdr.read_exact(&t1, 1)) return DK_V_TCP_OPT_EIO;
                     if (t1 != 4) return DK_V_TCP_OPT;
                     if (!rdr.read_exact(t2, 2)) return DK_V_TCP_OPT_EIO;
+                    e.u16 = be16(t2);
                     break;
-                case 3:                                               // window scale
+                case 3:                                               // WindowScale(scale)
                     if (!rdr.read_exact(&t1, 1)) return DK_V_TCP_OPT_EIO;
                     if (t1 != 3) return DK_V_TCP_OPT;
                     if (!rdr.read_exact(&t1, 1)) return DK_V_TCP_OPT_EIO;
+                    e.u8 = t1;
                     break;
-                case 4:                                               // SACK permitted
+                case 4:                                               // SelectiveAcknowlegementPermitted
                     if (!rdr.read_exact(&t1, 1)) return DK_V_TCP_OPT_EIO;
                     if (t1 != 2) return DK_V_TCP_OPT;
                     break;
-                case 5: {                                             // SACK
+                case 5: {                                             // SelectiveAcknowlegement
                     if (!rdr.read_exact(&t1, 1)) return DK_V_TCP_OPT_EIO;
                     size_t num_sacks;
                     switch (t1) {
                         case 10: case 18: case 26: case 34: num_sacks = ((size_t)t1 - 2) / 8; break;
                         default: return DK_V_TCP_OPT;
                     }
-                    for (size_t s = 0; s < num_sacks; s++) {
+                    e.u8 = (uint8_t)num_sacks;
+                    e.u16 = (uint16_t)nsack;
+                    for (size_t k = 0; k < num_sacks; k++) {
+                        uint8_t b4[4];
                         if (!rdr.read_exact(t4, 4)) return DK_V_TCP_OPT_EIO;
-                        if (!rdr.read_exact(t4, 4)) return DK_V_TCP_OPT_EIO;
+                        if (!rdr.read_exact(b4, 4)) return DK_V_TCP_OPT_EIO;
+                        if (nsack < 4) {
+                            out->opts.sack[nsack][0] = be32(t4);
+                            out->opts.sack[nsack][1] = be32(b4);
+                            nsack++;
+                        }
                     }
                     break;
                 }
-                case 8:                                               // timestamp
+                case 8: {                                             // Timestamp
                     if (!rdr.read_exact(&t1, 1)) return DK_V_TCP_OPT_EIO;
                     if (t1 != 10) return DK_V_TCP_OPT;
+                    uint8_t b4[4];
                     if (!rdr.read_exact(t4, 4)) return DK_V_TCP_OPT_EIO;
-                    if (!rdr.read_exact(t4, 4)) return DK_V_TCP_OPT_EIO;
+                    if (!rdr.read_exact(b4, 4)) return DK_V_TCP_OPT_EIO;
+                    e.v0 = be32(t4);
+                    e.v1 = be32(b4);
                     break;
+                }
                 default: return DK_V_TCP_OPT;                         // "invalid TCP option"
             }
             if (num_options >= 5) return DK_V_TCP_OPT;                // "too many TCP options provided"
+            out->opts.opt[num_options] = e;                           // option_list[num_options] = option
             num_options++;
         }
     }
 done:
     out->num_options = num_options;
+    out->opts.num = (uint32_t)num_options;
     out->data_offset = (uint32_t)data_offset;
     buf.adjust(data_offset);                                          // :306-307
     return -1;
@@ -410,7 +430,8 @@ namespace {
 // The whole per-frame chain: layer2/mod.rs:56-79 -> layer3/mod.rs:71-120 -> layer4/mod.rs:97-107 ->
 // tcp/peer.rs:220-255 | udp/peer.rs:129-168. Writes the dk_rx.h result record for frame i.
 void receive_one(const dko_peer& peer, const uint8_t* frame, size_t len, uint32_t* meta, uint32_t* src, uint32_t* dst,
-                 uint32_t* ports, uint32_t* payload, uint32_t* flow, uint32_t* seq, uint32_t* ack, uint32_t* win) {
+                 uint32_t* ports, uint32_t* payload, uint32_t* flow, uint32_t* seq, uint32_t* ack, uint32_t* win,
+                 dk_tcp_opts* opts) {
     *meta = 0; *src = 0; *dst = 0; *ports = 0; *payload = 0; *flow = DK_FLOW_NONE; *seq = 0; *ack = 0; *win = 0;
     Buf buf{frame, len, 0};
     uint16_t et;
@@ -463,6 +484,7 @@ void receive_one(const dko_peer& peer, const uint8_t* frame, size_t len, uint32_
         *payload = (uint32_t)buf.off | (uint32_t)buf.len << 16;
         *flow = fid;
         *seq = th.seq; *ack = th.ack; *win = (uint32_t)th.window | (uint32_t)th.urgent << 16;
+        if (opts && th.data_offset > 20) *opts = th.opts;  // option-bearing segment (dk_rx.h tcp_opts)
         return;
     }
     // UdpPeer::receive (udp/peer.rs:129-168): parse_and_strip(&src_ipv4_addr, &self.local_ipv4_addr, ...)
@@ -523,7 +545,7 @@ int dko_peer_set_flows(dko_peer* p, const dk_flow* flows, uint32_t n) {
 static void dko_range(const dko_peer* p, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* off,
                       const uint16_t* len, uint32_t begin, uint32_t end, uint32_t* meta, uint32_t* src, uint32_t* dst,
                       uint32_t* ports, uint32_t* payload, uint32_t* flow, uint32_t* seq, uint32_t* ack, uint32_t* win,
-                      uint64_t* flow_counts, uint64_t* verdict_counts) {
+                      uint64_t* flow_counts, uint64_t* verdict_counts, dk_tcp_opts* opts) {
     for (uint32_t i = begin; i < end; i++) {
         uint32_t s_, a_, w_;
         if ((uint64_t)off[i] + len[i] > frames_bytes) {
@@ -531,7 +553,7 @@ static void dko_range(const dko_peer* p, const uint8_t* frames, uint64_t frames_
             s_ = a_ = w_ = 0;
         } else {
             receive_one(*p, frames + off[i], len[i], &meta[i], &src[i], &dst[i], &ports[i], &payload[i], &flow[i],
-                        &s_, &a_, &w_);
+                        &s_, &a_, &w_, opts ? opts + i : nullptr);
         }
         if (seq) seq[i] = s_;
         if (ack) ack[i] = a_;
@@ -544,9 +566,9 @@ static void dko_range(const dko_peer* p, const uint8_t* frames, uint64_t frames_
 void dko_process(const dko_peer* p, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* off,
                  const uint16_t* len, uint32_t n, uint32_t* meta, uint32_t* src, uint32_t* dst, uint32_t* ports,
                  uint32_t* payload, uint32_t* flow, uint32_t* seq, uint32_t* ack, uint32_t* win,
-                 uint64_t* flow_counts, uint64_t* verdict_counts) {
+                 uint64_t* flow_counts, uint64_t* verdict_counts, dk_tcp_opts* opts) {
     dko_range(p, frames, frames_bytes, off, len, 0, n, meta, src, dst, ports, payload, flow, seq, ack, win,
-              flow_counts, verdict_counts);
+              flow_counts, verdict_counts, opts);
 }
 
 // Scaled CPU baseline: packet shards over `threads` OpenMP threads (counts merged after the loop). Returns the
@@ -563,13 +585,13 @@ int dko_process_mt(const dko_peer* p, const uint8_t* frames, uint64_t frames_byt
         used = nt;
         uint32_t b = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
         dko_range(p, frames, frames_bytes, off, len, b, e, meta, src, dst, ports, payload, flow, nullptr, nullptr,
-                  nullptr, nullptr, nullptr);
+                  nullptr, nullptr, nullptr, nullptr);
     }
     return used;
 #else
     (void)threads;
     dko_range(p, frames, frames_bytes, off, len, 0, n, meta, src, dst, ports, payload, flow, nullptr, nullptr, nullptr,
-              nullptr, nullptr);
+              nullptr, nullptr, nullptr);
     return 1;
 #endif
 }

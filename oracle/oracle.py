@@ -15,6 +15,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libdk_oracle.so")
 
 DK_V_COUNT = 39  # enum dk_verdict in include/dk_rx.h (tests/test_oracle.py checks it)
+# struct dk_tcp_opts (include/dk_rx.h): the parsed [TcpOptions2; 5] list of one segment.
+TCP_OPT_DTYPE = np.dtype([("kind", "u1"), ("u8", "u1"), ("u16", "<u2"), ("v0", "<u4"), ("v1", "<u4")])
+TCP_OPTS_DTYPE = np.dtype([("num", "<u4"), ("opt", TCP_OPT_DTYPE, (5,)), ("sack", "<u4", (4, 2))])
+assert TCP_OPT_DTYPE.itemsize == 12 and TCP_OPTS_DTYPE.itemsize == 96
 FLOW_DTYPE = np.dtype([("kind", "<u4"), ("local_ip", "<u4"), ("remote_ip", "<u4"),
                        ("local_port", "<u2"), ("remote_port", "<u2")])
 
@@ -37,7 +41,7 @@ def lib() -> ctypes.CDLL:
         L.dko_peer_free.argtypes = [vp]
         L.dko_peer_set_flows.restype = c_int
         L.dko_peer_set_flows.argtypes = [vp, vp, c_uint32]
-        L.dko_process.argtypes = [vp, vp, c_uint64, vp, vp, c_uint32] + [vp] * 11
+        L.dko_process.argtypes = [vp, vp, c_uint64, vp, vp, c_uint32] + [vp] * 12
         L.dko_process_mt.restype = c_int
         L.dko_process_mt.argtypes = [vp, vp, c_uint64, vp, vp, c_uint32] + [vp] * 6 + [c_int]
         L.dko_ipv4_parse.restype = c_int
@@ -99,12 +103,13 @@ class OraclePeer:
                ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win")}
         out["flow_counts"] = np.zeros(max(self.nflows, 1), np.uint64)
         out["verdict_counts"] = np.zeros(DK_V_COUNT, np.uint64)
+        out["tcp_opts"] = np.zeros(max(n, 1), TCP_OPTS_DTYPE)[:n]  # written for option-bearing TCP segments only
         fb = blob.nbytes if frames_bytes is None else frames_bytes
         self._L.dko_process(self._p, blob.ctypes.data if blob.size else None, fb, off.ctypes.data,
                             lens.ctypes.data, n,
                             *[out[k].ctypes.data for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id",
                                                            "tcp_seq", "tcp_ack", "tcp_win", "flow_counts",
-                                                           "verdict_counts")])
+                                                           "verdict_counts", "tcp_opts")])
         return out
 
     def process_mt(self, blob, off, lens, threads: int) -> tuple[dict, int]:

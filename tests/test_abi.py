@@ -46,7 +46,8 @@ def test_struct_layout_matches_ctypes(tmp_path):
     """sizeof/offsetof from the C compiler == the ctypes mirror (dk_rx_cfg, dk_flow, dk_rx_batch, dk_rx_results)."""
     structs = {"dk_rx_cfg": N.DkRxCfg, "dk_flow": N.DkFlow, "dk_rx_batch": N.DkRxBatch, "dk_rx_results": N.DkRxResults,
                "dk_tcp_view": N.DkTcpView, "dk_tcp_conn": N.DkTcpConn, "dk_tcp_out": N.DkTcpOut,
-               "dk_demi_sgaseg_t": N.DemiSgaseg, "dk_demi_sgarray_t": N.DemiSgarray}
+               "dk_demi_sgaseg_t": N.DemiSgaseg, "dk_demi_sgarray_t": N.DemiSgarray, "dk_tcp_opt": N.DkTcpOpt,
+               "dk_tcp_opts": N.DkTcpOpts}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADERS[0]}"', f'#include "{HEADERS[3]}"',
              f'#include "{HEADERS[4]}"',
              "int main(void) {"]
@@ -67,6 +68,9 @@ def test_struct_layout_matches_ctypes(tmp_path):
             assert int(got[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert ctypes.sizeof(N.DkFlow) == N.FLOW_DTYPE.itemsize == 16
     assert ctypes.sizeof(N.DkTcpConn) == N.CONN_DTYPE.itemsize == 288
+    assert ctypes.sizeof(N.DkTcpOpts) == N.TCP_OPTS_DTYPE.itemsize == 96
+    for fname, _ in N.DkTcpOpts._fields_:
+        assert N.TCP_OPTS_DTYPE.fields[fname][1] == getattr(N.DkTcpOpts, fname).offset, fname
     for fname, _ in N.DkTcpConn._fields_:
         assert N.CONN_DTYPE.fields[fname][1] == getattr(N.DkTcpConn, fname).offset, fname
 

@@ -183,13 +183,37 @@ def test_fuzz_headers(torch_cuda):
 
 
 def test_ip_and_tcp_options(torch_cuda):
+    """IPv4 and TCP options: verdicts (T5 incl. EIO) and, requested, every option-bearing segment's parsed list
+    (dk_tcp_opts: the reference's [TcpOptions2; 5]) equal the oracle's — through the HBM-resident call (only those
+    records written) and the host pipeline (every record written, zero for the rest)."""
+    import torch
+
+    from demikernel_amd import RxResults
+
     pl = bytes(range(200))
     frames = []
+    ts = bytes([8, 10]) + bytes(range(1, 9))
+    extra = [bytes([2, 4, 5, 0xB4, 1, 3, 3, 14, 4, 2, 1, 1]) + ts,
+             bytes([1, 1, 5, 34]) + bytes(range(100, 132)) + bytes([1, 1]),
+             bytes([5, 10]) + bytes(range(8)) + bytes([5, 18]) + bytes(range(16)) + bytes([1, 1, 1, 1])]
     for ihl_opts in (b"", bytes([1, 1, 1, 0]), bytes(8), bytes(40)):
-        for opts, _ in F.tcp_opt_cases():
+        for opts in [c[0] for c in F.tcp_opt_cases()] + extra:
             frames.append(F.tcp_frame(pl[: len(frames) % 150], options=opts, ip_options=ihl_opts))
-    blob, off, lens = F.pack(frames)
-    check(blob, off, lens, F.corpus_flows(), ctx="options")
+    for misalign in (None, [0, 2, 1, 6]):
+        blob, off, lens = F.pack(frames, misalign=misalign)
+        check(blob, off, lens, F.corpus_flows(), ctx="options")
+        eng = RxEngine(Config(LOCAL))
+        eng.set_sockets(F.corpus_flows())
+        r = eng.results(len(off), tcp_fields=True, tcp_opts=True)
+        eng.receive_batch(FrameBatch.from_numpy(blob, off, lens), r)
+        torch.cuda.synchronize()
+        got = r.to_numpy()
+        exp = run_oracle(blob, off, lens, F.corpus_flows())
+        assert (exp["tcp_opts"]["num"] > 0).sum() > 40
+        assert got["tcp_opts"].tobytes() == exp["tcp_opts"].tobytes(), "tcp_opts (device-resident)"
+        h = RxResults(len(off), len(F.corpus_flows()), tcp_fields=True, host=True, tcp_opts=True)
+        eng.receive_batch_host(blob, off, lens, h, chunk_frames=37)
+        assert h.to_numpy()["tcp_opts"].tobytes() == exp["tcp_opts"].tobytes(), "tcp_opts (host pipeline)"
 
 
 def test_bad_descriptors_and_edges(torch_cuda):

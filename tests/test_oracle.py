@@ -254,3 +254,41 @@ def test_control_plane_fields():
     assert VERDICTS[m[2] & 0xFF] == "ARP" and (m[2] >> 8) & 0xFF == 0 and m[2] >> 16 == 2
     assert r["src_ip"][2] == ipv4(BOB_IPV4) and r["dst_ip"][2] == ipv4(F.ALICE_IPV4)
     assert r["payload"][2] == 14 | (28 + 18) << 16 and r["flow_id"][2] == 0xFFFFFFFF
+
+
+def test_tcp_option_values():
+    """The option list parse_and_strip builds (tcp/header.rs:215-302, [TcpOptions2; 5] in header order, NOP / EOL not
+    entries) as the dk_tcp_opts record: hand-derived values for a SYN-style list, a SACK list sharing the block array,
+    duplicates kept in order, EOL stopping the walk; no record for segments without options or failing parse."""
+    import frames as F
+    from demikernel_amd.synth import BOB_IPV4
+
+    ts = bytes([8, 10]) + (0x11223344).to_bytes(4, "big") + (0x55667788).to_bytes(4, "big")
+    sack2 = bytes([5, 18]) + b"".join(x.to_bytes(4, "big") for x in (100, 200, 300, 400))
+    cases = [
+        (bytes([2, 4, 0x05, 0xB4, 1, 3, 3, 7, 4, 2, 1, 1]) + ts,                  # MSS, NOP, WS, SACK-OK, NOP NOP, TS
+         [(2, 0, 1460, 0, 0), (3, 7, 0, 0, 0), (4, 0, 0, 0, 0), (8, 0, 0, 0x11223344, 0x55667788)], []),
+        (bytes([1, 1]) + sack2 + bytes([5, 10]) + (7).to_bytes(4, "big") + (9).to_bytes(4, "big") + bytes([0, 0]),
+         [(5, 2, 0, 0, 0), (5, 1, 2, 0, 0)], [(100, 200), (300, 400), (7, 9)]),
+        (bytes([3, 3, 2, 3, 3, 9, 0, 2, 4, 0x05, 0xB4, 0, 0]),                     # WS 2, WS 9, EOL: rest ignored
+         [(3, 2, 0, 0, 0), (3, 9, 0, 0, 0)], []),
+    ]
+    frames = [F.tcp_frame(b"x" * 10, options=o) for o, _, _ in cases]
+    frames += [F.tcp_frame(b"plain"), F.tcp_frame(b"", options=bytes([9, 2, 0, 0]))]  # no options; TCP_OPT
+    blob, off, lens = F.pack(frames)
+    p = O.OraclePeer(ipv4(BOB_IPV4))
+    p.set_flows(F.corpus_flows())
+    r = p.process(blob, off, lens)
+    rec = r["tcp_opts"]
+    for k, (_, opts, sacks) in enumerate(cases):
+        assert VERDICTS[r["meta"][k] & 0xFF] in ("OK_TCP", "TCP_NOSOCK"), k
+        assert rec[k]["num"] == len(opts), k
+        for j, (kind, u8, u16, v0, v1) in enumerate(opts):
+            o = rec[k]["opt"][j]
+            assert (o["kind"], o["u8"], o["u16"], o["v0"], o["v1"]) == (kind, u8, u16, v0, v1), (k, j)
+        for j in range(len(opts), 5):
+            assert rec[k]["opt"][j]["kind"] == 0
+        for j, (b, e) in enumerate(sacks):
+            assert tuple(rec[k]["sack"][j]) == (b, e), (k, j)
+    assert VERDICTS[r["meta"][4] & 0xFF] == "TCP_OPT"
+    assert rec[3].tobytes() == bytes(96) and rec[4].tobytes() == bytes(96)

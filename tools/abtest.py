@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--scheds", default="", help="comma list of DK_RX_SCHED values to interleave (default: host rule)")
     ap.add_argument("--knob", default="", help="NAME=v1,v2,...: interleave values of one more env knob (e.g. DK_RX_SPLIT=0,1)")
     ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
+    ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
     args = ap.parse_args()
     import torch
 
@@ -34,6 +35,7 @@ def main():
 
     base = RxEngine(Config(synth.BOB_IPV4))
     batch, flows, tr = bench.make_batch(base, args.workload, 0, synth.SEED, 1)
+    rot = [batch] + [bench.make_batch(base, args.workload, 0, synth.SEED + 1000 * k, 1)[0] for k in range(1, args.rotate)]
     engines = {}
     for v in args.variants:
         e = RxEngine(Config(synth.BOB_IPV4), lib_path=os.path.abspath(v))
@@ -66,11 +68,11 @@ def main():
             for k, (e, r) in engines.items():
                 if hasattr(e.lib, "dk_diag_rx_set_tuning"):  # later builds read them once per context
                     e.set_tuning(**knobs)
-                run = (lambda: e.tx_checksum(batch)) if args.tx else (lambda: e.receive_batch(batch, r))  # noqa: E731
-                run()
+                run = (lambda b: e.tx_checksum(b)) if args.tx else (lambda b: e.receive_batch(b, r))  # noqa: E731
+                run(batch)
                 ev0.record()
-                for _ in range(args.iters):
-                    run()
+                for it in range(args.iters):
+                    run(rot[it % len(rot)])
                 ev1.record()
                 torch.cuda.synchronize()
                 times[(k, g, cf)].append(ev0.elapsed_time(ev1) / args.iters)

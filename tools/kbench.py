@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--no-rx", action="store_true")
     ap.add_argument("--tx", action="store_true", help="also time dk_tx_checksum (rewrites the batch's checksums)")
     ap.add_argument("--no-counts", action="store_true", help="pass NULL flow/verdict counters (cost attribution)")
+    ap.add_argument("--modes", default="3,4,6,7,8")
+    ap.add_argument("--grids", default="256,512,768,1024")
+    ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
     args = ap.parse_args()
 
     import torch
@@ -53,10 +56,16 @@ def main():
 
     eng = RxEngine(Config(synth.BOB_IPV4))
     batch, flows, tr = bench.make_batch(eng, args.workload, 0, synth.SEED, 1)
+    rot = [batch] + [bench.make_batch(eng, args.workload, 0, synth.SEED + 1000 * k, 1)[0] for k in range(1, args.rotate)]
     res = eng.results(batch.n, counts=not args.no_counts)
+    it = [0]
+
+    def next_batch():
+        it[0] += 1
+        return rot[it[0] % len(rot)]
     fb = int(tr.frame_len.astype(np.int64).sum())
     if not args.no_rx:
-        t = time_events(lambda: eng.receive_batch(batch, res), args.iters)
+        t = time_events(lambda: eng.receive_batch(next_batch(), res), args.iters)
         algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES)
         print(json.dumps({"kernel": "dk_rx", "workload": args.workload, "counts": not args.no_counts,
                           "frames": batch.n, "frame_bytes": fb, "algo_bytes": algo, "blob_bytes": batch.blob.numel(),
@@ -72,8 +81,8 @@ def main():
     if args.probe or args.probe_one:
         lib = N.load_library()
         nbytes = batch.blob.numel() // 16 * 16
-        for mode in ((1,) if args.probe_one else (3, 4, 6, 7, 8)):
-            for grid in ((1024,) if args.probe_one else (256, 512, 768, 1024)):
+        for mode in ((1,) if args.probe_one else tuple(int(m) for m in args.modes.split(','))):
+            for grid in ((1024,) if args.probe_one else tuple(int(g) for g in args.grids.split(','))):
                 scratch = torch.zeros(grid, dtype=torch.int32, device="cuda")
                 s = torch.cuda.current_stream().cuda_stream
 
