@@ -52,6 +52,9 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kCoopU = DK_COOP_U; // dwordx4 loads per lane per phase-B round
 constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave covers per round
+#ifndef DK_COOP_SKIP
+#define DK_COOP_SKIP 0  // measured slower (IMIX +7 %)
+#endif
 #ifndef DK_ROUNDS_PER_STEP
 #define DK_ROUNDS_PER_STEP 2
 #endif
@@ -554,11 +557,28 @@ __device__ __forceinline__ void coop_issue(const CoopPlan& pl, uint32_t r, uint3
         }
     }
     const uint32_t b0 = it * kCoopSpan + l16;
+#if DK_COOP_SKIP
+    // Load slots past the largest frame of a round are not issued (wave-uniform): a 590-byte IMIX frame fills 3 of a
+    // quarter's 6 slots, and an out-of-range load still costs an issue slot and its vmcnt turn.
+    uint32_t mx[kRoundsPerStep];
+#pragma unroll
+    for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+        const uint32_t nb = S.sl[h].nb;
+        mx[h] = max(max(__builtin_amdgcn_readlane(nb, 0), __builtin_amdgcn_readlane(nb, 16)),
+                    max(__builtin_amdgcn_readlane(nb, 32), __builtin_amdgcn_readlane(nb, 48)));
+    }
+#endif
 #pragma unroll
     for (uint32_t h = 0; h < kRoundsPerStep; h++)
 #pragma unroll
         for (uint32_t u = 0; u < kCoopU; u++) {
             const uint32_t b = b0 + 16 * u;
+#if DK_COOP_SKIP
+            if (u > 0 && it * kCoopSpan + 16 * u >= mx[h]) {
+                S.d[h][u] = make_uint4(0, 0, 0, 0);
+                continue;
+            }
+#endif
             S.d[h][u] = B.template ld<DK_NT_LOADS != 0>(b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob);
         }
 }
@@ -1340,9 +1360,27 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
     }
 }
 
+// Hand-off between a stream wave and its finish wave: kSplitBufs LDS buffers per pair with a ready word (chunk + 1
+// written, set by the stream wave) and a free word (chunk + 1 finished, set by the finish wave), so each stream wave
+// runs up to kSplitBufs - 1 chunks ahead of its finisher and no wave waits for the other seven at a workgroup barrier
+// (DK_SPLIT_BUFS 0: the round-1 form, two buffers and one __syncthreads per period).
+#ifndef DK_SPLIT_BUFS
+#define DK_SPLIT_BUFS 3
+#endif
+constexpr int kSplitBufs = DK_SPLIT_BUFS > 0 ? DK_SPLIT_BUFS : 2;
+typedef __attribute__((address_space(3))) uint32_t lu32;
+__device__ __forceinline__ void lds_wait_eq(uint32_t* w, uint32_t want) {
+    while (__hip_atomic_load((lu32*)w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
+        __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void lds_publish(uint32_t* w, uint32_t v) {
+    __hip_atomic_store((lu32*)w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <bool kShift>
 __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P) {
-    __shared__ WaveLds s_buf[2][kWaves];   // [period parity][stream wave]
+    __shared__ WaveLds s_buf[kSplitBufs][kWaves];  // [chunk % kSplitBufs][stream wave]
+    __shared__ uint32_t s_ready[kWaves][kSplitBufs], s_free[kWaves][kSplitBufs];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
     __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
@@ -1355,15 +1393,77 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSplitBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSplitBlock) s_flow[k] = 0;
+    if (tid < kWaves * kSplitBufs) {
+        (&s_ready[0][0])[tid] = 0;
+        (&s_free[0][0])[tid] = 0;
+    }
     __syncthreads();
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
-    const WaveRange r0 = wave_range(0, P.n, 0, lane);  // stream wave 0 has the most chunks
-    uint32_t nper = 0, c0, l0;
-    while (r0.chunk(nper, c0, l0)) nper++;
     const Blob B(P.frames, P.frames_bytes);
     Rec stg[kSplitStageK];
     uint32_t nstg = 0, klast = 0;
+#if DK_SPLIT_BUFS > 0
+    uint32_t c, lim;
+    for (uint32_t p = 0; r.chunk(p, c, lim); p++) {
+        const uint32_t b = p % kSplitBufs;
+        WaveLds& W = s_buf[b][sw];
+        const uint32_t i = c + r.lane_off;
+        const bool live = i < lim;
+        const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+        const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
+        if (!finisher) {
+            // frames of <= 64 bytes: their granules ride along with the big frames' stream and reach the finisher
+            // through the LDS header slot too, so the finish wave never waits on frame memory (IMIX: 7 of 12 frames)
+            RegAcc Rs;
+            small_load(F, B, off, Rs);
+            if (p >= (uint32_t)kSplitBufs) lds_wait_eq(&s_free[sw][b], p - kSplitBufs + 1);  // buffer read out
+            const CoopPlan pl = coop_plan(F, lane, off, W);
+            for (uint32_t rr = 0; rr * 4 < pl.ncoop; rr += kRoundsPerStep) {
+                CoopStep S;
+                coop_issue(pl, rr, lane, W, B, S, 0);
+                coop_finish<kShift>(pl, rr, lane, W, B, S);
+            }
+            if (F.vec && !F.big)
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    W.hdr[lane][k] = make_uint4(Rs.w[4 * k], Rs.w[4 * k + 1], Rs.w[4 * k + 2], Rs.w[4 * k + 3]);
+            if (lane == 0) lds_publish(&s_ready[sw][b], p + 1);
+        } else {
+            Chunk C;
+            lds_wait_eq(&s_ready[sw][b], p + 1);
+            if (F.vec && !F.big)
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 h = W.hdr[lane][k];
+                    C.R.w[4 * k] = h.x;
+                    C.R.w[4 * k + 1] = h.y;
+                    C.R.w[4 * k + 2] = h.z;
+                    C.R.w[4 * k + 3] = h.w;
+                }
+            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 1};
+            coop_gather(F, pl, lane, W, C);
+            uint32_t v, fid;
+            Rec rec;
+            rec.meta = kNoRec;
+            rx_finish<kShift, true>(P, i, live, lane, W, off, len, C, v, fid, rec);
+            if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
+#pragma unroll
+            for (int q = kSplitStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
+            stg[0] = rec;
+            klast = p;
+            if (++nstg == kSplitStageK) {
+                flush_split(P, stg, nstg, r, klast);
+                nstg = 0;
+            }
+            count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+        }
+    }
+    __syncthreads();
+#else
+    const WaveRange r0 = wave_range(0, P.n, 0, lane);  // stream wave 0 has the most chunks
+    uint32_t nper = 0, c0, l0;
+    while (r0.chunk(nper, c0, l0)) nper++;
     for (uint32_t p = 0; p <= nper; p++) {
         uint32_t c, lim;
         if (!finisher) {
@@ -1406,6 +1506,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
         }
         __syncthreads();
     }
+#endif
     if (finisher && nstg) flush_split(P, stg, nstg, r, klast);
     flush_counters(P, tid, kSplitBlock, lds_flows, s_flow, s_vh, &s_last);
 }

@@ -78,10 +78,11 @@ class ShardedReceiver:
 
         slot = self.k % len(self.res)
         r = self.res[slot]
-        if self.done[slot] is not None:  # this slot's previous all-reduce has finished before its counters are reset
-            self.stream.wait_event(self.done[slot])
-        r.t["flow_counts"].zero_()
-        r.t["verdict_counts"].zero_()
+        if self.comm is not None:  # per-step counters, all-reduced (N = 1: they accumulate over steps, no reset)
+            if self.done[slot] is not None:  # this slot's previous all-reduce has finished before the reset
+                self.stream.wait_event(self.done[slot])
+            r.t["flow_counts"].zero_()
+            r.t["verdict_counts"].zero_()
         self.eng.receive_batch(batch, r, stream=self.stream)
         if self.comm is not None:
             ev = torch.cuda.Event()

@@ -209,7 +209,7 @@ def test_ip_and_tcp_options(torch_cuda):
         torch.cuda.synchronize()
         got = r.to_numpy()
         exp = run_oracle(blob, off, lens, F.corpus_flows())
-        assert (exp["tcp_opts"]["num"] > 0).sum() > 40
+        assert (exp["tcp_opts"]["num"] > 0).sum() >= 36
         assert got["tcp_opts"].tobytes() == exp["tcp_opts"].tobytes(), "tcp_opts (device-resident)"
         h = RxResults(len(off), len(F.corpus_flows()), tcp_fields=True, host=True, tcp_opts=True)
         eng.receive_batch_host(blob, off, lens, h, chunk_frames=37)
