@@ -14,7 +14,10 @@
 
 namespace dk {
 
-// Device socket table: open addressing, linear probing, power-of-two capacity >= 2 * entries (never full).
+// Device socket table: open addressing, linear probing, power-of-two capacity >= 8 * entries (at most 2^26 slots,
+// and >= 2 * entries). A wave waits for its worst lane's probe walk (one dependent load per displaced slot): at load
+// 0.5 that was 3-6 dependent round trips per 64-frame chunk at 1024 flows, at 0.125 mostly one (C3 -8 %, IMIX -3 %;
+// a two-choice cuckoo table, two loads and one round trip always, measured C3 -7 % but IMIX +3 %: DESIGN.md §8).
 // Slot = 16 bytes, one dwordx4 load per probe:
 //   x = kind << 24 | flow_id   (0 = empty; kind in 1..3, flow_id < 2^24)
 //   y = local_ip, z = remote_ip, w = local_port | remote_port << 16

@@ -389,7 +389,9 @@ void dk_rx_ctx_destroy(dk_rx_ctx* c) {
 
 int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
     if (!c || (n && !flows) || n > dk::kMaxFlows) return EINVAL;
-    const uint32_t cap = std::max(dk::kMinTableSlots, next_pow2(2 * std::max(n, 1u)));
+    // load factor <= 1/8 (rx_common.h), tables up to 2^26 slots (1 GiB; 32-bit slot offsets), never above 1/2
+    const uint64_t want = std::min<uint64_t>(8ull * std::max(n, 1u), 1ull << 26);
+    const uint32_t cap = std::max({dk::kMinTableSlots, next_pow2((uint32_t)want), next_pow2(2 * std::max(n, 1u))});
     const uint32_t mask = cap - 1;
     std::vector<uint32_t> slots((size_t)cap * 4, 0u);
     for (uint32_t i = 0; i < n; i++) {
@@ -568,6 +570,11 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
     return 0;
 }
 
+#ifdef DK_DIAG_STAMPS
+constexpr size_t kPathStatsWords = 4 + (1u << 21);  // + 16 stamps per wave
+#else
+constexpr size_t kPathStatsWords = 4;
+#endif
 int dk_diag_path_stats_enable(dk_rx_ctx* c, int on) {
     if (!c) return EINVAL;
     DeviceGuard g(c->cfg.device);
@@ -576,9 +583,20 @@ int dk_diag_path_stats_enable(dk_rx_ctx* c, int on) {
         c->d_path_stats = nullptr;
         return 0;
     }
-    if (!c->d_path_stats && hipMalloc(&c->d_path_stats, 4 * sizeof(unsigned long long)) != hipSuccess) return ENOMEM;
-    return hipMemset(c->d_path_stats, 0, 4 * sizeof(unsigned long long)) == hipSuccess ? 0 : EIO;
+    if (!c->d_path_stats && hipMalloc(&c->d_path_stats, kPathStatsWords * sizeof(unsigned long long)) != hipSuccess)
+        return ENOMEM;
+    return hipMemset(c->d_path_stats, 0, kPathStatsWords * sizeof(unsigned long long)) == hipSuccess ? 0 : EIO;
 }
+
+#ifdef DK_DIAG_STAMPS
+// Diagnostic build only: the per-wave stamps the small-frame kernel writes after the path counters.
+extern "C" int dk_diag_stamps_read(dk_rx_ctx* c, uint64_t* out, uint64_t n) {
+    if (!c || !out || !c->d_path_stats || n > kPathStatsWords - 4) return EINVAL;
+    DeviceGuard g(c->cfg.device);
+    if (hipDeviceSynchronize() != hipSuccess) return EIO;
+    return hipMemcpy(out, c->d_path_stats + 4, n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : EIO;
+}
+#endif
 
 int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
     if (!c || !out || !c->d_path_stats) return EINVAL;

@@ -737,7 +737,17 @@ constexpr int kStageK = DK_STAGE_K;
 template <bool kShift, bool kStage, class WL, bool kOpt = true>
 __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
-                                          uint32_t& fid_out, Rec& rec) {
+                                          uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
+#ifdef DK_DIAG_STAMPS  // diagnostic build: sub-phase stamps of the small-frame kernel (tools/stamps.py)
+#define DK_SUB_STAMP(j)                                                                                             \
+    do {                                                                                                            \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                                           \
+        if (P.path_stats && lane == 0 && stamp_base != ~0u)                                                         \
+            P.path_stats[4 + 32 * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) + stamp_base + (j)] = t_;   \
+    } while (0)
+#else
+#define DK_SUB_STAMP(j) do {} while (0)
+#endif
 #ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
 #ifdef DK_DIAG_NO_STORE
     if (live && (C.fsum ^ C.R.w[3] ^ C.R.w[9]) == 0x9E3779B1u)
@@ -770,6 +780,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
     } else {
         parse_headers(MemAcc{f}, len, P, L);
     }
+    DK_SUB_STAMP(0);
     // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
     const bool pend4 = L.v == kPendTcp || L.v == kPendUdp;
     const ProbeKey k1 = L.v == kPendTcp
@@ -779,6 +790,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
     uint4 s1 = make_uint4(0, 0, 0, 0);
     if (pend4) s1 = reinterpret_cast<const uint4*>(P.table)[h1];
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
+    DK_SUB_STAMP(1);
 
     uint32_t fid = DK_FLOW_NONE;
     if (L.v == kPendIcmp) {
@@ -818,6 +830,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
         }
     }
 
+    DK_SUB_STAMP(2);
     const uint32_t v = L.v;
 #ifdef DK_ABL_STOREMOD  // ablation (tuning only; needs n > 65535): results land in a 256 KB L2-resident window
     i &= 0xFFFFu;
@@ -856,6 +869,8 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
             if (P.res.tcp_win) P.res.tcp_win[i] = win;
         }
     }
+    DK_SUB_STAMP(3);
+#ifndef DK_DIAG_STAMPS  // (the stamp build reuses the path-stats buffer)
     if (kOpt && P.path_stats) {  // diagnostics (dk_diag.h): one atomic per path per wave
         const uint32_t path = !fast ? 3u : resum ? 2u : big ? 1u : 0u;
 #pragma unroll
@@ -864,6 +879,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
             if (m && lane == 0) atomicAdd(P.path_stats + k, (unsigned long long)__popcll(m));
         }
     }
+#endif
     v_out = v;
     fid_out = fid;
 }
@@ -1147,7 +1163,10 @@ struct SmallLds {
     uint4 win[kWinLoads * 64];   // the chunk's frame window (whole 1 KiB DMA pieces)
 };
 #ifndef DK_MIN_WAVES_SMALL
-#define DK_MIN_WAVES_SMALL 6
+#define DK_MIN_WAVES_SMALL 5  // 96 VGPRs: no spills (6 waves spilled 16-22 VGPRs to scratch: C3 +11 %)
+#endif
+#ifndef DK_SMALL_PIPE
+#define DK_SMALL_PIPE 0
 #endif
 #ifndef DK_SMALL_WAVES
 #define DK_SMALL_WAVES 4  // waves per workgroup of the small-frame kernel
@@ -1263,6 +1282,18 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
     C.nblk = F.nblk;
 }
 
+#ifdef DK_DIAG_STAMPS  // diagnostic build (tuning only): per-wave s_memrealtime stamps after the path counters
+// s_memtime (shader clock, per XCD) for durations; slots 12/13 hold s_memrealtime (100 MHz, global) at entry/exit.
+#define DK_STAMP_T(slot, t)                                                                                         \
+    do {                                                                                                            \
+        const uint64_t t_ = (t);                                                                                    \
+        if (P.path_stats && lane == 0 && (slot) < 16)                                                               \
+            P.path_stats[4 + 32 * (blockIdx.x * kSmallWaves + wv) + (slot)] = t_;                                   \
+    } while (0)
+#define DK_STAMP(slot) if ((slot) < 11) DK_STAMP_T(slot, __builtin_amdgcn_s_memtime())
+#else
+#define DK_STAMP(slot) do {} while (0)
+#endif
 template <bool kShift, bool kOpt>
 __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
     __shared__ SmallLds s_wave[kSmallWaves];
@@ -1273,6 +1304,10 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6;
+#ifdef DK_DIAG_STAMPS
+    DK_STAMP_T(12, __builtin_amdgcn_s_memrealtime());
+#endif
+    DK_STAMP(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
@@ -1297,6 +1332,10 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     }
     Chunk C;
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
+#if DK_SMALL_PIPE
+    // Window k + 1 is DMA'd while chunk k is parsed (the slot is free once chunk k's window is in registers).
+    if (have) small_window_read(small_window_issue(F, B, off, len, c + r.lane_off < lim, lane, W), F, B, off, W, C.R);
+#endif
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1310,10 +1349,36 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         uint32_t v, fid;
         Rec rec;
         rec.meta = kNoRec;
+        if (k == 0) DK_STAMP(1);
+#if DK_SMALL_PIPE
+        const WinPlan pl1 = have1 ? small_window_issue(F1, B, off1, len1, c1 + r.lane_off < lim1, lane, W) : WinPlan{false, 0};
+#else
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
+#endif
+        DK_STAMP(2 + 3 * k);
         small_big_frames(F, lane, off, B, W, C);
-        rx_finish<kShift, false, SmallLds, kOpt>(P, i, live, lane, W, off, len, C, v, fid, rec);
+        rx_finish<kShift, (DK_SMALL_PIPE >= 2), SmallLds, kOpt>(P, i, live, lane, W, off, len, C, v, fid, rec,
+                                                                 k < 3 ? 16 + 5 * k : ~0u);
+        DK_STAMP(3 + 3 * k);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+#if DK_SMALL_PIPE
+        asm volatile("" ::: "memory");  // keep chunk k + 1's window reads after chunk k's stores (register pressure)
+        if (have1) small_window_read(pl1, F1, B, off1, W, C.R);
+#if DK_SMALL_PIPE >= 2
+        // Chunk k's results leave after chunk k + 1's window is in: the window wait (vmcnt, in order) then never
+        // waits for these stores, only for the DMA issued before chunk k's parse.
+        asm volatile("" ::: "memory");
+        if (rec.meta != kNoRec) {
+            st_res(P.res.meta + i, rec.meta);
+            st_res(P.res.src_ip + i, rec.src);
+            if (P.res.dst_ip) st_res(P.res.dst_ip + i, rec.dst);
+            st_res(P.res.ports + i, rec.ports);
+            st_res(P.res.payload + i, rec.pay);
+            st_res(P.res.flow_id + i, rec.fid);
+        }
+#endif
+#endif
+        DK_STAMP(4 + 3 * k);
         // rotate the pipeline
         have = have1;
         c = c1;
@@ -1327,8 +1392,15 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
+#ifdef DK_DIAG_STAMPS
+    DK_STAMP_T(14, __builtin_amdgcn_s_memtime());
+#endif
     __syncthreads();
     flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh, &s_last);
+#ifdef DK_DIAG_STAMPS
+    DK_STAMP_T(15, __builtin_amdgcn_s_memtime());
+    DK_STAMP_T(13, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
