@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Summarise tools/pmc_kernel.sh passes: per kernel, the mean over launches of every counter, plus derived figures
-(instructions per wave, VALU busy %, occupancy %, wait share). usage: tools/pmc_summary.py gpurun_out/pmc_<tag> [out.json]"""
+(instructions per wave, VALU busy %, occupancy %, wait share).
+usage: tools/pmc_summary.py gpurun_out/pmc_<tag> [out.json] [kernel_us]
+kernel_us: the kernel's average duration from a --kernel-trace run of the same build (the busy / occupancy shares are
+taken against it at 2.4 GHz, i.e. lower bounds; GRBM_GUI_ACTIVE read inconsistently across passes on this pool)."""
 import csv
 import glob
 import json
@@ -38,7 +41,17 @@ def main():
                        "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH"):
                 if cn in m:
                     der[cn + "_per_wave"] = round(m[cn] / w, 1)
-        if g:
+        us = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
+        if us:
+            cyc = us * 2400.0  # shader cycles at the 2.4 GHz ceiling
+            der["kernel_us_traced"] = us
+            if "SQ_ACTIVE_INST_VALU" in m:  # quad-cycles summed over the 4 SIMDs of every CU
+                der["VALUBusy_pct"] = round(100 * 4 * m["SQ_ACTIVE_INST_VALU"] / (4 * CU) / cyc, 1)
+            if "SQ_WAVE_CYCLES" in m:  # resident waves per CU / 32
+                der["OccupancyPercent"] = round(100 * 4 * m["SQ_WAVE_CYCLES"] / CU / cyc / 32, 1)
+            if "SQ_WAVE_CYCLES" in m and "SQ_WAIT_ANY" in m:
+                der["wait_any_share_of_wave_cycles"] = round(m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"], 3)
+        elif g:
             # gfx950: SQ_WAVE_CYCLES / SQ_ACTIVE_* count quad-cycles (MI355X_MICROARCH.md constants table)
             if "SQ_ACTIVE_INST_VALU" in m:
                 der["VALUBusy_pct"] = round(100 * m["SQ_ACTIVE_INST_VALU"] / CU / g, 1)
