@@ -191,6 +191,11 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride) {
 
 // Choose the flow-count mode and the persistent grid, then launch on `stream` with that stream's counter scratch.
 // size_hint = bytes of blob the batch covers (the family and grid follow the mean bytes per frame).
+#ifndef DK_SPLIT2_MIN_BYTES
+#define DK_SPLIT2_MIN_BYTES (1u << 30)  // mixed-size batches: the split kernel with 2 finishers per stream wave
+#endif
+constexpr uint64_t kSplit2MinBytes = DK_SPLIT2_MIN_BYTES;
+
 int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t stream) {
     if (p.n == 0) return 0;
     const Tuning& T = c->tune;
@@ -222,14 +227,15 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     // Never more workgroups per CU than the occupancy admits (large socket tables take LDS).
     const uint64_t bytes_per_frame = size_hint / p.n;
     p.stage = bytes_per_frame >= 128 ? 1u : 0u;
-    p.split = bytes_per_frame >= 1024 ? 1u : 0u;
+    p.split = bytes_per_frame >= 1024 ? 1u : bytes_per_frame >= kSplit2MinBytes ? 2u : 0u;
     p.small = bytes_per_frame <= 96 ? 1u : 0u;
     if (T.stage >= 0) p.stage = T.stage ? 1u : 0u;
-    if (T.split >= 0) p.split = T.split ? 1u : 0u;
+    if (T.split >= 0) p.split = T.split == 2 ? 2u : T.split ? 1u : 0u;
     if (T.small >= 0) p.small = T.small ? 1u : 0u;
     if (p.small) p.split = p.stage = 0;
     p.sched = T.sched >= 0 ? (uint32_t)std::min(T.sched, 3) : 0u;
     const uint32_t family = p.small   ? dk::kFamilySmall
+                            : p.split == 2 ? dk::kFamilySplit2
                             : p.split ? dk::kFamilySplit
                             : p.stage ? dk::kFamilyStaged
                                       : dk::kFamilyUnstaged;

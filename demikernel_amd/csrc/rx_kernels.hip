@@ -509,23 +509,42 @@ __device__ __forceinline__ void small_load(const FrameDesc<kShift>& F, const Blo
 // (DPP row scan). A step = kRoundsPerStep rounds of 4 frames, all loads in flight together.
 struct CoopPlan {  // wave-uniform
     uint32_t ncoop;  // big frames in the chunk
-    uint32_t maxit;  // iterations per round (1 unless a frame exceeds kCoopSpan granules, i.e. > 1536 bytes)
+    uint32_t nmed;   // of which medium (<= kMedGran granules): ranks [0, nmed), streamed by the medium step shape
+    uint32_t maxit;  // iterations per round of the large shape (1 unless a frame exceeds kCoopSpan granules)
 };
+// Two step shapes, both with kRoundsPerStep * kCoopU = 12 loads in flight per lane: large frames (> kMedGran granules)
+// take kCoopU = 6 slots per lane (a 1536-byte quarter-wave span), medium ones (IMIX 576 B) half that at twice the
+// rounds. A 590-byte frame filled 37 of the 96 slots of the large shape; unused slots cost issue and in-flight
+// capacity (loads at kOob), so medium frames are ranked first and streamed 4 rounds per step.
+#ifndef DK_COOP_MED_U
+#define DK_COOP_MED_U 3  // 0: one shape for every big frame
+#endif
+constexpr uint32_t kMedU = DK_COOP_MED_U > 0 ? DK_COOP_MED_U : 1;
+constexpr uint32_t kMedR = (kRoundsPerStep * kCoopU) / kMedU;
+constexpr uint32_t kMedGran = DK_COOP_MED_U > 0 ? 16 * kMedU : 0;
+template <uint32_t U, uint32_t R>
 struct CoopStep {
-    CoopSlot sl[kRoundsPerStep];
-    uint4 d[kRoundsPerStep][kCoopU];
+    CoopSlot sl[R];
+    uint4 d[R][U];
 };
 
-// Per-rank records of the chunk's big frames in W.rec; wave-uniform plan. Ends with a wave barrier.
+// Per-rank records of the chunk's big frames in W.rec (medium frames first); wave-uniform plan. Ends with a wave
+// barrier.
 template <bool kShift>
 __device__ __forceinline__ CoopPlan coop_plan(const FrameDesc<kShift>& F, uint32_t lane, uint32_t off, WaveLds& W) {
     CoopPlan pl;
     const uint64_t cm = __ballot(F.big);
     pl.ncoop = (uint32_t)__popcll(cm);
+    pl.nmed = 0;
     pl.maxit = 1;
     if (pl.ncoop == 0) return pl;
+    const bool med = F.big && F.nblk <= kMedGran;
+    const uint64_t mm = __ballot(med), lm = cm & ~mm;
+    pl.nmed = (uint32_t)__popcll(mm);
     if (F.big) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+        const uint64_t m = med ? mm : lm;
+        const uint32_t rank = (med ? 0u : pl.nmed) +
+                              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         W.rec[rank] = make_uint2(lane | (F.nblk << 8), off - F.sh);  // one ds_read_b64 per round
     }
     if (__ballot(F.nblk > kCoopSpan)) {
@@ -540,15 +559,16 @@ __device__ __forceinline__ CoopPlan coop_plan(const FrameDesc<kShift>& F, uint32
     return pl;
 }
 
-// Slots of step r (rounds r .. r + kRoundsPerStep - 1) and the loads of its iteration 0.
-__device__ __forceinline__ void coop_issue(const CoopPlan& pl, uint32_t r, uint32_t lane, const WaveLds& W,
-                                           const Blob& B, CoopStep& S, uint32_t it) {
+// Slots of step r (ranks k0 + 4 (r .. r + R - 1) + quarter, below k1) and the loads of its iteration 0.
+template <uint32_t U, uint32_t R>
+__device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r, uint32_t lane, const WaveLds& W,
+                                           const Blob& B, CoopStep<U, R>& S, uint32_t it) {
     const uint32_t q = lane >> 4, l16 = lane & 15;
     if (it == 0) {
 #pragma unroll
-        for (uint32_t h = 0; h < kRoundsPerStep; h++) {
-            const uint32_t k = (r + h) * 4 + q;
-            S.sl[h].has = k < pl.ncoop;
+        for (uint32_t h = 0; h < R; h++) {
+            const uint32_t k = k0 + (r + h) * 4 + q;
+            S.sl[h].has = k < k1;
             const uint2 rec = S.sl[h].has ? W.rec[k] : make_uint2(0, 0);
             S.sl[h].j = rec.x & 0xFFu;
             S.sl[h].nb = rec.x >> 8;  // 0 for an empty slot: every load is then out of range
@@ -556,41 +576,24 @@ __device__ __forceinline__ void coop_issue(const CoopPlan& pl, uint32_t r, uint3
             S.sl[h].acc = 0;
         }
     }
-    const uint32_t b0 = it * kCoopSpan + l16;
-#if DK_COOP_SKIP
-    // Load slots past the largest frame of a round are not issued (wave-uniform): a 590-byte IMIX frame fills 3 of a
-    // quarter's 6 slots, and an out-of-range load still costs an issue slot and its vmcnt turn.
-    uint32_t mx[kRoundsPerStep];
+    const uint32_t b0 = it * 16 * U + l16;
 #pragma unroll
-    for (uint32_t h = 0; h < kRoundsPerStep; h++) {
-        const uint32_t nb = S.sl[h].nb;
-        mx[h] = max(max(__builtin_amdgcn_readlane(nb, 0), __builtin_amdgcn_readlane(nb, 16)),
-                    max(__builtin_amdgcn_readlane(nb, 32), __builtin_amdgcn_readlane(nb, 48)));
-    }
-#endif
+    for (uint32_t h = 0; h < R; h++)
 #pragma unroll
-    for (uint32_t h = 0; h < kRoundsPerStep; h++)
-#pragma unroll
-        for (uint32_t u = 0; u < kCoopU; u++) {
+        for (uint32_t u = 0; u < U; u++) {
             const uint32_t b = b0 + 16 * u;
-#if DK_COOP_SKIP
-            if (u > 0 && it * kCoopSpan + 16 * u >= mx[h]) {
-                S.d[h][u] = make_uint4(0, 0, 0, 0);
-                continue;
-            }
-#endif
             S.d[h][u] = B.template ld<DK_NT_LOADS != 0>(b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob);
         }
 }
 
-template <bool kShift>
-__device__ __forceinline__ void coop_consume(CoopStep& S, WaveLds& W, uint32_t lane, uint32_t it) {
+template <bool kShift, uint32_t U, uint32_t R>
+__device__ __forceinline__ void coop_consume(CoopStep<U, R>& S, WaveLds& W, uint32_t lane, uint32_t it) {
     constexpr uint32_t kHdrGran = kShift ? 5u : 4u;  // header granules the owner lane needs
-    const uint32_t l16 = lane & 15, b0 = it * kCoopSpan + l16;
+    const uint32_t l16 = lane & 15, b0 = it * 16 * U + l16;
 #pragma unroll
-    for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+    for (uint32_t h = 0; h < R; h++) {
 #pragma unroll
-        for (uint32_t u = 0; u < kCoopU; u++) {
+        for (uint32_t u = 0; u < U; u++) {
             S.sl[h].acc = block_sum(S.d[h][u], S.sl[h].acc);
             if (b0 + 16 * u + 1 == S.sl[h].nb) W.tail[S.sl[h].j] = S.d[h][u];  // nb == 0: never
         }
@@ -599,16 +602,16 @@ __device__ __forceinline__ void coop_consume(CoopStep& S, WaveLds& W, uint32_t l
 }
 
 // Finish step r whose iteration-0 loads are in flight in S: consume them, run the remaining iterations, reduce.
-template <bool kShift>
-__device__ __forceinline__ void coop_finish(const CoopPlan& pl, uint32_t r, uint32_t lane, WaveLds& W, const Blob& B,
-                                            CoopStep& S) {
+template <bool kShift, uint32_t U, uint32_t R>
+__device__ __forceinline__ void coop_finish(uint32_t k0, uint32_t k1, uint32_t maxit, uint32_t r, uint32_t lane,
+                                            WaveLds& W, const Blob& B, CoopStep<U, R>& S) {
     coop_consume<kShift>(S, W, lane, 0);
-    for (uint32_t it = 1; it < pl.maxit; it++) {
-        coop_issue(pl, r, lane, W, B, S, it);
+    for (uint32_t it = 1; it < maxit; it++) {
+        coop_issue(k0, k1, r, lane, W, B, S, it);
         coop_consume<kShift>(S, W, lane, it);
     }
 #pragma unroll
-    for (uint32_t h = 0; h < kRoundsPerStep; h++) {
+    for (uint32_t h = 0; h < R; h++) {
         // Quarter = DPP row of 16 lanes: inclusive row scan by row_shr 1/2/4/8; lane 15 holds the sum.
         uint32_t acc = S.sl[h].acc;
         acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xF, 0xF, false);
@@ -616,6 +619,23 @@ __device__ __forceinline__ void coop_finish(const CoopPlan& pl, uint32_t r, uint
         acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x114, 0xF, 0xF, false);
         acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x118, 0xF, 0xF, false);
         if (S.sl[h].has && (lane & 15) == 15) W.csum[S.sl[h].j] = acc;
+    }
+}
+
+// Phase B of one chunk: the medium frames' steps, then the large frames' steps.
+template <bool kShift>
+__device__ __forceinline__ void coop_stream(const CoopPlan& pl, uint32_t lane, WaveLds& W, const Blob& B) {
+#if DK_COOP_MED_U > 0
+    for (uint32_t r = 0; r * 4 < pl.nmed; r += kMedR) {
+        CoopStep<kMedU, kMedR> S;
+        coop_issue(0, pl.nmed, r, lane, W, B, S, 0);
+        coop_finish<kShift>(0, pl.nmed, 1, r, lane, W, B, S);
+    }
+#endif
+    for (uint32_t r = 0; r * 4 < pl.ncoop - pl.nmed; r += kRoundsPerStep) {
+        CoopStep<kCoopU, kRoundsPerStep> S;
+        coop_issue(pl.nmed, pl.ncoop, r, lane, W, B, S, 0);
+        coop_finish<kShift>(pl.nmed, pl.ncoop, pl.maxit, r, lane, W, B, S);
     }
 }
 
@@ -668,11 +688,7 @@ __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t fra
     const Blob B(frames, frames_bytes);
     small_load(F, B, off, C.R);
     const CoopPlan pl = coop_plan(F, lane, off, W);
-    for (uint32_t r = 0; r * 4 < pl.ncoop; r += kRoundsPerStep) {
-        CoopStep S;
-        coop_issue(pl, r, lane, W, B, S, 0);
-        coop_finish<kShift>(pl, r, lane, W, B, S);
-    }
+    coop_stream<kShift>(pl, lane, W, B);
     coop_gather(F, pl, lane, W, C);
 }
 
@@ -684,9 +700,19 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WL& W, ui
                                                  int E, bool& resum) {
     const RegAcc& R = C.R;
     if (!C.big) {
-        // [34, E) inside the register window: block 2 (bytes 32..47) and block 3 (48..63)
-        const uint32_t s = block_sum_masked(R.w[8], R.w[9], R.w[10], R.w[11], 2, min(E, 48) - 32, 0);
-        return block_sum_masked(R.w[12], R.w[13], R.w[14], R.w[15], 0, min(E, 64) - 48, s);
+        // [34, E) inside the register window, E even in [34, 64]: dword k keeps its bytes below E, i.e. the low
+        // 32 - sh bits with sh = clamp(32 - 8 (E - 4k), 0, 32) — one 64-bit shift per dword instead of two clamped
+        // byte-mask computations (C3: -30 VALU per frame).
+        const int t = 32 - 8 * E;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 8; k < 16; k++) {
+            const uint32_t sh = (uint32_t)min(max(t + 32 * k, 0), 32);
+            uint32_t m = (uint32_t)(0xFFFFFFFFull >> sh);
+            if (k == 8) m &= 0xFFFF0000u;  // bytes 32, 33 are the IPv4 header's
+            acc = hsum2(R.w[k] & m, acc);
+        }
+        return acc;
     }
     if ((int)(16 * C.nblk - C.sh) - E <= 16) {
         uint32_t pre = block_sum(make_uint4(R.w[0], R.w[1], R.w[2], R.w[3]), 0);
@@ -1403,24 +1429,35 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 #endif
 }
 
-// Split kernel (large frames): one 512-thread workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their
-// chunk p into LDS buffer p % 2 (header windows, last granules, whole-frame sums) while finish waves 4..7 run phase C
-// of chunk p - 1 from the other buffer; one workgroup barrier per period. The streaming waves never stop for parse,
-// demux, counters or result stores — 4 streaming waves per CU is also the count at which the read probe peaks — and
-// the finish waves stage their results in registers (kSplitStageK chunks, 256 VGPRs at 2 waves/SIMD) for one burst
-// at exit. Stream wave w and finish wave w + 4 walk the same chunk sequence (sched 0 over 4 waves per workgroup).
-constexpr int kSplitBlock = 512;
-#ifndef DK_SPLIT_STAGE_K
-#define DK_SPLIT_STAGE_K 16
+// Split kernel: one workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their chunks (sched 0 over the 4
+// stream waves of each workgroup) into LDS buffers (header windows, last granules, whole-frame sums; frames of <= 64
+// bytes ride along as their register window), and kFin finish waves per stream wave run phase C (parse, checksum,
+// options, demux, counters, results) from those buffers: finisher f of stream wave w takes w's chunks p with
+// p % kFin == f. The streaming waves never stop for parse, demux, counters or result stores — 4 streaming waves per CU
+// is also the count at which the read probe peaks — and the finish waves stage their results in registers for one
+// burst per kStg chunks.
+//   kFin = 1 (512 threads, 2 waves/SIMD, 256 VGPRs, 16 staged chunks): large frames (C2, C5), where phase C is a small
+//     share of a chunk's time;
+//   kFin = 2 (768 threads, 3 waves/SIMD, 168 VGPRs, 4 staged chunks): mixed sizes (IMIX), where phase C of 64 frames
+//     costs as much as streaming them and one finisher per stream wave was the bottleneck.
+#ifndef DK_SPLIT2_STAGE_K
+#define DK_SPLIT2_STAGE_K 4
 #endif
-constexpr int kSplitStageK = DK_SPLIT_STAGE_K;
-__device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[kSplitStageK], uint32_t nst,
-                                            const WaveRange& r, uint32_t k_last) {
+template <int kFin>
+struct SplitShape {
+    static constexpr int kThreads = 64 * kWaves * (1 + kFin);
+    static constexpr int kBufs = kFin == 1 ? 3 : kFin + 1;  // LDS buffers per stream wave
+    static constexpr int kStg = kFin == 1 ? 16 : kFin == 2 ? DK_SPLIT2_STAGE_K : 2;  // chunks of results a finish wave stages
+};
+constexpr int kSplitBlock = SplitShape<1>::kThreads;  // the TX split kernel's shape
+template <int kStgK>
+__device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[kStgK], uint32_t nst,
+                                            const WaveRange& r, uint32_t k_last, uint32_t stride) {
 #pragma unroll
-    for (int q = kSplitStageK - 1; q >= 0; q--) {
+    for (int q = kStgK - 1; q >= 0; q--) {
         if ((uint32_t)q >= nst) continue;
         uint32_t c, lim;
-        (void)r.chunk(k_last - (uint32_t)q, c, lim);
+        (void)r.chunk(k_last - (uint32_t)q * stride, c, lim);
         if (stg[q].meta == kNoRec) continue;
         const uint32_t i = c + r.lane_off;
         st_res(P.res.meta + i, stg[q].meta);
@@ -1432,14 +1469,9 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
     }
 }
 
-// Hand-off between a stream wave and its finish wave: kSplitBufs LDS buffers per pair with a ready word (chunk + 1
-// written, set by the stream wave) and a free word (chunk + 1 finished, set by the finish wave), so each stream wave
-// runs up to kSplitBufs - 1 chunks ahead of its finisher and no wave waits for the other seven at a workgroup barrier
-// (DK_SPLIT_BUFS 0: the round-1 form, two buffers and one __syncthreads per period).
-#ifndef DK_SPLIT_BUFS
-#define DK_SPLIT_BUFS 3
-#endif
-constexpr int kSplitBufs = DK_SPLIT_BUFS > 0 ? DK_SPLIT_BUFS : 2;
+// Hand-off through kBufs LDS buffers per stream wave (chunk p in buffer p % kBufs), each with a ready word (p + 1:
+// written, set by the stream wave) and a free word (p + 1: read out, set by the finish wave that took p). A stream wave
+// runs up to kBufs - 1 chunks ahead of the slowest finisher and no wave waits at a workgroup barrier.
 typedef __attribute__((address_space(3))) uint32_t lu32;
 __device__ __forceinline__ void lds_wait_eq(uint32_t* w, uint32_t want) {
     while (__hip_atomic_load((lu32*)w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
@@ -1449,10 +1481,13 @@ __device__ __forceinline__ void lds_publish(uint32_t* w, uint32_t v) {
     __hip_atomic_store((lu32*)w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <bool kShift>
-__global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P) {
-    __shared__ WaveLds s_buf[kSplitBufs][kWaves];  // [chunk % kSplitBufs][stream wave]
-    __shared__ uint32_t s_ready[kWaves][kSplitBufs], s_free[kWaves][kSplitBufs];
+template <bool kShift, int kFin>
+__global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_kernel(RxParams P) {
+    using S = SplitShape<kFin>;
+    constexpr int kBufs = S::kBufs;
+    constexpr int kStg = S::kStg;
+    __shared__ WaveLds s_buf[kBufs][kWaves];  // [chunk % kBufs][stream wave]
+    __shared__ uint32_t s_ready[kWaves][kBufs], s_free[kWaves][kBufs];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
     __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
@@ -1461,11 +1496,12 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6, sw = wv & (kWaves - 1);
     const bool finisher = wv >= (uint32_t)kWaves;
+    const uint32_t fin = finisher ? (wv - kWaves) / kWaves : 0u;  // which of the stream wave's finishers
     const bool lds_flows = P.flow_mode == kFlowLds;
-    for (uint32_t k = tid; k < DK_V_COUNT; k += kSplitBlock) s_vh[k] = 0;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += S::kThreads) s_vh[k] = 0;
     if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += kSplitBlock) s_flow[k] = 0;
-    if (tid < kWaves * kSplitBufs) {
+        for (uint32_t k = tid; k < P.flow_words; k += S::kThreads) s_flow[k] = 0;
+    if (tid < kWaves * kBufs) {
         (&s_ready[0][0])[tid] = 0;
         (&s_free[0][0])[tid] = 0;
     }
@@ -1473,12 +1509,12 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
     const Blob B(P.frames, P.frames_bytes);
-    Rec stg[kSplitStageK];
+    Rec stg[kStg];
     uint32_t nstg = 0, klast = 0;
-#if DK_SPLIT_BUFS > 0
     uint32_t c, lim;
-    for (uint32_t p = 0; r.chunk(p, c, lim); p++) {
-        const uint32_t b = p % kSplitBufs;
+    const uint32_t p0 = finisher ? fin : 0u, dp = finisher ? (uint32_t)kFin : 1u;
+    for (uint32_t p = p0; r.chunk(p, c, lim); p += dp) {
+        const uint32_t b = p % kBufs;
         WaveLds& W = s_buf[b][sw];
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1489,13 +1525,9 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
             // through the LDS header slot too, so the finish wave never waits on frame memory (IMIX: 7 of 12 frames)
             RegAcc Rs;
             small_load(F, B, off, Rs);
-            if (p >= (uint32_t)kSplitBufs) lds_wait_eq(&s_free[sw][b], p - kSplitBufs + 1);  // buffer read out
+            if (p >= (uint32_t)kBufs) lds_wait_eq(&s_free[sw][b], p - kBufs + 1);  // buffer read out
             const CoopPlan pl = coop_plan(F, lane, off, W);
-            for (uint32_t rr = 0; rr * 4 < pl.ncoop; rr += kRoundsPerStep) {
-                CoopStep S;
-                coop_issue(pl, rr, lane, W, B, S, 0);
-                coop_finish<kShift>(pl, rr, lane, W, B, S);
-            }
+            coop_stream<kShift>(pl, lane, W, B);
             if (F.vec && !F.big)
 #pragma unroll
                 for (int k = 0; k < 4; k++)
@@ -1513,7 +1545,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
                     C.R.w[4 * k + 2] = h.z;
                     C.R.w[4 * k + 3] = h.w;
                 }
-            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 1};
+            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 0, 1};
             coop_gather(F, pl, lane, W, C);
             uint32_t v, fid;
             Rec rec;
@@ -1521,66 +1553,19 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
             rx_finish<kShift, true>(P, i, live, lane, W, off, len, C, v, fid, rec);
             if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
 #pragma unroll
-            for (int q = kSplitStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
+            for (int q = kStg - 1; q > 0; q--) stg[q] = stg[q - 1];
             stg[0] = rec;
             klast = p;
-            if (++nstg == kSplitStageK) {
-                flush_split(P, stg, nstg, r, klast);
+            if (++nstg == (uint32_t)kStg) {
+                flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
                 nstg = 0;
             }
             count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         }
     }
     __syncthreads();
-#else
-    const WaveRange r0 = wave_range(0, P.n, 0, lane);  // stream wave 0 has the most chunks
-    uint32_t nper = 0, c0, l0;
-    while (r0.chunk(nper, c0, l0)) nper++;
-    for (uint32_t p = 0; p <= nper; p++) {
-        uint32_t c, lim;
-        if (!finisher) {
-            if (r.chunk(p, c, lim)) {
-                WaveLds& W = s_buf[p & 1][sw];
-                const uint32_t i = c + r.lane_off;
-                const bool live = i < lim;
-                const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
-                const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
-                const CoopPlan pl = coop_plan(F, lane, off, W);
-                for (uint32_t rr = 0; rr * 4 < pl.ncoop; rr += kRoundsPerStep) {
-                    CoopStep S;
-                    coop_issue(pl, rr, lane, W, B, S, 0);
-                    coop_finish<kShift>(pl, rr, lane, W, B, S);
-                }
-            }
-        } else if (p > 0 && r.chunk(p - 1, c, lim)) {
-            WaveLds& W = s_buf[(p - 1) & 1][sw];
-            const uint32_t i = c + r.lane_off;
-            const bool live = i < lim;
-            const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
-            const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
-            Chunk C;
-            small_load(F, B, off, C.R);
-            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 1};
-            coop_gather(F, pl, lane, W, C);
-            uint32_t v, fid;
-            Rec rec;
-            rec.meta = kNoRec;
-            rx_finish<kShift, true>(P, i, live, lane, W, off, len, C, v, fid, rec);
-#pragma unroll
-            for (int q = kSplitStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
-            stg[0] = rec;
-            klast = p - 1;
-            if (++nstg == kSplitStageK) {
-                flush_split(P, stg, nstg, r, klast);
-                nstg = 0;
-            }
-            count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
-        }
-        __syncthreads();
-    }
-#endif
-    if (finisher && nstg) flush_split(P, stg, nstg, r, klast);
-    flush_counters(P, tid, kSplitBlock, lds_flows, s_flow, s_vh, &s_last);
+    if (finisher && nstg) flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
+    flush_counters(P, tid, S::kThreads, lds_flows, s_flow, s_vh, &s_last);
 }
 
 // Adds the per-workgroup rows of flow_scratch[rows][row_words] into the caller's u64 counters: columns
@@ -1588,7 +1573,10 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_rx_split_kernel(RxParams P)
 // (verdict_counts). Block (x, y) = 64 columns x kReduceRows rows: wave w sums every 4th row of the block's rows (lane =
 // column: 256-byte row pieces, 8 independent loads in flight per lane), the 4 waves combine in LDS and the block adds
 // its 64-bit partials with device-scope atomics: rows / kReduceRows adds per counter.
-constexpr uint32_t kReduceRows = 64;
+#ifndef DK_REDUCE_ROWS
+#define DK_REDUCE_ROWS 64
+#endif
+constexpr uint32_t kReduceRows = DK_REDUCE_ROWS;
 constexpr uint32_t kReduceCols = 64;
 __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* scratch, uint32_t rows,
                                                                 uint32_t row_words, uint32_t row_stride, uint32_t flow_words,
@@ -1833,11 +1821,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
                 const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
                 const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
                 const CoopPlan pl = coop_plan(F, lane, off, W);
-                for (uint32_t rr = 0; rr * 4 < pl.ncoop; rr += kRoundsPerStep) {
-                    CoopStep S;
-                    coop_issue(pl, rr, lane, W, B, S, 0);
-                    coop_finish<true>(pl, rr, lane, W, B, S);
-                }
+                coop_stream<true>(pl, lane, W, B);
             }
         } else if (p > 0 && r.chunk(p - 1, c, lim)) {
             WaveLds& W = s_buf[(p - 1) & 1][sw];
@@ -1847,7 +1831,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
             const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
             Chunk C;
             small_load(F, B, off, C.R);
-            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 1};
+            const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 0, 1};
             coop_gather(F, pl, lane, W, C);
 #if DK_TX_STAGE_K > 0
             TxWin win;
@@ -1902,8 +1886,11 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     int blocks = 0;
     hipError_t e;
-    if (family == dk::kFamilySplit)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true>, dk::kSplitBlock,
+    if (family == dk::kFamilySplit2)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 2>,
+                                                          dk::SplitShape<2>::kThreads, dyn_lds_bytes);
+    else if (family == dk::kFamilySplit)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 1>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
     else if (family == dk::kFamilySmall)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kSmallBlock,
@@ -1928,10 +1915,16 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.split == 2 && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 2>), dim3(grid), dim3(dk::SplitShape<2>::kThreads), dyn, s,
+                           p);
+    else if (p.split == 2)
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<true, 2>), dim3(grid), dim3(dk::SplitShape<2>::kThreads), dyn, s,
+                           p);
     else if (p.split && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_split_kernel<false>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 1>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split)
-        hipLaunchKernelGGL((dk::dk_rx_split_kernel<true>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<true, 1>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.aligned16 && p.stage)
         hipLaunchKernelGGL((dk::dk_rx_kernel<false, true>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     else if (p.aligned16)

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--modes", default="3,4,6,7,8")
     ap.add_argument("--grids", default="256,512,768,1024")
     ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
+    ap.add_argument("--lib", default=None, help="a variant libdk_rx.so (tools/variants.sh) instead of the in-tree one")
     args = ap.parse_args()
 
     import torch
@@ -53,8 +54,7 @@ def main():
     import bench
     from demikernel_amd import Config, RxEngine, synth
     from demikernel_amd import _native as N
-
-    eng = RxEngine(Config(synth.BOB_IPV4))
+    eng = RxEngine(Config(synth.BOB_IPV4), lib_path=os.path.abspath(args.lib) if args.lib else None)
     batch, flows, tr = bench.make_batch(eng, args.workload, 0, synth.SEED, 1)
     rot = [batch] + [bench.make_batch(eng, args.workload, 0, synth.SEED + 1000 * k, 1)[0] for k in range(1, args.rotate)]
     res = eng.results(batch.n, counts=not args.no_counts)
