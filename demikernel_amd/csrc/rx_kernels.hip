@@ -512,12 +512,13 @@ struct CoopPlan {  // wave-uniform
     uint32_t nmed;   // of which medium (<= kMedGran granules): ranks [0, nmed), streamed by the medium step shape
     uint32_t maxit;  // iterations per round of the large shape (1 unless a frame exceeds kCoopSpan granules)
 };
-// Two step shapes, both with kRoundsPerStep * kCoopU = 12 loads in flight per lane: large frames (> kMedGran granules)
-// take kCoopU = 6 slots per lane (a 1536-byte quarter-wave span), medium ones (IMIX 576 B) half that at twice the
-// rounds. A 590-byte frame filled 37 of the 96 slots of the large shape; unused slots cost issue and in-flight
-// capacity (loads at kOob), so medium frames are ranked first and streamed 4 rounds per step.
+// Step shapes, both with kRoundsPerStep * kCoopU = 12 loads in flight per lane: kCoopU = 6 slots per lane (a 1536-byte
+// quarter-wave span) for every big frame, or (DK_COOP_MED_U = 3) medium frames (<= kMedGran granules, IMIX 576 B)
+// ranked first and streamed with half the span at twice the rounds. A 590-byte frame fills 37 of the 96 slots of
+// the large shape, but the medium shape measured no gain (IMIX +0.7 %, C2 ±0): the slots at kOob cost
+// neither memory traffic nor, it turns out, time.
 #ifndef DK_COOP_MED_U
-#define DK_COOP_MED_U 3  // 0: one shape for every big frame
+#define DK_COOP_MED_U 0  // 3: medium frames take the half-span shape (measured IMIX +0.7 %, C2 ±0: off)
 #endif
 constexpr uint32_t kMedU = DK_COOP_MED_U > 0 ? DK_COOP_MED_U : 1;
 constexpr uint32_t kMedR = (kRoundsPerStep * kCoopU) / kMedU;
