@@ -231,10 +231,11 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.small = bytes_per_frame <= 96 ? 1u : 0u;
     if (T.stage >= 0) p.stage = T.stage ? 1u : 0u;
     if (T.split >= 0) p.split = T.split == 2 ? 2u : T.split ? 1u : 0u;
-    if (T.small >= 0) p.small = T.small ? 1u : 0u;
+    if (T.small >= 0) p.small = T.small == 2 ? 2u : T.small ? 1u : 0u;
     if (p.small) p.split = p.stage = 0;
     p.sched = T.sched >= 0 ? (uint32_t)std::min(T.sched, 3) : 0u;
-    const uint32_t family = p.small   ? dk::kFamilySmall
+    const uint32_t family = p.small == 2 ? dk::kFamilySmallSplit
+                            : p.small ? dk::kFamilySmall
                             : p.split == 2 ? dk::kFamilySplit2
                             : p.split ? dk::kFamilySplit
                             : p.stage ? dk::kFamilyStaged
@@ -247,7 +248,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u);
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
-    const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
+    const uint32_t tiles_per_wg = p.small == 2 ? 2u : p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
     uint32_t grid = std::min((ntiles + tiles_per_wg - 1) / tiles_per_wg, per_cu * c->cu_count);
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)

@@ -1206,9 +1206,9 @@ struct WinPlan {
     uint32_t lo;  // blob offset of the window's first granule
 };
 // Issue the chunk's window DMA if its frames lie in one window (the wave's window slot must no longer be read).
-template <bool kShift>
+template <bool kShift, class WL>
 __device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F, const Blob& B, uint32_t off,
-                                                      uint32_t len, bool live, uint32_t lane, SmallLds& W) {
+                                                      uint32_t len, bool live, uint32_t lane, WL& W) {
     WinPlan pl{false, 0};
 #ifndef DK_SMALL_NOWIN
     const bool use = F.vec && !F.big;
@@ -1233,9 +1233,9 @@ __device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F
     return pl;
 }
 // The chunk's register windows: from the DMA'd window in LDS, or by per-lane loads (scattered frames).
-template <bool kShift>
+template <bool kShift, class WL>
 __device__ __forceinline__ void small_window_read(const WinPlan& pl, const FrameDesc<kShift>& F, const Blob& B,
-                                                  uint32_t off, SmallLds& W, RegAcc& R) {
+                                                  uint32_t off, WL& W, RegAcc& R) {
     if (pl.win) {
         const uint32_t b = F.vec && !F.big ? (off - F.sh - pl.lo) >> 4 : 0u;
 #pragma unroll
@@ -1252,9 +1252,9 @@ __device__ __forceinline__ void small_window_read(const WinPlan& pl, const Frame
     small_load(F, B, off, R);
 }
 
-template <bool kShift>
+template <bool kShift, class WL>
 __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uint32_t lane, uint32_t off, const Blob& B,
-                                                 SmallLds& W, Chunk& C) {
+                                                 WL& W, Chunk& C) {
     RegAcc& R = C.R;
     uint32_t x[4] = {0, 0, 0, 0};
     C.fsum = 0;
@@ -1430,6 +1430,137 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 #endif
 }
 
+// LDS flag words between the waves of a workgroup (the split kernels' hand-off): acquire spin, release publish.
+typedef __attribute__((address_space(3))) uint32_t lu32;
+__device__ __forceinline__ void lds_wait_eq(uint32_t* w, uint32_t want) {
+    while (__hip_atomic_load((lu32*)w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
+        __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void lds_publish(uint32_t* w, uint32_t v) {
+    __hip_atomic_store((lu32*)w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Small-frame split kernel (DK_RX_SMALL=2): the small-frame kernel's chunk chain without the frame read on it.
+// 512-thread workgroups, two per CU: DK_SS_STREAM stream waves load descriptors and DMA each chunk's frame window into
+// LDS for their finish waves (2 buffers per finisher, ready / free words as in the split kernel); the other waves
+// read their frames from LDS and run phase C. A finisher's chain per chunk is then LDS read -> parse -> table probe ->
+// stores, and its vmcnt never waits for a window in flight. Scattered chunks (frames beyond one 4.5 KiB window) and
+// frames past the 64-byte register window are loaded by the finisher itself.
+#ifndef DK_SS_STREAM
+#define DK_SS_STREAM 2  // stream waves per 8-wave workgroup (divides the 8 - DK_SS_STREAM finish waves)
+#endif
+constexpr uint32_t kSsStream = DK_SS_STREAM, kSsFin = 8 - DK_SS_STREAM, kSsWaves = 8, kSsBlock = 64 * kSsWaves;
+constexpr uint32_t kSsPer = kSsFin / kSsStream;  // finishers per stream wave
+static_assert(kSsPer * kSsStream == kSsFin, "stream waves must divide the finish waves");
+struct SsBuf {
+    uint4 win[kWinLoads * 64];  // the chunk's frame window
+    uint2 desc[64];             // {off, len} per lane (0, 0 for lanes past the chunk)
+    uint32_t lo, win_ok;        // window base (blob offset of its first granule); 1 if the window holds every frame
+};
+struct SsView {  // what the shared small-frame helpers read as W: the window and the finisher's tail slots
+    uint4* win;
+    uint4* tail;
+};
+template <bool kShift, bool kOpt>
+__global__ __launch_bounds__(kSsBlock, 2) void dk_rx_small_split_kernel(RxParams P) {
+    __shared__ SsBuf s_buf[kSsFin][2];
+    __shared__ uint4 s_tail[kSsFin][64];
+    __shared__ uint32_t s_ready[kSsFin][2], s_free[kSsFin][2];
+    __shared__ uint32_t s_vh[DK_V_COUNT];
+    __shared__ uint32_t s_last;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6;
+    const bool lds_flows = P.flow_mode == kFlowLds;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kSsBlock) s_vh[k] = 0;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += kSsBlock) s_flow[k] = 0;
+    if (tid < kSsFin * 2) {
+        (&s_ready[0][0])[tid] = 0;
+        (&s_free[0][0])[tid] = 0;
+    }
+    __syncthreads();
+    const Blob B(P.frames, P.frames_bytes);
+    // finisher f of workgroup b walks chunks (gf + k nf) * 64, gf = b * kSsFin + f (sched 0 over the finish waves)
+    const uint32_t nf = gridDim.x * kSsFin;
+    if (wv < kSsStream) {
+        // stream wave s serves finishers s, s + kSsStream, ...
+        uint32_t off[kSsPer], len[kSsPer];
+        bool has[kSsPer];
+        auto load_desc = [&](uint32_t k) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSsPer; j++) {
+                const uint32_t gf = blockIdx.x * kSsFin + wv + kSsStream * j;
+                const uint32_t c = (gf + k * nf) * 64u;
+                has[j] = c < P.n;
+                const uint32_t i = c + lane;
+                off[j] = has[j] && i < P.n ? P.off[i] : 0u;
+                len[j] = has[j] && i < P.n ? P.len[i] : 0u;
+            }
+        };
+        load_desc(0);
+        for (uint32_t k = 0; has[0]; k++) {  // finisher wv has the most chunks of this wave's finishers
+            const uint32_t b = k & 1;
+#pragma unroll
+            for (uint32_t j = 0; j < kSsPer; j++) {
+                if (!has[j]) continue;
+                const uint32_t f = wv + kSsStream * j;
+                SsBuf& SB = s_buf[f][b];
+                if (k >= 2) lds_wait_eq(&s_free[f][b], k - 1);  // chunk k - 2 read out of this buffer
+                const uint32_t c = (blockIdx.x * kSsFin + f + k * nf) * 64u;
+                const bool live = c + lane < P.n;
+                const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off[j], len[j]);
+                SsView V{SB.win, nullptr};
+                const WinPlan pl = small_window_issue(F, B, off[j], len[j], live, lane, V);
+                SB.desc[lane] = make_uint2(off[j], len[j]);
+                if (lane == 0) {
+                    SB.lo = pl.lo;
+                    SB.win_ok = pl.win ? 1u : 0u;
+                }
+            }
+            bool h[kSsPer];
+#pragma unroll
+            for (uint32_t j = 0; j < kSsPer; j++) h[j] = has[j];
+            load_desc(k + 1);                                  // next descriptors in flight with the windows
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // windows (LDS-DMA) and records written
+            if (lane == 0)
+#pragma unroll
+                for (uint32_t j = 0; j < kSsPer; j++)
+                    if (h[j]) lds_publish(&s_ready[wv + kSsStream * j][b], k + 1);
+        }
+    } else {
+        const uint32_t f = wv - kSsStream;
+        const uint32_t gf = blockIdx.x * kSsFin + f;
+        SsView V{nullptr, s_tail[f]};
+        for (uint32_t k = 0; (gf + k * nf) * 64u < P.n; k++) {
+            const uint32_t b = k & 1;
+            SsBuf& SB = s_buf[f][b];
+            const uint32_t c = (gf + k * nf) * 64u;
+            const uint32_t i = c + lane;
+            const bool live = i < P.n;
+            lds_wait_eq(&s_ready[f][b], k + 1);
+            const uint2 d = SB.desc[lane];
+            const uint32_t off = d.x, len = d.y;
+            const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
+            Chunk C;
+            V.win = SB.win;
+            const WinPlan pl{SB.win_ok != 0, SB.lo};
+            small_window_read(pl, F, B, off, V, C.R);
+            if (lane == 0) lds_publish(&s_free[f][b], k + 1);  // after this wave's reads of the buffer (release)
+            small_big_frames(F, lane, off, B, V, C);
+            uint32_t v, fid;
+            Rec rec;
+            rec.meta = kNoRec;
+            rx_finish<kShift, false, SsView, kOpt>(P, i, live, lane, V, off, len, C, v, fid, rec);
+            count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+        }
+    }
+    __syncthreads();
+    flush_counters(P, tid, kSsBlock, lds_flows, s_flow, s_vh, &s_last);
+}
+
 // Split kernel: one workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their chunks (sched 0 over the 4
 // stream waves of each workgroup) into LDS buffers (header windows, last granules, whole-frame sums; frames of <= 64
 // bytes ride along as their register window), and kFin finish waves per stream wave run phase C (parse, checksum,
@@ -1473,14 +1604,6 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
 // Hand-off through kBufs LDS buffers per stream wave (chunk p in buffer p % kBufs), each with a ready word (p + 1:
 // written, set by the stream wave) and a free word (p + 1: read out, set by the finish wave that took p). A stream wave
 // runs up to kBufs - 1 chunks ahead of the slowest finisher and no wave waits at a workgroup barrier.
-typedef __attribute__((address_space(3))) uint32_t lu32;
-__device__ __forceinline__ void lds_wait_eq(uint32_t* w, uint32_t want) {
-    while (__hip_atomic_load((lu32*)w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
-        __builtin_amdgcn_s_sleep(1);
-}
-__device__ __forceinline__ void lds_publish(uint32_t* w, uint32_t v) {
-    __hip_atomic_store((lu32*)w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 template <bool kShift, int kFin>
 __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_kernel(RxParams P) {
@@ -1893,6 +2016,9 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     else if (family == dk::kFamilySplit)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 1>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
+    else if (family == dk::kFamilySmallSplit)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_split_kernel<true, true>,
+                                                          dk::kSsBlock, dyn_lds_bytes);
     else if (family == dk::kFamilySmall)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kSmallBlock,
                                                           dyn_lds_bytes);
@@ -1910,7 +2036,13 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
-    if (p.small && p.aligned16)
+    if (p.small == 2 && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<false, true>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
+    else if (p.small == 2 && opt)
+        hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<true, true>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
+    else if (p.small == 2)
+        hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<true, false>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
+    else if (p.small && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
