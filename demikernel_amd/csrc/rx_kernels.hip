@@ -42,6 +42,9 @@ constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | 
 #ifndef DK_COOP_U
 #define DK_COOP_U 6
 #endif
+#ifndef DK_HDR_TEMPORAL
+#define DK_HDR_TEMPORAL 0
+#endif
 #ifndef DK_NT_LOADS
 #define DK_NT_LOADS 1
 #endif
@@ -583,7 +586,10 @@ __device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r,
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
             const uint32_t b = b0 + 16 * u;
-            S.d[h][u] = B.template ld<DK_NT_LOADS != 0>(b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob);
+            // DK_HDR_TEMPORAL (tuning): the first 16 granules of each frame (its first 256 bytes, u = 0 of
+            // iteration 0) with the default policy, e.g. for the TX kernel's header-window rewrite to hit L2
+            const uint32_t a = b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob;
+            S.d[h][u] = (DK_HDR_TEMPORAL && u == 0) ? B.template ld<false>(a) : B.template ld<DK_NT_LOADS != 0>(a);
         }
 }
 
