@@ -42,6 +42,9 @@ constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | 
 #ifndef DK_COOP_U
 #define DK_COOP_U 6
 #endif
+#ifndef DK_TX_HDR_SPLIT
+#define DK_TX_HDR_SPLIT 0
+#endif
 #ifndef DK_HDR_TEMPORAL
 #define DK_HDR_TEMPORAL 0  // 1: the receive kernels too load each frame's first 256 bytes with the default policy
 #endif
@@ -590,6 +593,14 @@ __device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r,
             // policy instead of nontemporal, so the header-window rewrite finds its line in L2 (TX C2 -3 %; the
             // receive kernels measured +1.4 % with it)
             const uint32_t a = b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob;
+#if DK_TX_HDR_SPLIT
+            if (kHdrT && u == 0 && it == 0) {  // granules 0..3 (the header window) temporal, 4..15 nontemporal
+                const uint4 t = B.template ld<false>(l16 < 4 ? a : kOob);
+                const uint4 q = B.template ld<DK_NT_LOADS != 0>(l16 < 4 ? kOob : a);
+                S.d[h][u] = make_uint4(t.x | q.x, t.y | q.y, t.z | q.z, t.w | q.w);
+                continue;
+            }
+#endif
             S.d[h][u] = ((kHdrT || DK_HDR_TEMPORAL) && u == 0 && it == 0) ? B.template ld<false>(a)
                                                                             : B.template ld<DK_NT_LOADS != 0>(a);
         }
