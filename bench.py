@@ -105,7 +105,10 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
         for _ in range(5):
             c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             c0.record(sr.side)
-            eng.counts_allreduce(r, comm.handle, stream=sr.side)
+            if hasattr(comm, "handle"):
+                eng.counts_allreduce(r, comm.handle, stream=sr.side)
+            else:  # shard.TorchCountsAllreduce fallback
+                comm(r, sr.side)
             c1.record(sr.side)
             torch.cuda.synchronize()
             coll.append(c0.elapsed_time(c1) / 1e3)
@@ -416,8 +419,19 @@ def main():
     from demikernel_amd import Comm, Config, RxEngine, synth
     from demikernel_amd.shard import broadcast_comm_id
 
+    collective = "none"
     if world > 1:  # the receive path's own RCCL communicator (include/dk_comm.h), bootstrapped over the process group
-        comm = Comm.init_rank(world, broadcast_comm_id(dist, Comm.unique_id), rank, dev)
+        try:
+            comm = Comm.init_rank(world, broadcast_comm_id(dist, Comm.unique_id), rank, dev)
+            collective = ("dk_rx_flow_counts_allreduce (RCCL all-reduce of u64 flow + verdict counters) per step on a "
+                          "side stream, double-buffered (overlaps the next step's kernel)")
+        except Exception as e:  # noqa: BLE001 — keep the scaling run alive; the line says which collective ran
+            from demikernel_amd.shard import TorchCountsAllreduce
+
+            print(f"bench: dk_comm_init_rank failed ({e}); counters reduced through torch.distributed nccl",
+                  file=sys.stderr)
+            comm = TorchCountsAllreduce(dist.new_group(backend="nccl"))
+            collective = "torch.distributed nccl all_reduce of the counters (fallback: dk_comm init failed)"
 
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -461,9 +475,7 @@ def main():
         "data": "synthetic (seeded frames generated on device; 1% corrupted tail)",
         "config": {"workload": WORKLOADS[name][0], "name": name, "frames_per_gpu": batch.n,
                    "global_frames": total_frames, "parallelism": f"packet-shard x{world}",
-                   "collective": ("dk_rx_flow_counts_allreduce (RCCL all-reduce of u64 flow + verdict counters) per "
-                                  "step on a side stream, double-buffered (overlaps the next step's kernel)")
-                   if world > 1 else "none"},
+                   "collective": collective},
         "mpkt_s": round(total_frames * args.steps / wall / 1e6, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -536,7 +548,7 @@ def main():
         out["tcp_rx_64conns"] = tcp_rate(stream, 1 << 20, 64, cpu_seconds=1.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if comm is not None:
+    if comm is not None and hasattr(comm, "destroy"):
         comm.destroy()
     if dist is not None:
         dist.barrier()

@@ -52,6 +52,22 @@ def allreduce_counts(counts, group=None) -> None:
     dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
 
 
+class TorchCountsAllreduce:
+    """Fallback when the receive path's own RCCL communicator (dk_comm.h) cannot be created on a node: the same
+    all-reduce of the counter arrays through torch.distributed's RCCL (backend "nccl") process group."""
+
+    def __init__(self, group):
+        self.group = group
+
+    def __call__(self, results, stream) -> None:
+        import torch
+        import torch.distributed as dist
+
+        with torch.cuda.stream(stream):
+            dist.all_reduce(results.t["flow_counts"], op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(results.t["verdict_counts"], op=dist.ReduceOp.SUM, group=self.group)
+
+
 class ShardedReceiver:
     """One rank of a packet-sharded receive: its engine, its RCCL communicator, and double-buffered counters whose
     all-reduce runs on a side stream (the collective of batch k overlaps the kernel of batch k + 1)."""
@@ -88,7 +104,10 @@ class ShardedReceiver:
             ev = torch.cuda.Event()
             ev.record(self.stream)
             self.side.wait_event(ev)
-            self.eng.counts_allreduce(r, self.comm.handle, stream=self.side)
+            if isinstance(self.comm, TorchCountsAllreduce):
+                self.comm(r, self.side)
+            else:
+                self.eng.counts_allreduce(r, self.comm.handle, stream=self.side)
             done = torch.cuda.Event()
             done.record(self.side)
             self.done[slot] = done
