@@ -42,6 +42,9 @@ constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | 
 #ifndef DK_COOP_U
 #define DK_COOP_U 6
 #endif
+#ifndef DK_HDR_TEMPORAL_U
+#define DK_HDR_TEMPORAL_U 1  // loads u < this of a frame's first iteration take the default policy (kHdrT)
+#endif
 #ifndef DK_TX_HDR_SPLIT
 #define DK_TX_HDR_SPLIT 0
 #endif
@@ -601,8 +604,9 @@ __device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r,
                 continue;
             }
 #endif
-            S.d[h][u] = ((kHdrT || DK_HDR_TEMPORAL) && u == 0 && it == 0) ? B.template ld<false>(a)
-                                                                            : B.template ld<DK_NT_LOADS != 0>(a);
+            S.d[h][u] = ((kHdrT || DK_HDR_TEMPORAL) && u < DK_HDR_TEMPORAL_U && it == 0)
+                            ? B.template ld<false>(a)
+                            : B.template ld<DK_NT_LOADS != 0>(a);
         }
 }
 
