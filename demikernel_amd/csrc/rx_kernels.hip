@@ -752,14 +752,16 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WL& W, ui
 }
 
 #ifndef DK_RES_STORE
-#define DK_RES_STORE 0  // result stores: 0 plain, 1 nontemporal
+#define DK_RES_STORE 0  // result stores: 0 plain (nontemporal in the small-frame kernel), 1 nontemporal everywhere
 #endif
+// Result stores. The small-frame kernel stores nontemporal (C3 -3.7 %: its 20-24 B of results per 64-byte frame are
+// 28 % of its traffic); the other kernels measured ±0 either way (round 1) and keep plain stores.
+template <bool kNt = false>
 __device__ __forceinline__ void st_res(uint32_t* p, uint32_t v) {
-#if DK_RES_STORE == 1
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
+    if (kNt || DK_RES_STORE == 1)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
 }
 
 // One frame per lane, 64 frames per wave chunk. Returns the verdict and the flow id (DK_FLOW_NONE if none).
@@ -784,7 +786,7 @@ constexpr int kStageK = DK_STAGE_K;
 
 // Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
 // results (stored, or handed back in rec for staging).
-template <bool kShift, bool kStage, class WL, bool kOpt = true>
+template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false>
 __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
                                           uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
@@ -901,16 +903,16 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
         }
         rec = Rec{meta, src, dst, ports, pay, fid};
         if (!kStage) {
-        st_res(P.res.meta + i, meta);
+        st_res<kNtRes>(P.res.meta + i, meta);
 #ifdef DK_ABL_NOSTORE  // ablation (tuning only): one result array
         if (ports == 0x12345678u)
 #endif
         {
-        st_res(P.res.src_ip + i, src);
-        if (P.res.dst_ip) st_res(P.res.dst_ip + i, dst);
-        st_res(P.res.ports + i, ports);
-        st_res(P.res.payload + i, pay);
-        st_res(P.res.flow_id + i, fid);
+        st_res<kNtRes>(P.res.src_ip + i, src);
+        if (P.res.dst_ip) st_res<kNtRes>(P.res.dst_ip + i, dst);
+        st_res<kNtRes>(P.res.ports + i, ports);
+        st_res<kNtRes>(P.res.payload + i, pay);
+        st_res<kNtRes>(P.res.flow_id + i, fid);
         }
         }
         if (kOpt) {  // optional outputs (kOpt = false: the caller asked for none; fewer live SGPRs)
@@ -1407,8 +1409,8 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 #endif
         DK_STAMP(2 + 3 * k);
         small_big_frames(F, lane, off, B, W, C);
-        rx_finish<kShift, (DK_SMALL_PIPE >= 2), SmallLds, kOpt>(P, i, live, lane, W, off, len, C, v, fid, rec,
-                                                                 k < 3 ? 16 + 5 * k : ~0u);
+        rx_finish<kShift, (DK_SMALL_PIPE >= 2), SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid,
+                                                                       rec, k < 3 ? 16 + 5 * k : ~0u);
         DK_STAMP(3 + 3 * k);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
 #if DK_SMALL_PIPE
@@ -1576,7 +1578,7 @@ __global__ __launch_bounds__(kSsBlock, 2) void dk_rx_small_split_kernel(RxParams
             uint32_t v, fid;
             Rec rec;
             rec.meta = kNoRec;
-            rx_finish<kShift, false, SsView, kOpt>(P, i, live, lane, V, off, len, C, v, fid, rec);
+            rx_finish<kShift, false, SsView, kOpt, true>(P, i, live, lane, V, off, len, C, v, fid, rec);
             count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         }
     }
