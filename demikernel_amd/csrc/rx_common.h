@@ -92,7 +92,8 @@ struct RxParams {
     uint32_t stage;          // launch the instantiation that stages result stores in registers (large frames)
     uint32_t split;          // launch the split (stream waves / finish waves) kernel: 0 no, else finishers per stream
                              // wave (1: large frames, 2: mixed sizes)
-    uint32_t small;          // launch the small-frame kernel (minimum-size frames): 1, or 2 = its stream/finish form
+    uint32_t small;          // launch the small-frame kernel (minimum-size frames): 1, 2 = its stream/finish form,
+                             // 3 = its two-chunk form
     dk_rx_results res;
 };
 
@@ -113,7 +114,7 @@ struct TxParams {
 // Receive kernel families (launch_batch picks one per launch).
 namespace dk {
 constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFamilySmall = 3, kFamilySplit2 = 4,
-                   kFamilySmallSplit = 5;
+                   kFamilySmallSplit = 5, kFamilySmallPair = 6;
 }
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);

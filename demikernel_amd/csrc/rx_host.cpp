@@ -231,10 +231,11 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.small = bytes_per_frame <= 96 ? 1u : 0u;
     if (T.stage >= 0) p.stage = T.stage ? 1u : 0u;
     if (T.split >= 0) p.split = T.split == 2 ? 2u : T.split ? 1u : 0u;
-    if (T.small >= 0) p.small = T.small == 2 ? 2u : T.small ? 1u : 0u;
+    if (T.small >= 0) p.small = T.small == 2 || T.small == 3 ? (uint32_t)T.small : T.small ? 1u : 0u;
     if (p.small) p.split = p.stage = 0;
     p.sched = T.sched >= 0 ? (uint32_t)std::min(T.sched, 3) : 0u;
-    const uint32_t family = p.small == 2 ? dk::kFamilySmallSplit
+    const uint32_t family = p.small == 3 ? dk::kFamilySmallPair
+                            : p.small == 2 ? dk::kFamilySmallSplit
                             : p.small ? dk::kFamilySmall
                             : p.split == 2 ? dk::kFamilySplit2
                             : p.split ? dk::kFamilySplit

@@ -530,7 +530,7 @@ struct CoopPlan {  // wave-uniform
 #define DK_COOP_MED_U 0  // 3: medium frames take the half-span shape (measured IMIX +0.7 %, C2 ±0: off)
 #endif
 constexpr uint32_t kMedU = DK_COOP_MED_U > 0 ? DK_COOP_MED_U : 1;
-constexpr uint32_t kMedR = (kRoundsPerStep * kCoopU) / kMedU;
+[[maybe_unused]] constexpr uint32_t kMedR = (kRoundsPerStep * kCoopU) / kMedU;
 constexpr uint32_t kMedGran = DK_COOP_MED_U > 0 ? 16 * kMedU : 0;
 template <uint32_t U, uint32_t R>
 struct CoopStep {
@@ -785,11 +785,8 @@ struct Rec {
 constexpr int kStageK = DK_STAGE_K;
 
 // Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
-// results (stored, or handed back in rec for staging).
-template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false>
-__device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
-                                          uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
-                                          uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
+// results (stored, or handed back in rec for staging). Two halves so a kernel can interleave two chunks: rx_front
+// (parse, the first table probe issued, the L4 sum) and rx_back (verdicts, demux, results); rx_finish runs both.
 #ifdef DK_DIAG_STAMPS  // diagnostic build: sub-phase stamps of the small-frame kernel (tools/stamps.py)
 #define DK_SUB_STAMP(j)                                                                                             \
     do {                                                                                                            \
@@ -800,17 +797,18 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
 #else
 #define DK_SUB_STAMP(j) do {} while (0)
 #endif
-#ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
-#ifdef DK_DIAG_NO_STORE
-    if (live && (C.fsum ^ C.R.w[3] ^ C.R.w[9]) == 0x9E3779B1u)
-#else
-    if (live)
-#endif
-        P.res.meta[i] = C.fsum ^ C.R.w[3] ^ C.R.w[9];
-    v_out = kNone;
-    fid_out = DK_FLOW_NONE;
-    return;
-#endif
+struct FinState {
+    Lane L;
+    ProbeKey k1;
+    uint32_t h1;
+    uint4 s1;
+    bool fast, resum, big, inb;
+};
+template <bool kShift, class WL>
+__device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t lane, WL& W, uint32_t off,
+                                         uint32_t len, const Chunk& C, FinState& St, uint32_t stamp_base = ~0u) {
+    Lane& L = St.L;
+    bool& resum = St.resum;
     const RegAcc& R = C.R;
     const bool inb = C.inb, vec = C.vec, big = C.big;
     const uint8_t* f = P.frames + off;
@@ -818,9 +816,10 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
     // ---------------- Phase C: parse, checksum, options, demux, results ----------------
     // Fast parse: 16-byte aligned, whole Ethernet + IPv4 fixed header present, IHL == 5 (S == 34).
     // ARP (ethertype bytes 08 06) is parsed by the byte path (low volume).
+    St.big = big;
+    St.inb = inb;
     const bool fast = vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u && (R.w[3] & 0xFFFFu) != 0x0608u;
-    bool resum = false;  // path-stats: streamed frame whose segment is re-summed in-lane
-    Lane L;
+    resum = false;  // path-stats: streamed frame whose segment is re-summed in-lane
     L.v = kNone; L.src = L.dst = L.ports = L.mhi = L.seq = L.ack = L.winurg = 0;
     L.S = L.E = L.hlen = L.stored = L.need = L.lsum = 0;
     if (!live) {
@@ -835,14 +834,29 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
     DK_SUB_STAMP(0);
     // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
     const bool pend4 = L.v == kPendTcp || L.v == kPendUdp;
+    St.fast = fast;
     const ProbeKey k1 = L.v == kPendTcp
                             ? ProbeKey{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)}
                             : ProbeKey{DK_FLOW_UDP, P.local_ip, 0u, L.ports >> 16};
+    St.k1 = k1;
     const uint32_t h1 = probe_slot(P, k1);
-    uint4 s1 = make_uint4(0, 0, 0, 0);
-    if (pend4) s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+    St.h1 = h1;
+    St.s1 = make_uint4(0, 0, 0, 0);
+    if (pend4) St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
     DK_SUB_STAMP(1);
+}
+
+template <bool kStage, bool kOpt = true, bool kNtRes = false>
+__device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live, uint32_t lane, uint32_t off,
+                                        FinState& St, uint32_t& v_out, uint32_t& fid_out, Rec& rec,
+                                        uint32_t stamp_base = ~0u) {
+    Lane& L = St.L;
+    const ProbeKey& k1 = St.k1;
+    const uint32_t h1 = St.h1;
+    const uint4 s1 = St.s1;
+    const bool fast = St.fast, resum = St.resum, big = St.big, inb = St.inb;
+    const uint8_t* f = P.frames + off;
 
     uint32_t fid = DK_FLOW_NONE;
     if (L.v == kPendIcmp) {
@@ -934,6 +948,26 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
 #endif
     v_out = v;
     fid_out = fid;
+}
+
+template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false>
+__device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
+                                          uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
+                                          uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
+#ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
+#ifdef DK_DIAG_NO_STORE
+    if (live && (C.fsum ^ C.R.w[3] ^ C.R.w[9]) == 0x9E3779B1u)
+#else
+    if (live)
+#endif
+        P.res.meta[i] = C.fsum ^ C.R.w[3] ^ C.R.w[9];
+    v_out = kNone;
+    fid_out = DK_FLOW_NONE;
+    return;
+#endif
+    FinState St;
+    rx_front<kShift>(P, live, lane, W, off, len, C, St, stamp_base);
+    rx_back<kStage, kOpt, kNtRes>(P, i, live, lane, off, St, v_out, fid_out, rec, stamp_base);
 }
 
 // Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). Chunk k of a wave holds the
@@ -1463,6 +1497,92 @@ __device__ __forceinline__ void lds_wait_eq(uint32_t* w, uint32_t want) {
 }
 __device__ __forceinline__ void lds_publish(uint32_t* w, uint32_t v) {
     __hip_atomic_store((lu32*)w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Small-frame pair kernel (DK_RX_SMALL=3): each wave walks two chunks at once — chunk A's window by LDS-DMA, chunk
+// B's frames by per-lane loads, both in flight together; then parse A and B (both table probes in flight), then
+// verdicts, demux and results of A and of B. A wave's dependent chain (window -> parse -> probe -> results) is paid
+// once per two chunks, at 4 waves/SIMD (128 VGPRs) instead of 5.
+#ifndef DK_MIN_WAVES_PAIR
+#define DK_MIN_WAVES_PAIR 4
+#endif
+template <bool kShift, bool kOpt>
+__global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_PAIR) void dk_rx_small_pair_kernel(RxParams P) {
+    __shared__ SmallLds s_wave[kSmallWaves];
+    __shared__ uint32_t s_vh[DK_V_COUNT];
+    __shared__ uint32_t s_last;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = tid >> 6;
+    const bool lds_flows = P.flow_mode == kFlowLds;
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
+    __syncthreads();
+
+    const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
+    const Blob B(P.frames, P.frames_bytes);
+    SmallLds& W = s_wave[wv];
+    uint32_t cA, limA, cB = 0, limB = 0;
+    bool hasA = r.chunk(0, cA, limA);
+    bool hasB = hasA && r.chunk(1, cB, limB);
+    uint32_t offA = 0, lenA = 0, offB = 0, lenB = 0;
+    if (hasA && cA + r.lane_off < limA) {
+        offA = P.off[cA + r.lane_off];
+        lenA = P.len[cA + r.lane_off];
+    }
+    if (hasB && cB + r.lane_off < limB) {
+        offB = P.off[cB + r.lane_off];
+        lenB = P.len[cB + r.lane_off];
+    }
+    for (uint32_t k = 0; hasA; k += 2) {
+        const uint32_t iA = cA + r.lane_off, iB = cB + r.lane_off;
+        const bool liveA = iA < limA, liveB = hasB && iB < limB;
+        // next pair's descriptors, in flight with this pair's frames
+        uint32_t cA2 = 0, limA2 = 0, cB2 = 0, limB2 = 0, offA2 = 0, lenA2 = 0, offB2 = 0, lenB2 = 0;
+        const bool hasA2 = hasB && r.chunk(k + 2, cA2, limA2);
+        const bool hasB2 = hasA2 && r.chunk(k + 3, cB2, limB2);
+        if (hasA2 && cA2 + r.lane_off < limA2) {
+            offA2 = P.off[cA2 + r.lane_off];
+            lenA2 = P.len[cA2 + r.lane_off];
+        }
+        if (hasB2 && cB2 + r.lane_off < limB2) {
+            offB2 = P.off[cB2 + r.lane_off];
+            lenB2 = P.len[cB2 + r.lane_off];
+        }
+        const FrameDesc<kShift> FA(P.frames, P.frames_bytes, liveA, offA, lenA);
+        const FrameDesc<kShift> FB(P.frames, P.frames_bytes, liveB, offB, lenB);
+        Chunk CA, CB;
+        const WinPlan plA = small_window_issue(FA, B, offA, lenA, liveA, lane, W);
+        small_load(FB, B, offB, CB.R);
+        small_window_read(plA, FA, B, offA, W, CA.R);
+        FinState SA, SB;
+        small_big_frames(FA, lane, offA, B, W, CA);  // W.tail: chunk A's, read by rx_front(A) before B's replace it
+        rx_front<kShift>(P, liveA, lane, W, offA, lenA, CA, SA);
+        small_big_frames(FB, lane, offB, B, W, CB);
+        rx_front<kShift>(P, liveB, lane, W, offB, lenB, CB, SB);
+        uint32_t v, fid;
+        Rec rec;
+        rec.meta = kNoRec;
+        rx_back<false, kOpt, true>(P, iA, liveA, lane, offA, SA, v, fid, rec);
+        count_chunk(P, liveA, lane, v, fid, lds_flows, s_flow, s_vh);
+        rx_back<false, kOpt, true>(P, iB, liveB, lane, offB, SB, v, fid, rec);
+        count_chunk(P, liveB, lane, v, fid, lds_flows, s_flow, s_vh);
+        hasA = hasA2;
+        hasB = hasB2;
+        cA = cA2;
+        limA = limA2;
+        cB = cB2;
+        limB = limB2;
+        offA = offA2;
+        lenA = lenA2;
+        offB = offB2;
+        lenB = lenB2;
+    }
+    __syncthreads();
+    flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh, &s_last);
 }
 
 // Small-frame split kernel (DK_RX_SMALL=2): the small-frame kernel's chunk chain without the frame read on it.
@@ -2041,6 +2161,9 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     else if (family == dk::kFamilySplit)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 1>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
+    else if (family == dk::kFamilySmallPair)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_pair_kernel<true, true>,
+                                                          dk::kSmallBlock, dyn_lds_bytes);
     else if (family == dk::kFamilySmallSplit)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_split_kernel<true, true>,
                                                           dk::kSsBlock, dyn_lds_bytes);
@@ -2061,7 +2184,13 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
-    if (p.small == 2 && p.aligned16)
+    if (p.small == 3 && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_small_pair_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small == 3 && opt)
+        hipLaunchKernelGGL((dk::dk_rx_small_pair_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small == 3)
+        hipLaunchKernelGGL((dk::dk_rx_small_pair_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small == 2 && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<false, true>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
     else if (p.small == 2 && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<true, true>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);

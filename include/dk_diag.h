@@ -31,8 +31,9 @@ int dk_diag_path_stats_read(struct dk_rx_ctx* ctx, uint64_t out[4]); /* synchron
  * the environment when it is created (DK_RX_STAGE, DK_RX_SPLIT, DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID,
  * DK_RX_GRID_PER_CU, DK_RX_DEBUG), never on the launch path; this call replaces them. knobs[] = {stage, split, small,
  * sched, grid, grid_per_cu, debug}: stage/split/small force a kernel family on (1) or off (0) — split 2 is the split
- * kernel with two finish waves per stream wave, small 2 the small-frame kernel's stream/finish form — sched picks the
- * wave schedule (0..3), grid / grid_per_cu fix the persistent grid, debug > 0 prints each launch's choice to stderr. */
+ * kernel with two finish waves per stream wave, small 2 and 3 the small-frame kernel's stream/finish and two-chunk
+ * forms — sched picks the wave schedule (0..3), grid / grid_per_cu fix the persistent grid, debug > 0 prints each
+ * launch's choice to stderr. */
 #define DK_DIAG_RX_KNOBS 7
 int dk_diag_rx_set_tuning(struct dk_rx_ctx* ctx, const int32_t knobs[DK_DIAG_RX_KNOBS]); /* 0 or EINVAL */
 /* The same for dk_tx_checksum (process-wide; first read from DK_TX_SPLIT, DK_RX_SCHED, DK_RX_GRID_PER_CU). */
