@@ -45,9 +45,6 @@ constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | 
 #ifndef DK_HDR_TEMPORAL_U
 #define DK_HDR_TEMPORAL_U 1  // loads u < this of a frame's first iteration take the default policy (kHdrT)
 #endif
-#ifndef DK_TX_HDR_SPLIT
-#define DK_TX_HDR_SPLIT 0
-#endif
 #ifndef DK_HDR_TEMPORAL
 #define DK_HDR_TEMPORAL 0  // 1: the receive kernels too load each frame's first 256 bytes with the default policy
 #endif
@@ -61,9 +58,6 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kCoopU = DK_COOP_U; // dwordx4 loads per lane per phase-B round
 constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave covers per round
-#ifndef DK_COOP_SKIP
-#define DK_COOP_SKIP 0  // measured slower (IMIX +7 %)
-#endif
 #ifndef DK_ROUNDS_PER_STEP
 #define DK_ROUNDS_PER_STEP 2
 #endif
@@ -596,14 +590,6 @@ __device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r,
             // policy instead of nontemporal, so the header-window rewrite finds its line in L2 (TX C2 -3 %; the
             // receive kernels measured +1.4 % with it)
             const uint32_t a = b < S.sl[h].nb ? S.sl[h].boff + 16 * b : kOob;
-#if DK_TX_HDR_SPLIT
-            if (kHdrT && u == 0 && it == 0) {  // granules 0..3 (the header window) temporal, 4..15 nontemporal
-                const uint4 t = B.template ld<false>(l16 < 4 ? a : kOob);
-                const uint4 q = B.template ld<DK_NT_LOADS != 0>(l16 < 4 ? kOob : a);
-                S.d[h][u] = make_uint4(t.x | q.x, t.y | q.y, t.z | q.z, t.w | q.w);
-                continue;
-            }
-#endif
             S.d[h][u] = ((kHdrT || DK_HDR_TEMPORAL) && u < DK_HDR_TEMPORAL_U && it == 0)
                             ? B.template ld<false>(a)
                             : B.template ld<DK_NT_LOADS != 0>(a);
@@ -1251,9 +1237,6 @@ struct SmallLds {
 #ifndef DK_MIN_WAVES_SMALL
 #define DK_MIN_WAVES_SMALL 5  // 96 VGPRs: no spills (6 waves spilled 16-22 VGPRs to scratch: C3 +11 %)
 #endif
-#ifndef DK_SMALL_PIPE
-#define DK_SMALL_PIPE 0
-#endif
 #ifndef DK_SMALL_WAVES
 #define DK_SMALL_WAVES 4  // waves per workgroup of the small-frame kernel
 #endif
@@ -1418,10 +1401,6 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     }
     Chunk C;
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
-#if DK_SMALL_PIPE
-    // Window k + 1 is DMA'd while chunk k is parsed (the slot is free once chunk k's window is in registers).
-    if (have) small_window_read(small_window_issue(F, B, off, len, c + r.lane_off < lim, lane, W), F, B, off, W, C.R);
-#endif
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1436,34 +1415,13 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         Rec rec;
         rec.meta = kNoRec;
         if (k == 0) DK_STAMP(1);
-#if DK_SMALL_PIPE
-        const WinPlan pl1 = have1 ? small_window_issue(F1, B, off1, len1, c1 + r.lane_off < lim1, lane, W) : WinPlan{false, 0};
-#else
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
-#endif
         DK_STAMP(2 + 3 * k);
         small_big_frames(F, lane, off, B, W, C);
-        rx_finish<kShift, (DK_SMALL_PIPE >= 2), SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid,
-                                                                       rec, k < 3 ? 16 + 5 * k : ~0u);
+        rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,
+                                                       k < 3 ? 16 + 5 * k : ~0u);
         DK_STAMP(3 + 3 * k);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
-#if DK_SMALL_PIPE
-        asm volatile("" ::: "memory");  // keep chunk k + 1's window reads after chunk k's stores (register pressure)
-        if (have1) small_window_read(pl1, F1, B, off1, W, C.R);
-#if DK_SMALL_PIPE >= 2
-        // Chunk k's results leave after chunk k + 1's window is in: the window wait (vmcnt, in order) then never
-        // waits for these stores, only for the DMA issued before chunk k's parse.
-        asm volatile("" ::: "memory");
-        if (rec.meta != kNoRec) {
-            st_res(P.res.meta + i, rec.meta);
-            st_res(P.res.src_ip + i, rec.src);
-            if (P.res.dst_ip) st_res(P.res.dst_ip + i, rec.dst);
-            st_res(P.res.ports + i, rec.ports);
-            st_res(P.res.payload + i, rec.pay);
-            st_res(P.res.flow_id + i, rec.fid);
-        }
-#endif
-#endif
         DK_STAMP(4 + 3 * k);
         // rotate the pipeline
         have = have1;
