@@ -83,6 +83,8 @@ FUNCTIONS = [
     ("dk_rx_process", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_void_p]),
     ("dk_rx_process_host", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_uint32]),
     ("dk_rx_flow_counts_allreduce", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p]),
+    ("dk_rx_flow_counts_allreduce_to", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p, c_void_p,
+                                               c_void_p]),
     ("dk_tx_checksum", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
     ("dk_rx_verdict_name", c_char_p, [c_int]),
     ("dk_rx_verdict_errno", c_int, [c_int]),

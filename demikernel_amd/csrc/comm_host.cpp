@@ -59,20 +59,33 @@ int dk_comm_destroy(void* comm) {
     return rc_of(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
 }
 
-int dk_rx_flow_counts_allreduce(dk_rx_ctx* ctx, const dk_rx_results* res, void* nccl_comm, void* stream) {
+namespace {
+int counts_allreduce(dk_rx_ctx* ctx, const dk_rx_results* res, uint64_t* flow_out, uint64_t* verdict_out,
+                     void* nccl_comm, void* stream) {
     if (!ctx || !res || !nccl_comm) return EINVAL;
     const uint32_t nflows = dk_rx_flow_table_size(ctx);
     const ncclComm_t comm = static_cast<ncclComm_t>(nccl_comm);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const bool flows = res->flow_counts && nflows, verdicts = res->verdict_counts != nullptr;
+    if ((flows && !flow_out) || (verdicts && !verdict_out)) return EINVAL;
     if (!flows && !verdicts) return 0;
     int rc = rc_of(ncclGroupStart());
     if (rc) return rc;
-    if (flows) rc = rc_of(ncclAllReduce(res->flow_counts, res->flow_counts, nflows, ncclUint64, ncclSum, comm, s));
+    if (flows) rc = rc_of(ncclAllReduce(res->flow_counts, flow_out, nflows, ncclUint64, ncclSum, comm, s));
     if (rc == 0 && verdicts)
-        rc = rc_of(ncclAllReduce(res->verdict_counts, res->verdict_counts, DK_V_COUNT, ncclUint64, ncclSum, comm, s));
+        rc = rc_of(ncclAllReduce(res->verdict_counts, verdict_out, DK_V_COUNT, ncclUint64, ncclSum, comm, s));
     const int rc2 = rc_of(ncclGroupEnd());
     return rc ? rc : rc2;
+}
+}  // namespace
+
+int dk_rx_flow_counts_allreduce(dk_rx_ctx* ctx, const dk_rx_results* res, void* nccl_comm, void* stream) {
+    return res ? counts_allreduce(ctx, res, res->flow_counts, res->verdict_counts, nccl_comm, stream) : EINVAL;
+}
+
+int dk_rx_flow_counts_allreduce_to(dk_rx_ctx* ctx, const dk_rx_results* res, uint64_t* flow_out,
+                                   uint64_t* verdict_out, void* nccl_comm, void* stream) {
+    return counts_allreduce(ctx, res, flow_out, verdict_out, nccl_comm, stream);
 }
 
 }  // extern "C"

@@ -246,6 +246,18 @@ class RxEngine:
         _check(self.lib.dk_rx_flow_counts_allreduce(self._ctx, ctypes.byref(r), ctypes.c_void_p(comm),
                                                     ctypes.c_void_p(s.cuda_stream)), "dk_rx_flow_counts_allreduce")
 
+    def counts_allreduce_to(self, results: RxResults, flow_out, verdict_out, comm: int, stream=None) -> None:
+        """dk_rx_flow_counts_allreduce_to: the node-wide sums of this rank's (accumulating) counters into separate
+        device tensors (u64[flow table size], u64[DK_V_COUNT]), on `stream`."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        r = results.c_struct()
+        _check(self.lib.dk_rx_flow_counts_allreduce_to(
+            self._ctx, ctypes.byref(r), ctypes.c_void_p(flow_out.data_ptr() if flow_out is not None else 0),
+            ctypes.c_void_p(verdict_out.data_ptr() if verdict_out is not None else 0), ctypes.c_void_p(comm),
+            ctypes.c_void_p(s.cuda_stream)), "dk_rx_flow_counts_allreduce_to")
+
     def tx_checksum(self, batch: FrameBatch, stream=None) -> None:
         """Fill IPv4/TCP/UDP checksums in place (serialize_and_attach with tx offload off)."""
         import torch

@@ -237,6 +237,11 @@ int dk_rx_process_host(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_res
  * collective of the receive path (RCCL over xGMI; per-frame results stay on their GPU). Every rank must call it with
  * the same flow table size. Asynchronous. Returns 0, EINVAL or EIO. */
 int dk_rx_flow_counts_allreduce(dk_rx_ctx* ctx, const dk_rx_results* res, void* nccl_comm, void* stream);
+/* The same into separate device arrays (flow_out[flow table size], verdict_out[DK_V_COUNT]; required where the
+ * corresponding res array is set): each rank keeps accumulating its own counters across batches and reads the
+ * node-wide totals from the outputs, with no per-batch reset of its counters. */
+int dk_rx_flow_counts_allreduce_to(dk_rx_ctx* ctx, const dk_rx_results* res, uint64_t* flow_out,
+                                   uint64_t* verdict_out, void* nccl_comm, void* stream);
 
 /* TX side: compute and store the IPv4 header checksum and the TCP/UDP checksum of every
  * frame in place, as Ipv4Header/TcpHeader/UdpHeader::serialize_and_attach do (ipv4/header.rs:229-266,

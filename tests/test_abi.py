@@ -32,6 +32,7 @@ def test_every_declared_function_is_exported():
         names |= set(declared_functions(h))
     assert {"dk_rx_process", "dk_rx_ctx_create", "dk_tx_checksum", "dk_diag_read_probe", "dk_rx_process_tpacket3",
             "dk_tcp_rx_process", "dk_rx_into_sgarrays", "dk_tcp_into_sgarrays", "dk_rx_flow_counts_allreduce",
+            "dk_rx_flow_counts_allreduce_to",
             "dk_comm_init_rank"} <= names
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T " in l}

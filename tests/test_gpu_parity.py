@@ -524,8 +524,8 @@ def test_two_streams_one_context(torch_cuda):
 
 
 def test_counts_allreduce_one_rank(torch_cuda):
-    """dk_rx_flow_counts_allreduce through a 1-rank RCCL communicator (ncclCommInitAll over device 0): the counters
-    come back unchanged (the sum over one rank), per-frame results untouched."""
+    """dk_rx_flow_counts_allreduce (and its out-of-place form) through a 1-rank RCCL communicator (ncclCommInitAll over
+    device 0): the counters come back unchanged (the sum over one rank), per-frame results untouched."""
     import torch
 
     from demikernel_amd import Comm
@@ -546,11 +546,16 @@ def test_counts_allreduce_one_rank(torch_cuda):
         eng.receive_batch(FrameBatch.from_numpy(blob, off, lens), r)
         torch.cuda.synchronize()
         before = r.to_numpy()
+        fo = torch.full_like(r.t["flow_counts"], 7)
+        vo = torch.full_like(r.t["verdict_counts"], 7)
+        eng.counts_allreduce_to(r, fo, vo, comm.handle)  # out of place: the totals land in fo / vo
         eng.counts_allreduce(r, comm.handle)
         torch.cuda.synchronize()
         after = r.to_numpy()
         for k in before:
             assert np.array_equal(before[k], after[k]), k
+        assert np.array_equal(fo.cpu().numpy()[: len(flows)], before["flow_counts"])
+        assert np.array_equal(vo.cpu().numpy(), before["verdict_counts"])
         exp = run_oracle(blob, off, lens, flows)
         assert np.array_equal(after["flow_counts"], exp["flow_counts"][: len(flows)])
     finally:
