@@ -2004,82 +2004,50 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
     tx_finish<false>(P, lane, W, off, len, C, win);
 }
 
-#ifndef DK_TX_STAGE_K
-#define DK_TX_STAGE_K 0  // measured: no gain at 4, 6 or 8; kept as a tuning option
-#endif
-#if DK_TX_STAGE_K > 0
-constexpr int kTxStageK = DK_TX_STAGE_K;  // chunks of header windows a finish wave holds before one burst of stores
-__device__ __forceinline__ void flush_tx(const TxParams& P, const TxWin (&stg)[kTxStageK], uint32_t nst) {
-#pragma unroll
-    for (int q = kTxStageK - 1; q >= 0; q--) {
-        if ((uint32_t)q >= nst || stg[q].off == kNoWin) continue;
-        uint4* p = reinterpret_cast<uint4*>(P.frames + stg[q].off);
-#pragma unroll
-        for (int k = 0; k < 4; k++) p[k] = make_uint4(stg[q].d[4 * k], stg[q].d[4 * k + 1], stg[q].d[4 * k + 2], stg[q].d[4 * k + 3]);
-    }
-}
-#endif
 
-// Split TX kernel (large frames), the receive split kernel's structure: stream waves 0..3 run phases A+B of chunk p
-// into LDS buffer p % 2, finish waves 4..7 compute chunk p - 1's checksums and rewrite its header windows; the
-// streaming waves never wait on the checksum arithmetic or the writes.
+// Split TX kernel (large frames), the receive split kernel's structure and hand-off: stream waves 0..3 run phases A+B
+// of their chunks into 3 LDS buffers each, finish waves 4..7 compute the checksums and rewrite the header windows, with
+// ready / free words instead of a per-period workgroup barrier; the streaming waves never wait on the checksum
+// arithmetic or the writes.
 __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P) {
-    __shared__ WaveLds s_buf[2][kWaves];  // [period parity][stream wave]
+    constexpr int kBufs = SplitShape<1>::kBufs;
+    __shared__ WaveLds s_buf[kBufs][kWaves];  // [chunk % kBufs][stream wave]
+    __shared__ uint32_t s_ready[kWaves][kBufs], s_free[kWaves][kBufs];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6, sw = wv & (kWaves - 1);
     const bool finisher = wv >= (uint32_t)kWaves;
+    if (tid < kWaves * kBufs) {
+        (&s_ready[0][0])[tid] = 0;
+        (&s_free[0][0])[tid] = 0;
+    }
+    __syncthreads();
     const WaveRange r = wave_range(0, P.n, sw, lane);
-    const WaveRange r0 = wave_range(0, P.n, 0, lane);
-    uint32_t nper = 0, c0, l0;
-    while (r0.chunk(nper, c0, l0)) nper++;
     const Blob B(P.frames, P.frames_bytes);
-#if DK_TX_STAGE_K > 0
-    TxWin stg[kTxStageK];
-    uint32_t nstg = 0;  // wave-uniform
-#endif
-    for (uint32_t p = 0; p <= nper; p++) {
-        uint32_t c, lim;
+    uint32_t c, lim;
+    for (uint32_t p = 0; r.chunk(p, c, lim); p++) {
+        const uint32_t b = p % kBufs;
+        WaveLds& W = s_buf[b][sw];
+        const uint32_t i = c + r.lane_off;
+        const bool live = i < lim;
+        const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+        const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
         if (!finisher) {
-            if (r.chunk(p, c, lim)) {
-                WaveLds& W = s_buf[p & 1][sw];
-                const uint32_t i = c + r.lane_off;
-                const bool live = i < lim;
-                const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
-                const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
-                const CoopPlan pl = coop_plan(F, lane, off, W);
-                coop_stream<true, true>(pl, lane, W, B);
-            }
-        } else if (p > 0 && r.chunk(p - 1, c, lim)) {
-            WaveLds& W = s_buf[(p - 1) & 1][sw];
-            const uint32_t i = c + r.lane_off;
-            const bool live = i < lim;
-            const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
-            const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
+            if (p >= (uint32_t)kBufs) lds_wait_eq(&s_free[sw][b], p - kBufs + 1);  // buffer read out
+            const CoopPlan pl = coop_plan(F, lane, off, W);
+            coop_stream<true, true>(pl, lane, W, B);
+            if (lane == 0) lds_publish(&s_ready[sw][b], p + 1);
+        } else {
             Chunk C;
             small_load(F, B, off, C.R);
+            lds_wait_eq(&s_ready[sw][b], p + 1);
             const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 0, 1};
             coop_gather(F, pl, lane, W, C);
-#if DK_TX_STAGE_K > 0
-            TxWin win;
-            tx_finish<true>(P, lane, W, off, len, C, win);
-#pragma unroll
-            for (int q = kTxStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
-            stg[0] = win;
-            if (++nstg == (uint32_t)kTxStageK) {
-                flush_tx(P, stg, nstg);
-                nstg = 0;
-            }
-#else
             TxWin win;
             tx_finish<false>(P, lane, W, off, len, C, win);
-#endif
+            if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
         }
-        __syncthreads();
     }
-#if DK_TX_STAGE_K > 0
-    if (finisher && nstg) flush_tx(P, stg, nstg);
-#endif
 }
 
 // Persistent, same schedule as dk_rx_kernel.
