@@ -94,7 +94,7 @@ class FrameBatch:
         costs speed, never correctness."""
         import torch
 
-        assert blob.dtype == torch.uint8 and blob.is_cuda
+        assert blob.dtype == torch.uint8 and (blob.is_cuda or blob.is_pinned()), "blob: HBM or pinned host memory"
         assert off.dtype == torch.int32 and lens.dtype == torch.int16 and off.numel() == lens.numel()
         self.blob, self.off, self.len = blob, off, lens
         self.n = off.numel()
@@ -111,6 +111,19 @@ class FrameBatch:
         ln = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint16).view(np.int16)).to(dev)
         aligned = b.data_ptr() % 16 == 0 and bool(np.all(np.asarray(off, dtype=np.uint64) % 16 == 0))
         return cls(b, o, ln, aligned16=aligned)
+
+    @classmethod
+    def host_mapped(cls, blob_pinned, off: np.ndarray, lens: np.ndarray, device: int = 0) -> "FrameBatch":
+        """Zero-copy: frames stay in page-locked host memory (a DPDK mempool registered with hipHostRegister, a
+        hipHostMalloc'd NIC buffer) and the kernel reads them over PCIe through the mapped address; the descriptors
+        go to HBM. `blob_pinned` is a pinned uint8 CPU tensor."""
+        import torch
+
+        dev = torch.device("cuda", device)
+        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint32).view(np.int32)).to(dev)
+        ln = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint16).view(np.int16)).to(dev)
+        aligned = blob_pinned.data_ptr() % 16 == 0 and bool(np.all(np.asarray(off, dtype=np.uint64) % 16 == 0))
+        return cls(blob_pinned, o, ln, aligned16=aligned)
 
     def c_struct(self) -> N.DkRxBatch:
         return N.DkRxBatch(_ptr(self.blob), self.frames_bytes, _ptr(self.off), _ptr(self.len), self.n,

@@ -523,6 +523,36 @@ def test_two_streams_one_context(torch_cuda):
     assert np.array_equal(got["flow_counts"], total * sum(e["flow_counts"][: len(flows)] for e in exps))
 
 
+@pytest.mark.parametrize("data_off", [128, 130])
+def test_mbuf_zero_copy(torch_cuda, data_off):
+    """DPDK-style ingest without a staging copy (catnip/runtime/mod.rs:348-365): frames in
+    2 KiB mbuf slots at data_off (RTE_PKTMBUF_HEADROOM 128, and 130 for an IP-aligned layout) inside page-locked host
+    memory, read by the kernel over PCIe through the mapped address (FrameBatch.host_mapped). Bit-exact vs the
+    oracle, IMIX sizes with 2 % corruption."""
+    import torch
+
+    n = 6000
+    flows = np.concatenate([synth.make_flows(400), synth.make_flows(16, kind="udp")])
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=21), flows, seed=22)
+    packed, poff, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(packed, poff, synth.corruption_plan(n, 0.02, tr))
+    slot = 2048
+    mb = np.zeros(n * slot, np.uint8)
+    off = (np.arange(n, dtype=np.uint64) * slot + data_off).astype(np.uint32)
+    for k in range(n):
+        mb[off[k]: off[k] + lens[k]] = packed[poff[k]: poff[k] + lens[k]]
+    pinned = torch.from_numpy(mb).pin_memory()
+    eng = RxEngine(Config(LOCAL), device=0)
+    eng.set_sockets(flows)
+    b = FrameBatch.host_mapped(pinned, off, lens)
+    r = eng.results(n, tcp_fields=True)
+    eng.receive_batch(b, r)
+    torch.cuda.synchronize()
+    got = r.to_numpy()
+    eng.close()
+    assert_same(got, run_oracle(mb, off, lens, flows), f"mbuf zero-copy data_off={data_off}")
+
+
 def test_counts_allreduce_one_rank(torch_cuda):
     """dk_rx_flow_counts_allreduce (and its out-of-place form) through a 1-rank RCCL communicator (ncclCommInitAll over
     device 0): the counters come back unchanged (the sum over one rank), per-frame results untouched."""
