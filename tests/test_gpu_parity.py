@@ -347,8 +347,12 @@ def test_tx_checksum_large_frames_schedule(torch_cuda):
     tx_check(blob, off, lens, "large")
 
 
-def test_host_pipeline_matches_device_path(torch_cuda):
-    """dk_rx_process_host (pinned host -> HBM -> host) gives the same results as the device-resident call."""
+@pytest.mark.parametrize("mem", ["pageable", "pinned_staged", "pinned_zero_copy"])
+def test_host_pipeline_matches_device_path(torch_cuda, monkeypatch, mem):
+    """dk_rx_process_host gives the oracle's results from pageable memory (staged copies), from pinned memory with
+    staging forced (DK_RX_HOST_ZC=0), and from pinned, GPU-mapped memory read in place (the default there)."""
+    import torch
+
     from demikernel_amd import RxResults
 
     flows = synth.make_flows(256)
@@ -357,6 +361,10 @@ def test_host_pipeline_matches_device_path(torch_cuda):
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr))
     exp = run_oracle(blob, off, lens, flows)
+    if mem != "pageable":
+        blob = torch.from_numpy(blob).pin_memory().numpy()
+    if mem == "pinned_staged":
+        monkeypatch.setenv("DK_RX_HOST_ZC", "0")
     eng = RxEngine(Config(LOCAL))
     eng.set_sockets(flows)
     r = RxResults(n, len(flows), tcp_fields=True, host=True)
