@@ -225,10 +225,15 @@ uint32_t dk_rx_flow_table_size(const dk_rx_ctx* ctx);
  * Returns 0, EINVAL (null required pointer, frames_bytes > DK_RX_MAX_BLOB) or EIO (launch failure). */
 int dk_rx_process(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results* res, void* stream);
 
-/* Process a batch that lives in host memory (a NIC ring / raw-socket buffer): chunked pinned-host -> HBM copies,
- * the kernel, and results copied back to host arrays, pipelined over the context's own streams. Synchronous.
- * batch/res pointers are host pointers (pinned for full PCIe rate). flow/verdict counts are host arrays too.
- * chunk_frames = frames per pipeline stage (0 = default). Returns 0, EINVAL, ENOMEM or EIO. */
+/* Process a batch that lives in host memory (a NIC ring / raw-socket buffer / DPDK mempool): the kernel, with
+ * descriptors copied in and results copied back to host arrays, over the context's own streams. Synchronous.
+ * batch/res pointers are host pointers. Frames in page-locked, GPU-mapped memory (hipHostMalloc, hipHostRegister)
+ * are read by the kernel in place over PCIe, one launch for the batch (zero-copy; DK_RX_HOST_ZC=0 at context creation
+ * turns it off); other memory is staged through chunked H2D copies pipelined over 3 streams. flow/verdict counts are
+ * host arrays too. chunk_frames = frames per pipeline stage (0 = default: 65,536 staged, the whole batch zero-copy).
+ * Returns 0, EINVAL, ENOMEM or EIO.
+ * (dk_rx_process itself also accepts a batch whose frames pointer is the device alias of mapped host memory: the
+ * DPDK-mbuf path of INTEGRATION.md.) */
 int dk_rx_process_host(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results* res, uint32_t chunk_frames);
 
 /* Multi-GPU packet shards: sum res->flow_counts[0 .. flow table size) and
