@@ -1704,6 +1704,9 @@ __global__ __launch_bounds__(kSsBlock, 2) void dk_rx_small_split_kernel(RxParams
 //     share of a chunk's time;
 //   kFin = 2 (768 threads, 3 waves/SIMD, 168 VGPRs, 4 staged chunks): mixed sizes (IMIX), where phase C of 64 frames
 //     costs as much as streaming them and one finisher per stream wave was the bottleneck.
+#ifndef DK_SPLIT_NT_RES
+#define DK_SPLIT_NT_RES true  // split kernels: result bursts nontemporal (C2 -0.3 %, C5 -1.4 %, steadier)
+#endif
 #ifndef DK_SPLIT2_STAGE_K
 #define DK_SPLIT2_STAGE_K 4
 #endif
@@ -1724,12 +1727,12 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
         (void)r.chunk(k_last - (uint32_t)q * stride, c, lim);
         if (stg[q].meta == kNoRec) continue;
         const uint32_t i = c + r.lane_off;
-        st_res(P.res.meta + i, stg[q].meta);
-        st_res(P.res.src_ip + i, stg[q].src);
-        if (P.res.dst_ip) st_res(P.res.dst_ip + i, stg[q].dst);
-        st_res(P.res.ports + i, stg[q].ports);
-        st_res(P.res.payload + i, stg[q].pay);
-        st_res(P.res.flow_id + i, stg[q].fid);
+        st_res<DK_SPLIT_NT_RES>(P.res.meta + i, stg[q].meta);
+        st_res<DK_SPLIT_NT_RES>(P.res.src_ip + i, stg[q].src);
+        if (P.res.dst_ip) st_res<DK_SPLIT_NT_RES>(P.res.dst_ip + i, stg[q].dst);
+        st_res<DK_SPLIT_NT_RES>(P.res.ports + i, stg[q].ports);
+        st_res<DK_SPLIT_NT_RES>(P.res.payload + i, stg[q].pay);
+        st_res<DK_SPLIT_NT_RES>(P.res.flow_id + i, stg[q].fid);
     }
 }
 
