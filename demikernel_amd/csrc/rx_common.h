@@ -25,6 +25,13 @@ namespace dk {
 //   TCP Active  (1, local_ip, remote_ip, local_port, remote_port)  SocketId::Active(local, remote)
 //   TCP Passive (2, local_ip, 0,         local_port, 0)            SocketId::Passive(local)
 //   UDP         (3, ip or 0.0.0.0, 0,    port,       0)            SocketAddrV4 (udp/peer.rs:38)
+// UDP binds and TCP listeners are keyed by a port alone once the address is fixed: every lookup asks for the configured
+// local address or 0.0.0.0, so they live in a direct-indexed port table (one exact load, no probe walk) after the
+// Active slots: words [kPortUdpLocal + port] (UDP bound to local_ipv4), [kPortUdpAny + port] (UDP on 0.0.0.0),
+// [kPortTcpPassive + port] (Passive on local_ipv4) hold the flow id or DK_FLOW_NONE. Entries for other local
+// addresses can never match a lookup and are not stored. The Active table holds only Active connections.
+constexpr uint32_t kPortUdpLocal = 0, kPortUdpAny = 1u << 16, kPortTcpPassive = 2u << 16;
+constexpr uint32_t kPortTabWords = 3u << 16;
 constexpr uint32_t kMaxFlows = (1u << 24) - 1;
 constexpr uint32_t kMinTableSlots = 16;
 
@@ -75,8 +82,9 @@ struct RxParams {
     uint32_t local_ip;
     uint32_t tcp_offload;
     uint32_t udp_offload;
-    const uint32_t* table;  // slots as 4 x u32
+    const uint32_t* table;  // Active slots as 4 x u32
     uint32_t table_mask;
+    const uint32_t* port_tab;  // kPortTabWords: UDP / Passive flow ids by port
     uint32_t nflows;
     uint32_t flow_mode;      // kFlow*
     uint32_t flow_words;     // kFlowLds: ceil(nflows / 2), else 0

@@ -68,7 +68,7 @@ struct Tuning {
 
 struct dk_rx_ctx {
     dk_rx_cfg cfg{};
-    uint32_t* table = nullptr;  // device, (mask + 1) * 4 u32
+    uint32_t* table = nullptr;  // device: (mask + 1) * 4 u32 of Active slots, then the kPortTabWords port table
     uint32_t table_mask = 0;
     uint32_t nflows = 0;
     // host pipeline state (lazily allocated)
@@ -336,6 +336,7 @@ dk::RxParams base_params(const dk_rx_ctx* c) {
     p.udp_offload = c->cfg.udp_rx_checksum_offload ? 1u : 0u;
     p.table = c->table;
     p.table_mask = c->table_mask;
+    p.port_tab = c->table + (size_t)(c->table_mask + 1) * 4;
     p.nflows = c->nflows;
     return p;
 }
@@ -374,7 +375,8 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     t.debug = env_knob("DK_RX_DEBUG");
     t.host_zc = env_knob("DK_RX_HOST_ZC");
     // Empty socket table: every probe misses.
-    std::vector<uint32_t> slots(dk::kMinTableSlots * 4, 0u);
+    std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
+    std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
     int rc = upload_table(c, slots, dk::kMinTableSlots - 1);
     if (rc) {
         delete c;
@@ -399,25 +401,40 @@ void dk_rx_ctx_destroy(dk_rx_ctx* c) {
 
 int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
     if (!c || (n && !flows) || n > dk::kMaxFlows) return EINVAL;
-    // load factor <= 1/8 (rx_common.h), tables up to 2^26 slots (1 GiB; 32-bit slot offsets), never above 1/2
-    const uint64_t want = std::min<uint64_t>(8ull * std::max(n, 1u), 1ull << 26);
-    const uint32_t cap = std::max({dk::kMinTableSlots, next_pow2((uint32_t)want), next_pow2(2 * std::max(n, 1u))});
-    const uint32_t mask = cap - 1;
-    std::vector<uint32_t> slots((size_t)cap * 4, 0u);
+    uint32_t nact = 0;
     for (uint32_t i = 0; i < n; i++) {
+        const uint32_t k = flows[i].kind;
+        if (k != DK_FLOW_TCP_ACTIVE && k != DK_FLOW_TCP_PASSIVE && k != DK_FLOW_UDP) return EINVAL;
+        nact += k == DK_FLOW_TCP_ACTIVE;
+    }
+    // Active connections: open addressing at load factor <= 1/8 (rx_common.h), up to 2^26 slots (1 GiB; 32-bit slot
+    // offsets), never above 1/2.
+    const uint64_t want = std::min<uint64_t>(8ull * std::max(nact, 1u), 1ull << 26);
+    const uint32_t cap = std::max({dk::kMinTableSlots, next_pow2((uint32_t)want), next_pow2(2 * std::max(nact, 1u))});
+    const uint32_t mask = cap - 1;
+    std::vector<uint32_t> slots((size_t)cap * 4 + dk::kPortTabWords, 0u);
+    uint32_t* ports_tab = slots.data() + (size_t)cap * 4;
+    std::fill(ports_tab, ports_tab + dk::kPortTabWords, DK_FLOW_NONE);
+    const uint32_t cfg_ip = c->cfg.local_ipv4;
+    for (uint32_t i = 0; i < n; i++) {  // in table order: HashMap::insert, the last duplicate wins
         const dk_flow& f = flows[i];
-        uint32_t lip = f.local_ip, rip = 0, ports = f.local_port;
-        if (f.kind == DK_FLOW_TCP_ACTIVE) {
-            rip = f.remote_ip;
-            ports |= (uint32_t)f.remote_port << 16;
-        } else if (f.kind != DK_FLOW_TCP_PASSIVE && f.kind != DK_FLOW_UDP) {
-            return EINVAL;
+        if (f.kind == DK_FLOW_UDP) {
+            // SocketAddrV4 keys: udp/peer.rs looks up (local_ipv4_addr, port), then (0.0.0.0, port) (udp/peer.rs:147-165);
+            // a bind to any other address is never looked up
+            if (f.local_ip == cfg_ip) ports_tab[dk::kPortUdpLocal + f.local_port] = i;
+            if (f.local_ip == 0) ports_tab[dk::kPortUdpAny + f.local_port] = i;
+            continue;
         }
+        if (f.kind == DK_FLOW_TCP_PASSIVE) {  // SocketId::Passive(local_ipv4_addr, port) (tcp/peer.rs:246-251)
+            if (f.local_ip == cfg_ip) ports_tab[dk::kPortTcpPassive + f.local_port] = i;
+            continue;
+        }
+        const uint32_t lip = f.local_ip, rip = f.remote_ip, ports = f.local_port | (uint32_t)f.remote_port << 16;
         uint32_t h = dk::flow_hash(f.kind, lip, rip, ports) & mask;
         for (;;) {
             uint32_t* s = &slots[(size_t)h * 4];
-            if (s[0] == 0 || ((s[0] >> 24) == f.kind && s[1] == lip && s[2] == rip && s[3] == ports)) {
-                s[0] = (f.kind << 24) | i;  // HashMap::insert: the last duplicate wins
+            if (s[0] == 0 || (s[1] == lip && s[2] == rip && s[3] == ports)) {
+                s[0] = (f.kind << 24) | i;
                 s[1] = lip;
                 s[2] = rip;
                 s[3] = ports;

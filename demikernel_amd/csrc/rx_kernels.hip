@@ -379,14 +379,12 @@ __device__ __forceinline__ uint32_t probe_finish(const RxParams& P, const ProbeK
     }
     return DK_FLOW_NONE;
 }
-__device__ __forceinline__ uint32_t probe(const RxParams& P, uint32_t kind, uint32_t lip, uint32_t rip,
-                                          uint32_t lport_rport) {
-    const ProbeKey k{kind, lip, rip, lport_rport};
-    const uint32_t h = probe_slot(P, k);
+// UDP binds and TCP listeners: one exact load of the port table (rx_common.h).
+__device__ __forceinline__ uint32_t port_lookup(const RxParams& P, uint32_t base, uint32_t port) {
 #ifdef DK_ABL_NOPROBE  // ablation (tuning only): no table load
-    return h & 1023u;
+    return port & 1023u;
 #endif
-    return probe_finish(P, k, h, reinterpret_cast<const uint4*>(P.table)[h]);
+    return P.port_tab[base + port];
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -819,16 +817,17 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     }
     DK_SUB_STAMP(0);
     // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
-    const bool pend4 = L.v == kPendTcp || L.v == kPendUdp;
+    // TCP: the Active slot (hashed); UDP: the flow bound to (local_ip, port), one load of the port table.
     St.fast = fast;
-    const ProbeKey k1 = L.v == kPendTcp
-                            ? ProbeKey{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)}
-                            : ProbeKey{DK_FLOW_UDP, P.local_ip, 0u, L.ports >> 16};
+    const ProbeKey k1{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)};
     St.k1 = k1;
     const uint32_t h1 = probe_slot(P, k1);
     St.h1 = h1;
     St.s1 = make_uint4(0, 0, 0, 0);
-    if (pend4) St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+#ifndef DK_ABL_NOPROBE
+    if (L.v == kPendTcp) St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+    else if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+#endif
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
     DK_SUB_STAMP(1);
 }
@@ -872,12 +871,12 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
         if (L.v == kPendTcp) {
             // SocketId::Active(local=(local_ip, dport), remote=(src, sport)), then Passive(local) (tcp/peer.rs:241-251)
             fid = probe_finish(P, k1, h1, s1);  // Active(local, remote)
-            if (fid == DK_FLOW_NONE) fid = probe(P, DK_FLOW_TCP_PASSIVE, P.local_ip, 0u, dport);
+            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortTcpPassive, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
         } else if (L.v == kPendUdp) {
             // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
-            fid = probe_finish(P, k1, h1, s1);  // (local_ip, port)
-            if (fid == DK_FLOW_NONE) fid = probe(P, DK_FLOW_UDP, 0u, 0u, dport);
+            fid = s1.x;  // (local_ip, port)
+            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortUdpAny, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
         }
     }
