@@ -257,6 +257,43 @@ def test_duplicate_and_large_flow_tables(torch_cuda):
     assert (got["flow_id"][tr.flow < 5000] >= len(flows)).all()
 
 
+@pytest.mark.parametrize("local", [LOCAL, "0.0.0.0"])
+def test_port_table_lookups(torch_cuda, local):
+    """UDP binds and TCP listeners (the direct-indexed port table, rx_common.h) against the oracle's HashMap lookups:
+    binds on the configured address, on 0.0.0.0 and on another address (never looked up), duplicates (the last wins),
+    ports 0 and 65535, listeners on the configured address, on 0.0.0.0 and elsewhere (Passive lookups ask for the
+    configured address only), Active connections on a listener's port, and unbound ports; with the configured address
+    a real one and 0.0.0.0 (then both UDP lookups ask for the same key)."""
+    from demikernel_amd._native import DK_FLOW_TCP_ACTIVE as ACT, DK_FLOW_TCP_PASSIVE as PAS, DK_FLOW_UDP as UDP
+
+    lip, other = ipv4(local), ipv4("10.9.9.9")
+    rows = [(UDP, lip, 0, p, 0) for p in (0, 1, 53, 5000, 5001, 65535)]
+    rows += [(UDP, 0, 0, p, 0) for p in (53, 6000, 6001, 65535)]
+    rows += [(UDP, other, 0, p, 0) for p in (5000, 7000)]
+    rows += [(UDP, lip, 0, 5001, 0), (UDP, 0, 0, 6000, 0)]  # duplicates: the last wins
+    rows += [(PAS, lip, 0, p, 0) for p in (80, 443, 0, 65535)]
+    rows += [(PAS, other, 0, 8080, 0), (PAS, 0, 0, 9090, 0), (PAS, lip, 0, 443, 0)]
+    active = synth.make_flows(200, local_ip=local, passive=False)
+    active["local_port"][:100] = 80  # established connections accepted by the port-80 listener
+    table = np.concatenate([np.array(rows, dtype=FLOW_DTYPE), active])
+    rng = np.random.default_rng(21)
+    udp_ports = [0, 1, 53, 5000, 5001, 6000, 6001, 7000, 65535, 12345]
+    tcp_ports = [80, 443, 0, 65535, 8080, 9090, 22]
+    tu = np.array([(UDP, lip, 0, p, 0) for p in udp_ports], dtype=FLOW_DTYPE)
+    tt = np.zeros(64, dtype=FLOW_DTYPE)  # segments from remotes with no Active entry: Passive or nothing
+    tt["kind"], tt["local_ip"] = ACT, lip
+    tt["remote_ip"] = (172 | 16 << 8 | rng.integers(0, 256, 64, dtype=np.uint32) << 16 | 7 << 24).astype(np.uint32)
+    tt["remote_port"] = rng.integers(1024, 65535, 64, dtype=np.uint16)
+    tt["local_port"] = np.array(tcp_ports, np.uint16)[np.arange(64) % len(tcp_ports)]
+    targets = np.concatenate([tu, tt, active])
+    n = 20000
+    tr = synth.traffic(n, 200, targets, local_ip=local, seed=9)
+    blob, off, lens = synth.build_numpy(tr)
+    got = check(blob, off, lens, table, Config(local), ctx=f"port table local={local}")
+    seen = {VERDICTS[m & 0xFF] for m in got["meta"]}
+    assert {"OK_UDP", "UDP_NOSOCK", "OK_TCP", "TCP_NOSOCK"} <= seen, seen
+
+
 def tx_check(blob, off, lens, ctx=""):
     """dk_tx_checksum on the GPU vs the oracle's serialize_and_attach restatement, frame by frame, whole blob."""
     import torch
