@@ -1093,6 +1093,9 @@ __device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
 __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
                                                const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
     if (!P.row_words) return;
+#ifdef DK_ABL_NOFLUSH  // ablation (tuning only): counters never leave LDS, no combine
+    return;
+#endif
     uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_stride;
     if (!P.fused) {  // rows with plain stores; dk_flow_reduce_kernel (a second launch) adds them up
         if (lds_flows)
@@ -2178,7 +2181,11 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     else
         hipLaunchKernelGGL((dk::dk_rx_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     if (hipGetLastError() != hipSuccess) return 5;
+#ifdef DK_ABL_NOFLUSH
+    if (false) {
+#else
     if (p.row_words && !p.fused) {
+#endif
         const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
                       (grid + dk::kReduceRows - 1) / dk::kReduceRows);
         hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, s, p.flow_scratch, grid, p.row_words,

@@ -215,9 +215,11 @@ typedef struct dk_rx_ctx dk_rx_ctx;
 int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out);
 void dk_rx_ctx_destroy(dk_rx_ctx* ctx);
 
-/* Install the socket table (host array of n entries; copied to HBM as an open-addressing hash table). Plays the role
- * of TcpPeer::addresses / UdpPeer::addresses (tcp/peer.rs, udp/peer.rs:38). Duplicate keys: the last entry wins,
- * as with HashMap::insert. Returns 0, EINVAL (bad kind) or ENOMEM. Synchronous. */
+/* Install the socket table (host array of n entries; copied to HBM: Active connections as an open-addressing hash
+ * table, UDP binds and TCP listeners as a port-indexed table for the configured local address and 0.0.0.0 — the only
+ * addresses the reference looks them up with). Plays the role of TcpPeer::addresses / UdpPeer::addresses (tcp/peer.rs,
+ * udp/peer.rs:38). Duplicate keys: the last entry wins, as with HashMap::insert. Returns 0, EINVAL (bad kind) or
+ * ENOMEM. Synchronous. */
 int dk_rx_flow_table_set(dk_rx_ctx* ctx, const dk_flow* flows, uint32_t n);
 uint32_t dk_rx_flow_table_size(const dk_rx_ctx* ctx);
 
