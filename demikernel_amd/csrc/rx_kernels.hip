@@ -255,8 +255,8 @@ __device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const 
     const uint32_t frag = a.be16(20);
     const uint32_t proto = a.b8(23);
     const uint32_t ipcs = a.be16(24);
-    const uint32_t hsum = a.le16(14) + a.le16(16) + a.le16(18) + a.le16(20) + a.le16(22) + a.le16(26) + a.le16(28) +
-                          a.le16(30) + a.le16(32);
+    // the 9 words of compute_checksum, whole dwords through v_dot2 (words at 16..22 and 28..30 are dwords 4, 5, 7)
+    const uint32_t hsum = hsum2(a.w[7], hsum2(a.w[5], hsum2(a.w[4], (a.w[3] >> 16) + (a.w[6] >> 16) + (a.w[8] & 0xFFFFu))));
     const uint32_t src = a.u32(26), dst = a.u32(30);
     const uint32_t seg = tot - 20;
     const uint32_t b12 = a.b8(46);
@@ -707,6 +707,12 @@ template <class WL>
 __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WL& W, uint32_t lane, const uint8_t* f,
                                                  int E, bool& resum) {
     const RegAcc& R = C.R;
+    if (!__ballot(C.big || E != 64)) {  // every active lane: [34, 64) is the window's dwords 8 (upper half) .. 15
+        uint32_t acc = hsum2(R.w[8] & 0xFFFF0000u, 0);
+#pragma unroll
+        for (int k = 9; k < 16; k++) acc = hsum2(R.w[k], acc);
+        return acc;
+    }
     if (!C.big) {
         // [34, E) inside the register window, E even in [34, 64]: dword k keeps its bytes below E, i.e. the low
         // 32 - sh bits with sh = clamp(32 - 8 (E - 4k), 0, 32) — one 64-bit shift per dword instead of two clamped
@@ -821,13 +827,18 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     St.fast = fast;
     const ProbeKey k1{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)};
     St.k1 = k1;
-    const uint32_t h1 = probe_slot(P, k1);
-    St.h1 = h1;
     St.s1 = make_uint4(0, 0, 0, 0);
+    uint32_t h1 = 0;
+    if (L.v == kPendTcp) {  // the hash only for TCP lanes (a wave of UDP frames skips it)
+        h1 = probe_slot(P, k1);
 #ifndef DK_ABL_NOPROBE
-    if (L.v == kPendTcp) St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
-    else if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+        St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
 #endif
+    }
+#ifndef DK_ABL_NOPROBE
+    if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+#endif
+    St.h1 = h1;
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
     DK_SUB_STAMP(1);
 }
