@@ -35,6 +35,8 @@ WORKLOADS = {
                    "tcp", 1),
     "c2_tcp1500": ("1M x 1500B IPv4/TCP, 1024 flows, device-resident", 1 << 20, 1486, "tcp", 1024),
     "c3_udp64": ("1M x 64B IPv4/UDP (min-size), device-resident, 8 rotating batches", 1 << 20, 50, "udp", 1024),
+    "c3_udp64_random_ports": ("C3 with the 1,024 UDP binds on random ports (1024..65535) instead of consecutive ones",
+                              1 << 20, 50, "udp_random_ports", 1024),
     "c4_imix": ("IMIX 40/576/1500 at 7:4:1, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, "imix", "tcp", 1024),
     "c5_tcp1500_10k": ("1500B IPv4/TCP, 10k flows, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, 1486, "tcp", 10000),
 }
@@ -517,7 +519,7 @@ def main():
     name = args.workload
     batch, flows, tr = make_batch(eng, name, rank, synth.SEED, world)
     batches = [batch]
-    if name == "c3_udp64":  # 64 B batches fit in the 256 MB MALL: rotate 8 distinct batches (> 512 MB)
+    if name.startswith("c3_udp64"):  # 64 B batches fit in the 256 MB MALL: rotate 8 distinct batches (> 512 MB)
         batches += [make_batch(eng, name, rank, synth.SEED + 1000 * k, world)[0] for k in range(1, 8)]
     res = eng.results(batch.n)
     frame_bytes = int(tr.frame_len.astype(np.int64).sum())
@@ -607,6 +609,8 @@ def main():
         c3, e, _, _ = rx_extra("c3_udp64", dev, stream, steps=40, warmup=4, rotate=8)
         c3b, e, _, _ = rx_extra("c3_udp64", dev, stream, steps=40, warmup=4, rotate=8, dst_ip=False)
         c3["compact_20B_results"] = {k: c3b[k] for k in ("gbps", "mpkt_s", "kernel_ms_avg", "roofline")}
+        c3r, e, _, _ = rx_extra("c3_udp64_random_ports", dev, stream, steps=40, warmup=4, rotate=8)
+        c3["random_ports"] = {k: c3r[k] for k in ("workload", "gbps", "mpkt_s", "kernel_ms_avg", "roofline")}
         out["c3_udp64"] = c3
         del e
         out["c4_imix"], e, _, _ = rx_extra("c4_imix", dev, stream)

@@ -50,7 +50,10 @@ def make_flows(nflows: int, local_ip: str = BOB_IPV4, kind: str = "tcp", seed: i
     a = np.zeros(nflows, dtype=FLOW_DTYPE)
     a["kind"] = DK_FLOW_UDP
     a["local_ip"] = lip
-    a["local_port"] = (5000 + np.arange(nflows)).astype(np.uint16)
+    if kind == "udp_random_ports":  # binds spread over the port space (no two on one cache line of the port table)
+        a["local_port"] = rng.permutation(np.arange(1024, 65536, dtype=np.uint32))[:nflows].astype(np.uint16)
+    else:
+        a["local_port"] = (5000 + np.arange(nflows)).astype(np.uint16)
     return a
 
 
