@@ -38,6 +38,8 @@ WORKLOADS = {
     "c3_udp64_random_ports": ("C3 with the 1,024 UDP binds on random ports (1024..65535) instead of consecutive ones",
                               1 << 20, 50, "udp_random_ports", 1024),
     "c4_imix": ("IMIX 40/576/1500 at 7:4:1, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, "imix", "tcp", 1024),
+    "c4_imix_tilesorted": ("IMIX with each 256-frame tile sorted by size (tuning probe, not a bench line)", 1 << 21,
+                           "imix_tilesorted", "tcp", 1024),
     "c5_tcp1500_10k": ("1500B IPv4/TCP, 10k flows, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, 1486, "tcp", 10000),
 }
 
@@ -57,7 +59,13 @@ def make_batch(eng, name, rank, seed_base, world=1):
     _, n, ip_len, kind, nflows = WORKLOADS[name]
     flows = synth.make_flows(nflows, kind=kind)
     total = n * world
-    ip_all = synth.imix_ip_lengths(total, seed_base) if ip_len == "imix" else np.full(total, ip_len, np.uint16)
+    if isinstance(ip_len, str) and ip_len.startswith("imix"):
+        ip_all = synth.imix_ip_lengths(total, seed_base)
+        if ip_len == "imix_tilesorted":
+            m = total // 256 * 256
+            ip_all[:m] = np.sort(ip_all[:m].reshape(-1, 256), axis=1).reshape(-1)
+    else:
+        ip_all = np.full(total, ip_len, np.uint16)
     frame_all = np.maximum(ip_all.astype(np.int64) + 14, synth.ETH_MIN_FRAME)
     a, b = byte_balanced_shards(frame_all, world)[rank]
     seed = seed_base + 7919 * rank
