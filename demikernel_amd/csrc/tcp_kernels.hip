@@ -389,6 +389,10 @@ constexpr uint32_t kWave = 64;
 
 using WaveScan = rocprim::warp_scan<uint32_t, kWave>;
 
+// kAhead: segment records kAhead windows ahead, frame indices kAhead + 1 (1 for many connections, where occupancy
+// hides the record latency; more for few connections, where one wave's window loop is the whole run and each window
+// otherwise waits out a record load).
+template <int kAhead>
 __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     __shared__ WaveScan::storage_type scan_tmp;
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
@@ -407,18 +411,25 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     }
     Out o{P.out.deliv + d0, 0, cnt + DK_TCP_DELIV_EXTRA};
     const uint32_t wend = w.reader + w.bufsz;
-    // Software pipeline over windows: frame indices two windows ahead, records one window ahead.
-    uint32_t icur = lane < cnt ? P.svals[k0 + lane] : 0u;
-    uint4 gnext = lane < cnt ? P.rec[icur] : make_uint4(0u, 0u, 0u, 0u);
-    uint32_t inext = kWave + lane < cnt ? P.svals[k0 + kWave + lane] : 0u;
+    // Software pipeline over windows: frame indices kAhead + 1 windows ahead, records kAhead windows ahead (register
+    // rings iq / gq: slot j holds window base / 64 + j).
+    uint32_t iq[kAhead + 1];
+    uint4 gq[kAhead];
+#pragma unroll
+    for (int j = 0; j <= kAhead; j++) iq[j] = j * kWave + lane < cnt ? P.svals[k0 + j * kWave + lane] : 0u;
+#pragma unroll
+    for (int j = 0; j < kAhead; j++) gq[j] = j * kWave + lane < cnt ? P.rec[iq[j]] : make_uint4(0u, 0u, 0u, 0u);
     for (uint32_t base = 0; base < cnt; base += kWave) {
         const uint32_t lim = min(cnt - base, kWave);
         const bool have = lane < lim;
-        const uint32_t i = icur;
-        const uint4 g = gnext;
-        icur = inext;
-        gnext = base + kWave + lane < cnt ? P.rec[icur] : make_uint4(0u, 0u, 0u, 0u);
-        inext = base + 2 * kWave + lane < cnt ? P.svals[k0 + base + 2 * kWave + lane] : 0u;
+        const uint32_t i = iq[0];
+        const uint4 g = gq[0];
+#pragma unroll
+        for (int j = 0; j < kAhead; j++) iq[j] = iq[j + 1];
+#pragma unroll
+        for (int j = 0; j + 1 < kAhead; j++) gq[j] = gq[j + 1];
+        gq[kAhead - 1] = base + kAhead * kWave + lane < cnt ? P.rec[iq[kAhead - 1]] : make_uint4(0u, 0u, 0u, 0u);
+        iq[kAhead] = base + (kAhead + 1) * kWave + lane < cnt ? P.svals[k0 + base + (kAhead + 1) * kWave + lane] : 0u;
         const uint32_t flags = (g.z >> 16) & 0xFFu, off = g.w & 0xFFFFu, len = g.w >> 16;
         const bool simple = have && !(flags & 0x07u);
         const bool ack_ok = (flags & 0x10u) && le(g.y, w.snd);
@@ -526,6 +537,15 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
 // Which walk runs: `force` (DK_TCP_WALK=lane|wave, read once at dk_tcp_ctx_create: 0 lane, 1 wave, -1 the rule);
 // otherwise the wave walk when connections average at least kWaveWalkMinSegs segments in the batch.
 constexpr uint32_t kWaveWalkMinSegs = 8;
+// Up to this many connections (waves) the wave walk prefetches DK_TCP_DEEP_AHEAD windows of records: a few waves per
+// SIMD at most, so the extra registers cost no occupancy.
+#ifndef DK_TCP_DEEP_AHEAD
+#define DK_TCP_DEEP_AHEAD 4
+#endif
+#ifndef DK_TCP_DEEP_MAX_CONNS
+#define DK_TCP_DEEP_MAX_CONNS 2048
+#endif
+constexpr uint32_t kDeepAheadMaxConns = DK_TCP_DEEP_MAX_CONNS;
 bool use_wave_walk(uint32_t n, uint32_t nconns, int force) {
     if (nconns > (1u << 24)) return false;  // grid of nconns waves
     if (force >= 0) return force == 1;
@@ -660,7 +680,10 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
     if (nconns) {
         if (use_wave_walk(n, nconns, t->walk))
-            hipLaunchKernelGGL(dk_tcp_wave_walk_kernel, dim3(nconns), dim3(kWave), 0, s, P);
+            if (nconns <= kDeepAheadMaxConns)
+                hipLaunchKernelGGL(dk_tcp_wave_walk_kernel<DK_TCP_DEEP_AHEAD>, dim3(nconns), dim3(kWave), 0, s, P);
+            else
+                hipLaunchKernelGGL(dk_tcp_wave_walk_kernel<1>, dim3(nconns), dim3(kWave), 0, s, P);
         else
             hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
     }
