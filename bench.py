@@ -49,14 +49,15 @@ def dist_env():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")), ws
 
 
-def make_batch(eng, name, rank, seed_base, world=1):
+def make_batch(eng, name, rank, seed_base, world=1, frames=0):
     """This rank's packet shard of the global batch (world x frames-per-GPU frames, weak scaling): the frame-size
     sequence is global and seeded, the shard boundaries are byte-balanced (demikernel_amd.shard), and each rank
-    synthesises only its own frames on its own GPU."""
+    synthesises only its own frames on its own GPU. frames > 0 overrides the workload's frames per GPU."""
     from demikernel_amd import synth
     from demikernel_amd.shard import byte_balanced_shards
 
     _, n, ip_len, kind, nflows = WORKLOADS[name]
+    n = frames or n
     flows = synth.make_flows(nflows, kind=kind)
     total = n * world
     if isinstance(ip_len, str) and ip_len.startswith("imix"):
@@ -111,18 +112,14 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
     kern = e0.elapsed_time(e1) / 1e3 / steps
     coll = []
     if comm is not None:  # the collective alone, unoverlapped, for the report
-        r = sr.res[0]
         for _ in range(5):
             c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             c0.record(sr.side)
-            if hasattr(comm, "handle"):
-                eng.counts_allreduce(r, comm.handle, stream=sr.side)
-            else:  # shard.TorchCountsAllreduce fallback
-                comm(r, sr.side)
+            sr.reduce(0, sr.side)
             c1.record(sr.side)
             torch.cuda.synchronize()
             coll.append(c0.elapsed_time(c1) / 1e3)
-    return wall, kern, coll
+    return wall, kern, coll, sr
 
 
 def mbuf_zero_copy_rate(dev, stream, n=1 << 17, slot=2048, data_off=128, reps=5):
@@ -458,7 +455,7 @@ def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True):
     _, flows, tr = made[0]
     n = batches[0].n
     res = eng.results(n, dst_ip=dst_ip)
-    wall, kern, _ = time_kernel(eng, batches, res, steps, warmup, stream)
+    wall, kern, _, _ = time_kernel(eng, batches, res, steps, warmup, stream)
     fb = int(tr.frame_len.astype(np.int64).sum())
     rb = RESULT_BYTES if dst_ip else RESULT_BYTES - 4
     algo = fb + n * (DESC_BYTES + rb)
@@ -485,7 +482,14 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--backend", default="gloo", choices=["nccl", "gloo"],
                     help="N > 1: process group for the barrier and the max-over-ranks timing only (the counters are "
-                         "reduced by dk_rx_flow_counts_allreduce over RCCL either way)")
+                         "reduced by dk_rx_flow_counts_allreduce_to over RCCL)")
+    ap.add_argument("--frames-per-gpu", type=int, default=0,
+                    help="override the workload's frames per GPU (tests only; the line's config records it)")
+    ap.add_argument("--counts-via-torch-gloo-test", action="store_true",
+                    help="TEST ONLY: reduce the counters through torch.distributed gloo instead of the product's RCCL "
+                         "communicator (2 ranks on one GPU, which RCCL refuses); the line names it")
+    ap.add_argument("--counts-out", default="",
+                    help="write the node-wide flow / verdict counters after the timed steps to this .npz (rank 0)")
     args = ap.parse_args()
 
     import torch
@@ -509,30 +513,37 @@ def main():
     from demikernel_amd.shard import broadcast_comm_id
 
     collective = "none"
-    if world > 1:  # the receive path's own RCCL communicator (include/dk_comm.h), bootstrapped over the process group
+    if world > 1 and args.counts_via_torch_gloo_test:
+        from demikernel_amd.shard import TorchCountsAllreduce
+
+        comm = TorchCountsAllreduce(dist.group.WORLD if args.backend == "gloo" else dist.new_group(backend="gloo"))
+        collective = "TEST ONLY: torch.distributed gloo all_reduce of the counters (--counts-via-torch-gloo-test)"
+    elif world > 1:  # the receive path's own RCCL communicator (include/dk_comm.h), bootstrapped over the process group
         try:
             comm = Comm.init_rank(world, broadcast_comm_id(dist, Comm.unique_id), rank, dev)
-            collective = ("dk_rx_flow_counts_allreduce (RCCL all-reduce of u64 flow + verdict counters) per step on a "
-                          "side stream, double-buffered (overlaps the next step's kernel)")
-        except Exception as e:  # noqa: BLE001 — keep the scaling run alive; the line says which collective ran
-            from demikernel_amd.shard import TorchCountsAllreduce
-
-            print(f"bench: dk_comm_init_rank failed ({e}); counters reduced through torch.distributed nccl",
-                  file=sys.stderr)
-            comm = TorchCountsAllreduce(dist.new_group(backend="nccl"))
-            collective = "torch.distributed nccl all_reduce of the counters (fallback: dk_comm init failed)"
+        except Exception as e:  # noqa: BLE001 — no silent fallback: a scaling line must come from the product collective
+            print(f"bench: rank {rank}: dk_comm_init_rank failed ({e}); the packet-sharded path needs the RCCL "
+                  f"communicator of include/dk_comm.h", file=sys.stderr, flush=True)
+            sys.exit(3)
+        collective = ("dk_rx_flow_counts_allreduce_to (RCCL all-reduce of accumulating u64 flow + verdict counters) "
+                      "per step on a side stream, double-buffered (overlaps the next step's kernel)")
 
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
     stream = torch.cuda.current_stream(dev)
     name = args.workload
-    batch, flows, tr = make_batch(eng, name, rank, synth.SEED, world)
+    batch, flows, tr = make_batch(eng, name, rank, synth.SEED, world, args.frames_per_gpu)
     batches = [batch]
     if name.startswith("c3_udp64"):  # 64 B batches fit in the 256 MB MALL: rotate 8 distinct batches (> 512 MB)
-        batches += [make_batch(eng, name, rank, synth.SEED + 1000 * k, world)[0] for k in range(1, 8)]
+        batches += [make_batch(eng, name, rank, synth.SEED + 1000 * k, world, args.frames_per_gpu)[0]
+                    for k in range(1, 8)]
     res = eng.results(batch.n)
     frame_bytes = int(tr.frame_len.astype(np.int64).sum())
 
-    wall, kern_avg, coll = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist, comm)
+    wall, kern_avg, coll, sr = time_kernel(eng, batches, res, args.steps, args.warmup, stream, dist, comm)
+    if args.counts_out and rank == 0:
+        fc, vc = sr.counts()
+        np.savez(args.counts_out, flow_counts=fc.cpu().numpy().view(np.uint64),
+                 verdict_counts=vc.cpu().numpy().view(np.uint64), steps=args.steps + args.warmup)
     if dist is not None:
         cdev = "cuda" if args.backend == "nccl" else "cpu"
         t = torch.tensor([wall], dtype=torch.float64, device=cdev)

@@ -82,6 +82,7 @@ FUNCTIONS = [
     ("dk_rx_flow_table_size", c_uint32, [c_void_p]),
     ("dk_rx_process", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_void_p]),
     ("dk_rx_process_host", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_uint32]),
+    ("dk_rx_stream_forget", c_int, [c_void_p, c_void_p]),
     ("dk_rx_flow_counts_allreduce", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p]),
     ("dk_rx_flow_counts_allreduce_to", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p, c_void_p,
                                                c_void_p]),

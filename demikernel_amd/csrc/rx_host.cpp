@@ -36,11 +36,14 @@ struct CountScratch {
 
 // A context's scratch is keyed by stream: calls on different streams never share counter rows or tickets, so their
 // launches may run concurrently. Past kMaxStreamSlots streams the least recently used slot is taken over, and the new
-// stream first waits for the slot's last launch (its event).
+// stream first waits for the slot's last launch (its event). Streams must outlive the context or be released with
+// dk_rx_stream_forget (dk_rx.h), so the handle a slot keeps is valid whenever it is used.
 struct StreamSlot {
     hipStream_t stream = nullptr;
     CountScratch cs;
-    hipEvent_t last = nullptr;  // non-null once the slot is in use; ordering event for a takeover
+    hipEvent_t last = nullptr;  // ordering event for a takeover (created with the slot's first use)
+    bool used = false;          // the slot belongs to `stream`
+    bool recorded = false;      // `last` was recorded after the slot's most recent launch
     uint64_t stamp = 0;
 };
 
@@ -78,6 +81,7 @@ struct dk_rx_ctx {
     uint64_t* d_verdict_counts = nullptr;
     StreamSlot slots[kMaxStreamSlots];
     uint64_t clock = 0;
+    bool saturated = false;  // a slot has been taken over: slot events are recorded after each launch
     Tuning tune;
     uint32_t cu_count = 0;
     uint32_t occ_dyn = ~0u;   // occupancy cache: dynamic LDS bytes -> resident blocks per CU
@@ -123,30 +127,43 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
     return 0;
 }
 
-void free_slot(StreamSlot& s) {  // the caller has synchronised the device
+void free_slot(StreamSlot& s) {  // the caller has waited for the slot's launches
     if (s.cs.rows) (void)hipFree(s.cs.rows);
     if (s.cs.tickets) (void)hipFree(s.cs.tickets);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
 }
 
-// The slot of `stream`. Past kMaxStreamSlots streams the least recently used slot is taken over: an event recorded on
-// its stream now completes after every launch that used the slot, and the new stream waits for it.
+// Wait (host side) for every launch that used the slot: its recorded event, else its stream; if neither can be waited
+// for, the whole device.
+void wait_slot(StreamSlot& s) {
+    if (!s.used) return;
+    if (s.recorded ? hipEventSynchronize(s.last) == hipSuccess : hipStreamSynchronize(s.stream) == hipSuccess) return;
+    (void)hipGetLastError();
+    (void)hipDeviceSynchronize();
+}
+
+// The slot of `stream`. Past kMaxStreamSlots streams the least recently used slot is taken over: the new stream waits
+// for an event that completes after every launch that used the slot. From the first takeover on, the context records
+// each slot's event right after its launches (`saturated`), so a later takeover waits on an event recorded while its
+// stream was in use; before that (<= 8 streams: the common case) no launch pays for an event record (~3 us).
 #ifndef DK_SLOT_EVENTS
 #define DK_SLOT_EVENTS 0  // 1: record the slot's event after every launch (measured: costs the launch gap)
 #endif
 int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
     StreamSlot* pick = nullptr;
     for (StreamSlot& s : c->slots)
-        if (s.last && s.stream == stream) pick = &s;
+        if (s.used && s.stream == stream) pick = &s;
     if (!pick)
         for (StreamSlot& s : c->slots)
-            if (!s.last) {
-                if (hipEventCreateWithFlags(&s.last, hipEventDisableTiming) != hipSuccess) {
+            if (!s.used) {
+                if (!s.last && hipEventCreateWithFlags(&s.last, hipEventDisableTiming) != hipSuccess) {
                     s.last = nullptr;
                     return EIO;
                 }
                 s.stream = stream;
+                s.used = true;
+                s.recorded = false;
                 pick = &s;
                 break;
             }
@@ -154,11 +171,17 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
         pick = &c->slots[0];
         for (StreamSlot& s : c->slots)
             if (s.stamp < pick->stamp) pick = &s;
-#if !DK_SLOT_EVENTS
-        if (hipEventRecord(pick->last, pick->stream) != hipSuccess) return EIO;
-#endif
-        if (hipStreamWaitEvent(stream, pick->last, 0) != hipSuccess) return EIO;
+        c->saturated = true;
+        bool ordered = pick->recorded;
+        if (!ordered && hipEventRecord(pick->last, pick->stream) == hipSuccess) ordered = true;
+        if (ordered) {
+            if (hipStreamWaitEvent(stream, pick->last, 0) != hipSuccess) return EIO;
+        } else {  // the old stream cannot be recorded on: wait for its work on the host instead
+            (void)hipGetLastError();
+            if (hipDeviceSynchronize() != hipSuccess) return EIO;
+        }
         pick->stream = stream;
+        pick->recorded = false;
     }
     pick->stamp = ++c->clock;
     *out = pick;
@@ -255,12 +278,13 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
+    // Per-workgroup histogram rows (flow pairs, then verdicts), combined in-launch per group of workgroups. Only a
+    // launch with counters uses the stream's scratch slot.
     StreamSlot* slot = nullptr;
-    int rc = acquire_slot(c, stream, &slot);
-    if (rc) return rc;
-    // Per-workgroup histogram rows (flow pairs, then verdicts), combined in-launch per group of workgroups.
+    int rc = 0;
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
     if (p.row_words) {
+        if ((rc = acquire_slot(c, stream, &slot))) return rc;
         p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
         if ((rc = ensure_counts(*slot, grid, p.row_stride))) return rc;
         p.flow_scratch = slot->cs.rows;
@@ -273,9 +297,10 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
                 p.small, p.fused);
     rc = dk_launch_rx(p, grid, stream);
-#if DK_SLOT_EVENTS
-    if (rc == 0 && hipEventRecord(slot->last, stream) != hipSuccess) rc = EIO;
-#endif
+    if (rc == 0 && slot && (DK_SLOT_EVENTS || c->saturated)) {
+        if (hipEventRecord(slot->last, stream) != hipSuccess) return EIO;
+        slot->recorded = true;
+    }
     return rc;
 }
 
@@ -389,12 +414,16 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
 void dk_rx_ctx_destroy(dk_rx_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->cfg.device);
+    // Wait for this context's launches only: each slot's stream (or its last recorded event) and the pipeline's own
+    // streams; then free the scratch.
+    for (StreamSlot& s : c->slots) wait_slot(s);
+    for (Stage& s : c->stages)
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+    for (StreamSlot& s : c->slots) free_slot(s);
     if (c->table) (void)hipFree(c->table);
     for (Stage& s : c->stages) free_stage(s);
     if (c->d_flow_counts) (void)hipFree(c->d_flow_counts);
     if (c->d_verdict_counts) (void)hipFree(c->d_verdict_counts);
-    (void)hipDeviceSynchronize();  // launches still using the context's scratch (streams may be gone)
-    for (StreamSlot& s : c->slots) free_slot(s);
     if (c->d_path_stats) (void)hipFree(c->d_path_stats);
     delete c;
 }
@@ -466,6 +495,22 @@ int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, vo
     p.aligned16 = (b->flags & DK_RX_BATCH_ALIGNED16) ? 1u : 0u;
     p.res = *r;
     return launch_batch(c, p, b->frames_bytes, (hipStream_t)stream);
+}
+
+int dk_rx_stream_forget(dk_rx_ctx* c, void* stream) {
+    if (!c) return EINVAL;
+    DeviceGuard g(c->cfg.device);
+    for (StreamSlot& s : c->slots) {
+        if (!s.used || s.stream != (hipStream_t)stream) continue;
+        const bool ok = s.recorded ? hipEventSynchronize(s.last) == hipSuccess
+                                   : hipStreamSynchronize(s.stream) == hipSuccess;
+        if (!ok) return EIO;
+        s.used = false;  // scratch buffers and the event stay for the slot's next stream
+        s.recorded = false;
+        s.stream = nullptr;
+        s.stamp = 0;
+    }
+    return 0;
 }
 
 namespace {

@@ -219,6 +219,12 @@ class RxEngine:
         _check(self.lib.dk_rx_process(self._ctx, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(s.cuda_stream)),
                "dk_rx_process")
 
+    def forget_stream(self, stream) -> None:
+        """dk_rx_stream_forget: release this context's scratch of `stream` (a torch.cuda.Stream or a raw hipStream_t
+        handle) before the stream is destroyed."""
+        h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        _check(self.lib.dk_rx_stream_forget(self._ctx, ctypes.c_void_p(h)), "dk_rx_stream_forget")
+
     def receive_batch_host(self, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, results: RxResults,
                            chunk_frames: int = 0, aligned16: Optional[bool] = None) -> None:
         """Host-resident batch (NIC ring / socket buffer): pipelined H2D -> kernel -> D2H. Synchronous.

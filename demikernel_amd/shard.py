@@ -7,10 +7,12 @@ RCCL / xGMI through the C ABI (dk_rx_flow_counts_allreduce on a dk_comm.h commun
 their GPU; frame bytes never cross xGMI.
 
 `ShardedReceiver` is the per-rank driver bench.py --gpus N runs (one process per GPU under torchrun): it bootstraps
-the RCCL communicator (rank 0's id handed out over the launcher's process group), receives the rank's shard and
-all-reduces the counters on a side stream so the reduction of batch k overlaps the kernel of batch k + 1. The CPU
-rehearsal (tests/test_multiproc.py, gloo, world size 2) drives the same sharding and bootstrap code with torch's
-all_reduce standing in for the RCCL call, which is covered on the GPU by a 1-rank communicator test.
+the RCCL communicator (rank 0's id handed out over the launcher's process group), receives the rank's shard into
+accumulating counters and all-reduces them out of place on a side stream, so the reduction of batch k overlaps the
+kernel of batch k + 1 and no step zeroes anything. The CPU rehearsal (tests/test_multiproc.py, gloo, world size 2)
+drives the same sharding and bootstrap code with torch's all_reduce standing in for the RCCL call; on the GPU the
+RCCL call runs through a 1-rank communicator test, and bench.py --gpus 2 runs as two child ranks on one GPU
+(tests/test_gpu_multiproc.py, gloo counts: RCCL refuses two ranks on one device).
 """
 from __future__ import annotations
 
@@ -53,24 +55,33 @@ def allreduce_counts(counts, group=None) -> None:
 
 
 class TorchCountsAllreduce:
-    """Fallback when the receive path's own RCCL communicator (dk_comm.h) cannot be created on a node: the same
-    all-reduce of the counter arrays through torch.distributed's RCCL (backend "nccl") process group."""
+    """TEST-ONLY stand-in for the product collective (dk_rx_flow_counts_allreduce_to over a dk_comm.h RCCL
+    communicator) when RCCL cannot run: the CPU gloo rehearsal, and 2-rank GPU tests on ONE GPU (RCCL refuses two
+    ranks on one device, rccl.h). The same out-of-place sum of the counter arrays through torch.distributed. bench.py
+    uses it only under --counts-via-torch-gloo-test and says so in its JSON line; a failed RCCL init otherwise ends the
+    run with an error."""
 
     def __init__(self, group):
         self.group = group
 
-    def __call__(self, results, stream) -> None:
+    def to(self, results, flow_out, verdict_out, stream) -> None:
         import torch
         import torch.distributed as dist
 
         with torch.cuda.stream(stream):
-            dist.all_reduce(results.t["flow_counts"], op=dist.ReduceOp.SUM, group=self.group)
-            dist.all_reduce(results.t["verdict_counts"], op=dist.ReduceOp.SUM, group=self.group)
+            flow_out.copy_(results.t["flow_counts"])
+            verdict_out.copy_(results.t["verdict_counts"])
+            dist.all_reduce(flow_out, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(verdict_out, op=dist.ReduceOp.SUM, group=self.group)
 
 
 class ShardedReceiver:
-    """One rank of a packet-sharded receive: its engine, its RCCL communicator, and double-buffered counters whose
-    all-reduce runs on a side stream (the collective of batch k overlaps the kernel of batch k + 1)."""
+    """One rank of a packet-sharded receive: its engine, its RCCL communicator, and `nbuf` sets of accumulating
+    counters. The kernel adds every step's counts to the set of slot k % nbuf (never zeroed: no memset kernels on the
+    launch stream); after the kernel, dk_rx_flow_counts_allreduce_to sums that set over the ranks into the slot's
+    node-wide totals on a side stream, overlapping the next step's kernel, which adds to the other set. A set is reused
+    only after its previous all-reduce has read it (one event wait). The node-wide counts of every step so far are the
+    sum of the slots' totals (`counts()`). With comm=None (one GPU) there is one set and no collective."""
 
     def __init__(self, engine, results, comm, stream, nbuf: int = 2):
         import torch
@@ -78,7 +89,10 @@ class ShardedReceiver:
         from .rx import RxResults
 
         self.eng, self.comm, self.stream = engine, comm, stream
-        self.side = torch.cuda.Stream(device=stream.device)
+        if comm is None:
+            nbuf = 1
+        self.side = torch.cuda.Stream(device=stream.device) if comm is not None else None
+        results.zero_counts()
         self.res = [results]
         for _ in range(nbuf - 1):  # same per-frame arrays, own counters
             r = RxResults.__new__(RxResults)
@@ -86,38 +100,47 @@ class ShardedReceiver:
             r.t["flow_counts"] = torch.zeros_like(results.t["flow_counts"])
             r.t["verdict_counts"] = torch.zeros_like(results.t["verdict_counts"])
             self.res.append(r)
+        self.tot = [(torch.zeros_like(r.t["flow_counts"]), torch.zeros_like(r.t["verdict_counts"])) for r in self.res] \
+            if comm is not None else None
         self.done = [None] * nbuf
         self.k = 0
+
+    def reduce(self, slot: int, stream) -> None:
+        """The slot's node-wide totals from every rank's accumulated set (on `stream`)."""
+        r, (fo, vo) = self.res[slot], self.tot[slot]
+        if isinstance(self.comm, TorchCountsAllreduce):
+            self.comm.to(r, fo, vo, stream)
+        else:
+            self.eng.counts_allreduce_to(r, fo, vo, self.comm.handle, stream=stream)
 
     def step(self, batch) -> None:
         import torch
 
         slot = self.k % len(self.res)
         r = self.res[slot]
-        if self.comm is not None:  # per-step counters, all-reduced (N = 1: they accumulate over steps, no reset)
-            if self.done[slot] is not None:  # this slot's previous all-reduce has finished before the reset
-                self.stream.wait_event(self.done[slot])
-            r.t["flow_counts"].zero_()
-            r.t["verdict_counts"].zero_()
+        if self.done[slot] is not None:  # the set's previous all-reduce has read it before the kernel adds to it
+            self.stream.wait_event(self.done[slot])
         self.eng.receive_batch(batch, r, stream=self.stream)
         if self.comm is not None:
             ev = torch.cuda.Event()
             ev.record(self.stream)
             self.side.wait_event(ev)
-            if isinstance(self.comm, TorchCountsAllreduce):
-                self.comm(r, self.side)
-            else:
-                self.eng.counts_allreduce(r, self.comm.handle, stream=self.side)
+            self.reduce(slot, self.side)
             done = torch.cuda.Event()
             done.record(self.side)
             self.done[slot] = done
         self.k += 1
 
     def drain(self) -> None:
-        self.side.synchronize()
+        if self.side is not None:
+            self.side.synchronize()
         self.stream.synchronize()
 
-    def counts(self, slot: Optional[int] = None):
-        """The counters of the last step (or of `slot`)."""
-        s = (self.k - 1) % len(self.res) if slot is None else slot
-        return self.res[s].t["flow_counts"], self.res[s].t["verdict_counts"]
+    def counts(self):
+        """Node-wide (comm) or this GPU's (no comm) flow and verdict counts of every step so far. Call after drain()."""
+        if self.comm is None:
+            return self.res[0].t["flow_counts"], self.res[0].t["verdict_counts"]
+        used = [s for s in range(len(self.res)) if self.done[s] is not None]
+        fo = sum(self.tot[s][0] for s in used) if used else self.tot[0][0]
+        vo = sum(self.tot[s][1] for s in used) if used else self.tot[0][1]
+        return fo, vo

@@ -30,7 +30,9 @@
  *   - Not re-entrant per context; one host thread per context (demikernel/bindings.rs:33-35). GPU work is
  *     ordered on the caller's stream. A context keeps its launch scratch per stream (up to 8 streams; past that the
  *     least recently used stream's scratch is taken over behind that stream's last launch), so batches issued on
- *     different streams of one context may run concurrently; counters they share are added atomically.
+ *     different streams of one context may run concurrently; counters they share are added atomically. A stream
+ *     handed to dk_rx_process must stay valid while the context lives, or be released with dk_rx_stream_forget
+ *     before it is destroyed (a later stream may reuse its handle value).
  *   - Tuning: the engine's choices (kernel family, grid) follow the batch; overrides are diagnostics (dk_diag.h),
  *     read from the environment once, when the context is created.
  *   - No torch / HIP types in signatures: streams are passed as void* (a hipStream_t, NULL = default stream).
@@ -226,6 +228,10 @@ uint32_t dk_rx_flow_table_size(const dk_rx_ctx* ctx);
 /* Process one HBM-resident batch on `stream` (hipStream_t or NULL). Asynchronous: returns after the launch.
  * Returns 0, EINVAL (null required pointer, frames_bytes > DK_RX_MAX_BLOB) or EIO (launch failure). */
 int dk_rx_process(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results* res, void* stream);
+
+/* Release the context's launch scratch of `stream` before the caller destroys that stream: waits for the stream's
+ * work, then frees the slot for another stream. Returns 0 (also when the context never saw the stream) or EIO. */
+int dk_rx_stream_forget(dk_rx_ctx* ctx, void* stream);
 
 /* Process a batch that lives in host memory (a NIC ring / raw-socket buffer / DPDK mempool): the kernel, with
  * descriptors copied in and results copied back to host arrays, over the context's own streams. Synchronous.

@@ -596,6 +596,39 @@ int dko_process_mt(const dko_peer* p, const uint8_t* frames, uint64_t frames_byt
 #endif
 }
 
+// Whole-batch parity checker for full-size GPU tests: every output dko_process writes (all nine result arrays, the
+// option records and both counter arrays), over `threads` OpenMP threads on contiguous frame ranges. Counters are
+// accumulated per thread and added after the loop (the same counting rule as dko_range). Returns the threads used.
+int dko_process_par(const dko_peer* p, const uint8_t* frames, uint64_t frames_bytes, const uint32_t* off,
+                    const uint16_t* len, uint32_t n, uint32_t* meta, uint32_t* src, uint32_t* dst, uint32_t* ports,
+                    uint32_t* payload, uint32_t* flow, uint32_t* seq, uint32_t* ack, uint32_t* win,
+                    uint64_t* flow_counts, uint64_t* verdict_counts, dk_tcp_opts* opts, int threads) {
+    const uint32_t nf = p->nflows ? p->nflows : 1;
+    int used = 1;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+    {
+        const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+#pragma omp single
+        used = nt;
+        std::vector<uint64_t> fc(nf, 0), vc(DK_V_COUNT, 0);
+        const uint32_t b = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
+        dko_range(p, frames, frames_bytes, off, len, b, e, meta, src, dst, ports, payload, flow, seq, ack, win,
+                  fc.data(), vc.data(), opts);
+#pragma omp critical
+        {
+            for (uint32_t i = 0; i < nf; i++) flow_counts[i] += fc[i];
+            for (uint32_t i = 0; i < DK_V_COUNT; i++) verdict_counts[i] += vc[i];
+        }
+    }
+#else
+    (void)threads;
+    dko_range(p, frames, frames_bytes, off, len, 0, n, meta, src, dst, ports, payload, flow, seq, ack, win,
+              flow_counts, verdict_counts, opts);
+#endif
+    return used;
+}
+
 // ---- per-layer entry points, so the reference's unit tests can be restated layer by layer -----------------------
 // Ipv4Header::parse_and_strip on a bare datagram: returns -1 on success (payload window in *poff/*plen) or a verdict.
 int dko_ipv4_parse(const uint8_t* dgram, size_t len, uint32_t* src, uint32_t* dst, uint8_t* proto, uint32_t* poff,

@@ -44,6 +44,8 @@ def lib() -> ctypes.CDLL:
         L.dko_process.argtypes = [vp, vp, c_uint64, vp, vp, c_uint32] + [vp] * 12
         L.dko_process_mt.restype = c_int
         L.dko_process_mt.argtypes = [vp, vp, c_uint64, vp, vp, c_uint32] + [vp] * 6 + [c_int]
+        L.dko_process_par.restype = c_int
+        L.dko_process_par.argtypes = [vp, vp, c_uint64, vp, vp, c_uint32] + [vp] * 12 + [c_int]
         L.dko_ipv4_parse.restype = c_int
         L.dko_ipv4_parse.argtypes = [vp, c_size_t, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint8),
                                      POINTER(c_uint32), POINTER(c_uint32)]
@@ -110,6 +112,31 @@ class OraclePeer:
                             *[out[k].ctypes.data for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id",
                                                            "tcp_seq", "tcp_ack", "tcp_win", "flow_counts",
                                                            "verdict_counts", "tcp_opts")])
+        return out
+
+    def process_par(self, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, threads: int = 0,
+                    frames_bytes: int | None = None) -> dict:
+        """`process` over OpenMP threads (dko_process_par): the same outputs, counters included, for whole-batch parity
+        at full size. threads <= 0: the CPUs this process may use."""
+        import os
+
+        if threads <= 0:
+            threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+        n = len(off)
+        blob = np.ascontiguousarray(blob, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        lens = np.ascontiguousarray(lens, np.uint16)
+        out = {k: np.zeros(n, np.uint32) for k in
+               ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win")}
+        out["flow_counts"] = np.zeros(max(self.nflows, 1), np.uint64)
+        out["verdict_counts"] = np.zeros(DK_V_COUNT, np.uint64)
+        out["tcp_opts"] = np.zeros(max(n, 1), TCP_OPTS_DTYPE)[:n]
+        fb = blob.nbytes if frames_bytes is None else frames_bytes
+        self._L.dko_process_par(self._p, blob.ctypes.data if blob.size else None, fb, off.ctypes.data,
+                                lens.ctypes.data, n,
+                                *[out[k].ctypes.data for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id",
+                                                               "tcp_seq", "tcp_ack", "tcp_win", "flow_counts",
+                                                               "verdict_counts", "tcp_opts")], threads)
         return out
 
     def process_mt(self, blob, off, lens, threads: int) -> tuple[dict, int]:

@@ -445,36 +445,48 @@ def test_tpacket3_ring_path_matches_oracle(torch_cuda):
         eng.close()
 
 
-def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, sample=20000):
-    """A device-generated batch at a BASELINE config's full size with a `corrupt` tail (synth.corruption_plan): every
-    intact frame is delivered to its own flow, every corrupted frame gets the oracle's verdict and fields, a random
-    sample is bit-exact against the oracle on every field, and both counter arrays are exactly the histograms of the
-    results. Returns (engine, batch, traffic, results as numpy, host copy of the blob)."""
+def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, host_checksums=False):
+    """A batch at a BASELINE config's full size with a `corrupt` tail (synth.corruption_plan), compared with the oracle
+    on EVERY frame: all nine result arrays and both counter arrays of the whole batch, bit for bit (the oracle runs
+    over the host's CPUs, OraclePeer.process_par). Plus the properties the workload is built for: every intact frame
+    delivered to its own flow, the corruptions rejected.
+
+    Checksums: host_checksums=True builds the batch on the host with synth.fill_checksums_numpy (an independent RFC 1071
+    implementation), so the product TX kernel never vouches for the RX kernel; otherwise the batch is generated on the
+    device and checksummed by dk_tx_checksum, and the whole-batch oracle comparison catches any common-mode error of
+    the two kernels (the oracle sums every segment itself). TCP/UDP checksum VALUES are pinned by no reference vector
+    (SURVEY.md §4): they rest on the oracle's restatement plus the independent implementation.
+    Returns (engine, batch, traffic, results as numpy, host copy of the blob)."""
     import torch
 
     tr = synth.traffic(n, ip_len, flows, seed=seed)
     eng = RxEngine(Config(LOCAL))
     eng.set_sockets(flows)
-    batch = synth.build_device(tr, eng, seed=seed)
-    off = np.asarray(batch.off.cpu().numpy().view(np.uint32))
-    lens = np.asarray(batch.len.cpu().numpy().view(np.uint16))
     plan = synth.corruption_plan(n, corrupt, tr, seed)
-    synth.corrupt_device(batch, off, plan)
+    if host_checksums:
+        blob, off, lens = synth.build_numpy(tr, seed=seed)
+        synth.corrupt_numpy(blob, off, plan)
+        batch = FrameBatch.from_numpy(blob, off, lens)
+    else:
+        batch = synth.build_device(tr, eng, seed=seed)
+        off = np.asarray(batch.off.cpu().numpy().view(np.uint32))
+        lens = np.asarray(batch.len.cpu().numpy().view(np.uint16))
+        synth.corrupt_device(batch, off, plan)
+        blob = batch.blob.cpu().numpy()
     r = eng.results(n, tcp_fields=True)
     eng.receive_batch(batch, r)
     torch.cuda.synchronize()
     got = r.to_numpy()
-    blob = batch.blob.cpu().numpy()
+    ref = OraclePeer(ipv4(LOCAL))
+    ref.set_flows(flows)
+    exp = ref.process_par(blob, off, lens)
+    assert_same(got, exp, f"full size n={n}")
     bad = np.array(sorted({i for i, _, _ in plan}), np.int64)
     good = np.ones(n, bool)
     good[bad] = False
     v = got["meta"] & 0xFF
     assert np.array_equal(v[good], np.where(tr.proto[good] == 6, V["OK_TCP"], V["OK_UDP"]).astype(np.uint32))
     assert np.array_equal(got["flow_id"][good], tr.flow[good].astype(np.uint32))
-    for idx, what in ((bad, "corrupted"), (np.random.default_rng(seed).choice(n, sample, replace=False), "sample")):
-        exp = run_oracle(blob, off[idx], lens[idx], flows)
-        for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win"):
-            assert np.array_equal(got[k][idx], exp[k]), (what, k)
     assert (v[bad] > 1).mean() > 0.8  # the corruptions really are rejected
     assert np.array_equal(got["verdict_counts"], np.bincount(v, minlength=len(VERDICTS)).astype(np.uint64))
     deliv = v <= 1
@@ -483,18 +495,35 @@ def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, sample=20000):
     return eng, batch, tr, got, blob
 
 
-def test_full_size_c2_properties(torch_cuda):
-    """BASELINE config 2 at full size (1M x 1500 B TCP, 1,024 flows) with the 1 % corrupted tail the bench times."""
+def test_full_size_c1_tcp_echo_shape(torch_cuda):
+    """BASELINE config 1's frame shape through the HIP path (the reference runs it on the CPU only: tcp-echo over
+    catpowder, 1 KiB payloads, tools/ci/job/linux.py:145): 131,072 x 1078 B TCP frames on ONE Active 4-tuple to port
+    12345, 1 % corrupted tail, checksums from the independent numpy RFC 1071 implementation; whole batch bit-exact."""
+    flows = synth.make_flows(1)
+    _, _, tr, got, _ = full_size(1 << 17, 1064, flows, seed=synth.SEED + 11, host_checksums=True)
+    assert int(got["flow_counts"][0]) == int(((got["meta"] & 0xFF) == V["OK_TCP"]).sum()) > 0.98 * (1 << 17)
+    assert np.all(tr.dport == synth.LOCAL_PORT)
+
+
+def test_full_size_c2(torch_cuda):
+    """BASELINE config 2 at full size (1M x 1500 B TCP, 1,024 flows) with the 1 % corrupted tail the bench times;
+    built on the host with independently computed checksums; whole batch bit-exact vs the oracle."""
+    full_size(1 << 20, 1486, synth.make_flows(1024), host_checksums=True)
+
+
+def test_full_size_c2_device_built(torch_cuda):
+    """The bench's own C2 batch (device-generated, checksummed by dk_tx_checksum): whole batch bit-exact."""
     full_size(1 << 20, 1486, synth.make_flows(1024))
 
 
-def test_full_size_c3_properties(torch_cuda):
-    """BASELINE config 3 at full size (1M x 64 B UDP, the small-frame kernel) with a 1 % corrupted tail."""
+def test_full_size_c3(torch_cuda):
+    """BASELINE config 3 at full size (1M x 64 B UDP, the small-frame kernel) with a 1 % corrupted tail; whole batch."""
     full_size(1 << 20, 50, synth.make_flows(1024, kind="udp"), seed=synth.SEED + 1)
 
 
 def test_full_size_c4_imix_shard(torch_cuda):
-    """BASELINE config 4's per-GPU shard (2M IMIX frames, 40/576/1500 B at 7:4:1) with a 1 % corrupted tail."""
+    """BASELINE config 4's per-GPU shard (2M IMIX frames, 40/576/1500 B at 7:4:1) with a 1 % corrupted tail; whole
+    batch bit-exact."""
     n = 1 << 21
     full_size(n, synth.imix_ip_lengths(n, seed=5), synth.make_flows(1024), seed=5)
 
@@ -503,7 +532,7 @@ def test_c5_host_pipeline_10k_flows(torch_cuda):
     """BASELINE config 5's per-GPU shard end to end: 2M x 1500 B TCP over 10,000 Active flows plus a Passive listener,
     1 % corrupted, from pinned host memory through dk_rx_process_host (chunked H2D, kernel, D2H on 3 streams): every
     result word and both counter arrays equal the HBM-resident call's (itself checked by full_size against the
-    oracle: intact frames, every corrupted frame and a 20k sample), frames of the Passive listener included."""
+    oracle on every frame of the 2M-frame shard), frames of the Passive listener included."""
     import torch
 
     from demikernel_amd import RxResults
@@ -566,6 +595,56 @@ def test_two_streams_one_context(torch_cuda):
     got = res[0].to_numpy()
     assert np.array_equal(got["verdict_counts"], total * sum(e["verdict_counts"] for e in exps))
     assert np.array_equal(got["flow_counts"], total * sum(e["flow_counts"][: len(flows)] for e in exps))
+
+
+def test_streams_destroyed_and_forgotten(torch_cuda):
+    """Streams created and destroyed one after another (more than the context's 8 scratch slots over its life), each
+    released with dk_rx_stream_forget before hipStreamDestroy, then a second round whose slots are taken over (9+
+    live streams): every batch's results equal the oracle's and the shared counters add up exactly."""
+    import ctypes
+
+    import torch
+
+    from demikernel_amd import _native
+
+    hip = _native.load_library()  # hipStreamCreate/Destroy of the HIP runtime the library (and torch) use
+    flows = np.concatenate([synth.make_flows(500), synth.make_flows(30, kind="udp")])
+    n = 20000
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=31), flows, seed=31)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr, seed=31))
+    exp = run_oracle(blob, off, lens, flows)
+    eng = RxEngine(Config(LOCAL))
+    eng.set_sockets(flows)
+    b = FrameBatch.from_numpy(blob, off, lens)
+    r = eng.results(n, tcp_fields=True)
+    torch.cuda.synchronize()
+    launches = 0
+    for _ in range(12):  # create -> launch -> forget -> destroy
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        eng.receive_batch(b, r, stream=torch.cuda.ExternalStream(s.value))
+        launches += 1
+        eng.forget_stream(s.value)
+        assert hip.hipStreamDestroy(s) == 0
+    live = []
+    for k in range(11):  # 11 live streams: slots taken over, events recorded from then on
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        live.append(s)
+        eng.receive_batch(b, r, stream=torch.cuda.ExternalStream(s.value))
+        eng.receive_batch(b, r, stream=torch.cuda.ExternalStream(live[k // 2].value))
+        launches += 2
+    for s in live:
+        eng.forget_stream(s.value)
+        assert hip.hipStreamDestroy(s) == 0
+    torch.cuda.synchronize()
+    got = r.to_numpy()
+    for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win"):
+        assert np.array_equal(got[k], exp[k]), k
+    assert np.array_equal(got["verdict_counts"], launches * exp["verdict_counts"])
+    assert np.array_equal(got["flow_counts"], launches * exp["flow_counts"][: len(flows)])
+    eng.close()
 
 
 @pytest.mark.parametrize("data_off", [128, 130])
