@@ -95,13 +95,11 @@ struct RxParams {
     uint32_t* tickets;       // [ceil(grid / kCountGroup)] arrival tickets, 0 between launches (the last arriver resets)
     uint32_t fused;          // 1: rows combined in-launch (flush_counters); 0: plain rows + dk_flow_reduce_kernel
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
-    uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave
+    uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave (tuning)
     uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path
     uint32_t stage;          // launch the instantiation that stages result stores in registers (large frames)
-    uint32_t split;          // launch the split (stream waves / finish waves) kernel: 0 no, else finishers per stream
-                             // wave (1: large frames, 2: mixed sizes)
-    uint32_t small;          // launch the small-frame kernel (minimum-size frames): 1, 2 = its stream/finish form,
-                             // 3 = its two-chunk form
+    uint32_t split;          // launch the split (stream waves / finish waves) kernel (large frames)
+    uint32_t small;          // launch the small-frame kernel (minimum-size frames)
     dk_rx_results res;
 };
 
@@ -121,8 +119,7 @@ struct TxParams {
 // Launchers implemented in rx_kernels.hip (internal symbols, not part of the C ABI).
 // Receive kernel families (launch_batch picks one per launch).
 namespace dk {
-constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFamilySmall = 3, kFamilySplit2 = 4,
-                   kFamilySmallSplit = 5, kFamilySmallPair = 6;
+constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFamilySmall = 3;
 }
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "rx_common.h"
+#include "rx_plan.h"
 
 static_assert(sizeof(dk_tcp_opt) == 12 && sizeof(dk_tcp_opts) == 96, "dk_rx.h tcp option record layout");
 
@@ -215,10 +216,6 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride) {
 
 // Choose the flow-count mode and the persistent grid, then launch on `stream` with that stream's counter scratch.
 // size_hint = bytes of blob the batch covers (the family and grid follow the mean bytes per frame).
-#ifndef DK_SPLIT2_MIN_BYTES
-#define DK_SPLIT2_MIN_BYTES (1u << 30)  // mixed-size batches: the split kernel with 2 finishers per stream wave
-#endif
-constexpr uint64_t kSplit2MinBytes = DK_SPLIT2_MIN_BYTES;
 
 int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t stream) {
     if (p.n == 0) return 0;
@@ -251,17 +248,14 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     // Never more workgroups per CU than the occupancy admits (large socket tables take LDS).
     const uint64_t bytes_per_frame = size_hint / p.n;
     p.stage = bytes_per_frame >= 128 ? 1u : 0u;
-    p.split = bytes_per_frame >= 1024 ? 1u : bytes_per_frame >= kSplit2MinBytes ? 2u : 0u;
+    p.split = bytes_per_frame >= 1024 ? 1u : 0u;
     p.small = bytes_per_frame <= 96 ? 1u : 0u;
     if (T.stage >= 0) p.stage = T.stage ? 1u : 0u;
-    if (T.split >= 0) p.split = T.split == 2 ? 2u : T.split ? 1u : 0u;
-    if (T.small >= 0) p.small = T.small == 2 || T.small == 3 ? (uint32_t)T.small : T.small ? 1u : 0u;
+    if (T.split >= 0) p.split = T.split ? 1u : 0u;
+    if (T.small >= 0) p.small = T.small ? 1u : 0u;
     if (p.small) p.split = p.stage = 0;
-    p.sched = T.sched >= 0 ? (uint32_t)std::min(T.sched, 3) : 0u;
-    const uint32_t family = p.small == 3 ? dk::kFamilySmallPair
-                            : p.small == 2 ? dk::kFamilySmallSplit
-                            : p.small ? dk::kFamilySmall
-                            : p.split == 2 ? dk::kFamilySplit2
+    p.sched = T.sched >= 0 ? (uint32_t)std::min(T.sched, 1) : 0u;
+    const uint32_t family = p.small ? dk::kFamilySmall
                             : p.split ? dk::kFamilySplit
                             : p.stage ? dk::kFamilyStaged
                                       : dk::kFamilyUnstaged;
@@ -273,7 +267,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u);
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
-    const uint32_t tiles_per_wg = p.small == 2 ? 2u : p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
+    const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
     uint32_t grid = std::min((ntiles + tiles_per_wg - 1) / tiles_per_wg, per_cu * c->cu_count);
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
@@ -550,27 +544,9 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
     const uint8_t* zc = c->tune.host_zc != 0 ? mapped_alias(b->frames, b->frames_bytes) : nullptr;
     const uint32_t chunk_n = zc && !chunk_frames ? b->n : chunk;
     // Chunk boundaries: consecutive frame ranges whose covering byte range stays under kMaxChunkBytes (staged).
-    struct Chunk { uint32_t a, e; uint64_t lo, hi; };
-    std::vector<Chunk> chunks;
-    uint64_t max_bytes = 0;
-    for (uint32_t a = 0; a < b->n;) {
-        uint64_t lo = UINT64_MAX, hi = 0;
-        uint32_t e = a;
-        while (e < b->n && e - a < chunk_n) {
-            const uint64_t o = b->off[e], end = o + b->len[e];
-            if (end <= b->frames_bytes) {  // out-of-blob frames copy nothing; the kernel flags them BAD_DESC
-                const uint64_t nlo = std::min<uint64_t>(lo, o & ~(uint64_t)15), nhi = std::max(hi, end);
-                if (!zc && e > a && nhi - nlo > kMaxChunkBytes) break;
-                lo = nlo;
-                hi = nhi;
-            }
-            e++;
-        }
-        if (lo == UINT64_MAX) lo = hi = 0;
-        chunks.push_back({a, e, lo, hi});
-        max_bytes = std::max(max_bytes, hi - lo);
-        a = e;
-    }
+    std::vector<dk::HostChunk> chunks;
+    const uint64_t max_bytes = dk::plan_host_chunks(b->off, b->len, b->n, b->frames_bytes, chunk_n, zc != nullptr,
+                                                    kMaxChunkBytes, chunks);
     uint32_t cap = 0;
     for (auto& ch : chunks) cap = std::max(cap, ch.e - ch.a);
     const size_t nstages = std::min<size_t>(chunks.size(), kPipeStreams);  // stages this call uses
@@ -602,7 +578,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
 
     int rc = 0;
     for (size_t k = 0; k < chunks.size() && rc == 0; k++) {
-        const Chunk& ch = chunks[k];
+        const dk::HostChunk& ch = chunks[k];
         Stage& st = c->stages[k % kPipeStreams];
         const uint32_t m = ch.e - ch.a;
         // The staged copy starts at a 16-aligned host offset; a virtual base keeps the descriptors unchanged.
@@ -747,7 +723,7 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
     const TxTuning& T = tx_tuning();
     if (T.split >= 0) p.split = T.split ? 1u : 0u;
     uint32_t per_cu = p.split ? 1u : std::min<uint32_t>(occ, p.sched ? 3u : 4u);
-    if (T.sched >= 0) p.sched = (uint32_t)std::min<int32_t>(T.sched, 3);
+    if (T.sched >= 0) p.sched = (uint32_t)std::min<int32_t>(T.sched, 1);
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
     return dk_launch_tx(p, grid, stream);

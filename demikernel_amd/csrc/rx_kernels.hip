@@ -967,31 +967,16 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
 }
 
 // Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). Chunk k of a wave holds the
-// frames i = c_k + lane_off (lane_off = lane unless noted) with i < lim_k:
+// frames i = c_k + lane with i < lim_k:
 //   sched 0: round-robin 256-frame tiles, wave wv of workgroup b takes frames [t * 256 + 64 wv, +64) of tiles
 //            t = b, b + G, ... (the grid sweeps one contiguous window of the blob);
-//   sched 3: sched 0 for the full rounds, then the frames of the last, partial round split evenly over all waves (one
-//            short chunk each) instead of whole 64-frame chunks for some waves and none for the rest;
-//   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame), walked in 64-frame chunks;
-//   sched 2: phase-B-step interleave: lane group g = lane / 8 of wave gw (of nw) takes the 8 consecutive frames
-//            c + 8 (g * nw + gw) + [0, 8), c = 0, 64 nw, ...: at any moment the whole grid reads one window of
-//            ~nw * 8 frames.
+//   sched 1: each wave owns one contiguous, equal share of the batch (+-1 frame), walked in 64-frame chunks.
+// (Two more schedules — a phase-B-step interleave and an evenly split last round — measured +1 .. +5 % and were
+// removed in round 3.)
 struct WaveRange {
     uint32_t f0, f1, step, lane_off;
-    uint32_t nfull, t0, t1;  // sched 3: chunks k < nfull are full; chunk nfull is [t0, t1)
-    bool tail;
     // Chunk k: false when the wave has no chunk k.
     __device__ __forceinline__ bool chunk(uint32_t k, uint32_t& c, uint32_t& lim) const {
-        if (tail) {
-            if (k < nfull) {
-                c = f0 + k * step;
-                lim = c + 64;
-                return true;
-            }
-            c = t0;
-            lim = t1;
-            return k == nfull && t0 < t1;
-        }
         c = f0 + k * step;
         lim = f1;
         return c < f1;
@@ -1002,28 +987,14 @@ __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint
     WaveRange r;
     const uint32_t nw = gridDim.x * kW, gw = blockIdx.x * kW + wv;
     r.lane_off = lane;
-    r.tail = false;
-    r.nfull = r.t0 = r.t1 = 0;
     if (sched == 1) {
         r.f0 = (uint32_t)(((uint64_t)n * gw) / nw);
         r.f1 = (uint32_t)(((uint64_t)n * (gw + 1)) / nw);
         r.step = 64;
-    } else if (sched == 2) {
-        r.f0 = 8 * gw;
-        r.f1 = n;
-        r.step = 64 * nw;
-        r.lane_off = (lane >> 3) * 8 * nw + (lane & 7);
     } else {
         r.f0 = gw * 64;  // == blockIdx.x * kBlock + wv * 64
         r.f1 = n;
         r.step = 64 * nw;
-        if (sched == 3) {
-            r.tail = true;
-            r.nfull = n / (64 * nw);
-            const uint32_t base = r.nfull * 64 * nw, rem = n - base;
-            r.t0 = base + (uint32_t)(((uint64_t)rem * gw) / nw);
-            r.t1 = base + (uint32_t)(((uint64_t)rem * (gw + 1)) / nw);
-        }
     }
     return r;
 }
@@ -1470,241 +1441,6 @@ __device__ __forceinline__ void lds_publish(uint32_t* w, uint32_t v) {
     __hip_atomic_store((lu32*)w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Small-frame pair kernel (DK_RX_SMALL=3): each wave walks two chunks at once — chunk A's window by LDS-DMA, chunk
-// B's frames by per-lane loads, both in flight together; then parse A and B (both table probes in flight), then
-// verdicts, demux and results of A and of B. A wave's dependent chain (window -> parse -> probe -> results) is paid
-// once per two chunks, at 4 waves/SIMD (128 VGPRs) instead of 5.
-#ifndef DK_MIN_WAVES_PAIR
-#define DK_MIN_WAVES_PAIR 4
-#endif
-#ifndef DK_PAIR_WIN2
-#define DK_PAIR_WIN2 0  // 1: chunk B's window by LDS-DMA too (4 KiB windows; measured 31.9 vs 30.2 us)
-#endif
-struct WinView {  // a window and tail slots, as the small-frame helpers read W
-    uint4* win;
-    uint4* tail;
-};
-struct PairLds {
-    uint4 tail[64];
-    uint4 win[2][256];  // 4 KiB per chunk
-};
-template <bool kShift, bool kOpt>
-__global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_PAIR) void dk_rx_small_pair_kernel(RxParams P) {
-#if DK_PAIR_WIN2
-    __shared__ PairLds s_pair[kSmallWaves];
-#else
-    __shared__ SmallLds s_wave[kSmallWaves];
-#endif
-    __shared__ uint32_t s_vh[DK_V_COUNT];
-    __shared__ uint32_t s_last;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = lane_id();
-    const uint32_t wv = tid >> 6;
-    const bool lds_flows = P.flow_mode == kFlowLds;
-    for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
-    if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
-    __syncthreads();
-
-    const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
-    const Blob B(P.frames, P.frames_bytes);
-#if DK_PAIR_WIN2
-    WinView W{s_pair[wv].win[0], s_pair[wv].tail};
-    WinView WB{s_pair[wv].win[1], s_pair[wv].tail};
-#else
-    SmallLds& W = s_wave[wv];
-#endif
-    uint32_t cA, limA, cB = 0, limB = 0;
-    bool hasA = r.chunk(0, cA, limA);
-    bool hasB = hasA && r.chunk(1, cB, limB);
-    uint32_t offA = 0, lenA = 0, offB = 0, lenB = 0;
-    if (hasA && cA + r.lane_off < limA) {
-        offA = P.off[cA + r.lane_off];
-        lenA = P.len[cA + r.lane_off];
-    }
-    if (hasB && cB + r.lane_off < limB) {
-        offB = P.off[cB + r.lane_off];
-        lenB = P.len[cB + r.lane_off];
-    }
-    for (uint32_t k = 0; hasA; k += 2) {
-        const uint32_t iA = cA + r.lane_off, iB = cB + r.lane_off;
-        const bool liveA = iA < limA, liveB = hasB && iB < limB;
-        // next pair's descriptors, in flight with this pair's frames
-        uint32_t cA2 = 0, limA2 = 0, cB2 = 0, limB2 = 0, offA2 = 0, lenA2 = 0, offB2 = 0, lenB2 = 0;
-        const bool hasA2 = hasB && r.chunk(k + 2, cA2, limA2);
-        const bool hasB2 = hasA2 && r.chunk(k + 3, cB2, limB2);
-        if (hasA2 && cA2 + r.lane_off < limA2) {
-            offA2 = P.off[cA2 + r.lane_off];
-            lenA2 = P.len[cA2 + r.lane_off];
-        }
-        if (hasB2 && cB2 + r.lane_off < limB2) {
-            offB2 = P.off[cB2 + r.lane_off];
-            lenB2 = P.len[cB2 + r.lane_off];
-        }
-        const FrameDesc<kShift> FA(P.frames, P.frames_bytes, liveA, offA, lenA);
-        const FrameDesc<kShift> FB(P.frames, P.frames_bytes, liveB, offB, lenB);
-        Chunk CA, CB;
-#if DK_PAIR_WIN2
-        const WinPlan plA = small_window_issue<kShift, WinView, 256>(FA, B, offA, lenA, liveA, lane, W);
-        const WinPlan plB = small_window_issue<kShift, WinView, 256>(FB, B, offB, lenB, liveB, lane, WB);
-        // the windows are read through generic pointers: the compiler does not see the LDS-DMA dependency
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        small_window_read(plA, FA, B, offA, W, CA.R);
-        small_window_read(plB, FB, B, offB, WB, CB.R);
-#else
-        const WinPlan plA = small_window_issue(FA, B, offA, lenA, liveA, lane, W);
-        small_load(FB, B, offB, CB.R);
-        small_window_read(plA, FA, B, offA, W, CA.R);
-#endif
-        FinState SA, SB;
-        small_big_frames(FA, lane, offA, B, W, CA);  // W.tail: chunk A's, read by rx_front(A) before B's replace it
-        rx_front<kShift>(P, liveA, lane, W, offA, lenA, CA, SA);
-        small_big_frames(FB, lane, offB, B, W, CB);
-        rx_front<kShift>(P, liveB, lane, W, offB, lenB, CB, SB);
-        uint32_t v, fid;
-        Rec rec;
-        rec.meta = kNoRec;
-        rx_back<false, kOpt, true>(P, iA, liveA, lane, offA, SA, v, fid, rec);
-        count_chunk(P, liveA, lane, v, fid, lds_flows, s_flow, s_vh);
-        rx_back<false, kOpt, true>(P, iB, liveB, lane, offB, SB, v, fid, rec);
-        count_chunk(P, liveB, lane, v, fid, lds_flows, s_flow, s_vh);
-        hasA = hasA2;
-        hasB = hasB2;
-        cA = cA2;
-        limA = limA2;
-        cB = cB2;
-        limB = limB2;
-        offA = offA2;
-        lenA = lenA2;
-        offB = offB2;
-        lenB = lenB2;
-    }
-    __syncthreads();
-    flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh, &s_last);
-}
-
-// Small-frame split kernel (DK_RX_SMALL=2): the small-frame kernel's chunk chain without the frame read on it.
-// 512-thread workgroups, two per CU: DK_SS_STREAM stream waves load descriptors and DMA each chunk's frame window into
-// LDS for their finish waves (2 buffers per finisher, ready / free words as in the split kernel); the other waves
-// read their frames from LDS and run phase C. A finisher's chain per chunk is then LDS read -> parse -> table probe ->
-// stores, and its vmcnt never waits for a window in flight. Scattered chunks (frames beyond one 4.5 KiB window) and
-// frames past the 64-byte register window are loaded by the finisher itself.
-#ifndef DK_SS_STREAM
-#define DK_SS_STREAM 2  // stream waves per 8-wave workgroup (divides the 8 - DK_SS_STREAM finish waves)
-#endif
-constexpr uint32_t kSsStream = DK_SS_STREAM, kSsFin = 8 - DK_SS_STREAM, kSsWaves = 8, kSsBlock = 64 * kSsWaves;
-constexpr uint32_t kSsPer = kSsFin / kSsStream;  // finishers per stream wave
-static_assert(kSsPer * kSsStream == kSsFin, "stream waves must divide the finish waves");
-struct SsBuf {
-    uint4 win[kWinLoads * 64];  // the chunk's frame window
-    uint2 desc[64];             // {off, len} per lane (0, 0 for lanes past the chunk)
-    uint32_t lo, win_ok;        // window base (blob offset of its first granule); 1 if the window holds every frame
-};
-struct SsView {  // what the shared small-frame helpers read as W: the window and the finisher's tail slots
-    uint4* win;
-    uint4* tail;
-};
-template <bool kShift, bool kOpt>
-__global__ __launch_bounds__(kSsBlock, 2) void dk_rx_small_split_kernel(RxParams P) {
-    __shared__ SsBuf s_buf[kSsFin][2];
-    __shared__ uint4 s_tail[kSsFin][64];
-    __shared__ uint32_t s_ready[kSsFin][2], s_free[kSsFin][2];
-    __shared__ uint32_t s_vh[DK_V_COUNT];
-    __shared__ uint32_t s_last;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = lane_id();
-    const uint32_t wv = tid >> 6;
-    const bool lds_flows = P.flow_mode == kFlowLds;
-    for (uint32_t k = tid; k < DK_V_COUNT; k += kSsBlock) s_vh[k] = 0;
-    if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += kSsBlock) s_flow[k] = 0;
-    if (tid < kSsFin * 2) {
-        (&s_ready[0][0])[tid] = 0;
-        (&s_free[0][0])[tid] = 0;
-    }
-    __syncthreads();
-    const Blob B(P.frames, P.frames_bytes);
-    // finisher f of workgroup b walks chunks (gf + k nf) * 64, gf = b * kSsFin + f (sched 0 over the finish waves)
-    const uint32_t nf = gridDim.x * kSsFin;
-    if (wv < kSsStream) {
-        // stream wave s serves finishers s, s + kSsStream, ...
-        uint32_t off[kSsPer], len[kSsPer];
-        bool has[kSsPer];
-        auto load_desc = [&](uint32_t k) {
-#pragma unroll
-            for (uint32_t j = 0; j < kSsPer; j++) {
-                const uint32_t gf = blockIdx.x * kSsFin + wv + kSsStream * j;
-                const uint32_t c = (gf + k * nf) * 64u;
-                has[j] = c < P.n;
-                const uint32_t i = c + lane;
-                off[j] = has[j] && i < P.n ? P.off[i] : 0u;
-                len[j] = has[j] && i < P.n ? P.len[i] : 0u;
-            }
-        };
-        load_desc(0);
-        for (uint32_t k = 0; has[0]; k++) {  // finisher wv has the most chunks of this wave's finishers
-            const uint32_t b = k & 1;
-#pragma unroll
-            for (uint32_t j = 0; j < kSsPer; j++) {
-                if (!has[j]) continue;
-                const uint32_t f = wv + kSsStream * j;
-                SsBuf& SB = s_buf[f][b];
-                if (k >= 2) lds_wait_eq(&s_free[f][b], k - 1);  // chunk k - 2 read out of this buffer
-                const uint32_t c = (blockIdx.x * kSsFin + f + k * nf) * 64u;
-                const bool live = c + lane < P.n;
-                const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off[j], len[j]);
-                SsView V{SB.win, nullptr};
-                const WinPlan pl = small_window_issue(F, B, off[j], len[j], live, lane, V);
-                SB.desc[lane] = make_uint2(off[j], len[j]);
-                if (lane == 0) {
-                    SB.lo = pl.lo;
-                    SB.win_ok = pl.win ? 1u : 0u;
-                }
-            }
-            bool h[kSsPer];
-#pragma unroll
-            for (uint32_t j = 0; j < kSsPer; j++) h[j] = has[j];
-            load_desc(k + 1);                                  // next descriptors in flight with the windows
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // windows (LDS-DMA) and records written
-            if (lane == 0)
-#pragma unroll
-                for (uint32_t j = 0; j < kSsPer; j++)
-                    if (h[j]) lds_publish(&s_ready[wv + kSsStream * j][b], k + 1);
-        }
-    } else {
-        const uint32_t f = wv - kSsStream;
-        const uint32_t gf = blockIdx.x * kSsFin + f;
-        SsView V{nullptr, s_tail[f]};
-        for (uint32_t k = 0; (gf + k * nf) * 64u < P.n; k++) {
-            const uint32_t b = k & 1;
-            SsBuf& SB = s_buf[f][b];
-            const uint32_t c = (gf + k * nf) * 64u;
-            const uint32_t i = c + lane;
-            const bool live = i < P.n;
-            lds_wait_eq(&s_ready[f][b], k + 1);
-            const uint2 d = SB.desc[lane];
-            const uint32_t off = d.x, len = d.y;
-            const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
-            Chunk C;
-            V.win = SB.win;
-            const WinPlan pl{SB.win_ok != 0, SB.lo};
-            small_window_read(pl, F, B, off, V, C.R);
-            if (lane == 0) lds_publish(&s_free[f][b], k + 1);  // after this wave's reads of the buffer (release)
-            small_big_frames(F, lane, off, B, V, C);
-            uint32_t v, fid;
-            Rec rec;
-            rec.meta = kNoRec;
-            rx_finish<kShift, false, SsView, kOpt, true>(P, i, live, lane, V, off, len, C, v, fid, rec);
-            count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
-        }
-    }
-    __syncthreads();
-    flush_counters(P, tid, kSsBlock, lds_flows, s_flow, s_vh, &s_last);
-}
 
 // Split kernel: one workgroup per CU, two roles. Stream waves 0..3 run phases A+B of their chunks (sched 0 over the 4
 // stream waves of each workgroup) into LDS buffers (header windows, last granules, whole-frame sums; frames of <= 64
@@ -1714,20 +1450,17 @@ __global__ __launch_bounds__(kSsBlock, 2) void dk_rx_small_split_kernel(RxParams
 // is also the count at which the read probe peaks — and the finish waves stage their results in registers for one
 // burst per kStg chunks.
 //   kFin = 1 (512 threads, 2 waves/SIMD, 256 VGPRs, 16 staged chunks): large frames (C2, C5), where phase C is a small
-//     share of a chunk's time;
-//   kFin = 2 (768 threads, 3 waves/SIMD, 168 VGPRs, 4 staged chunks): mixed sizes (IMIX), where phase C of 64 frames
-//     costs as much as streaming them and one finisher per stream wave was the bottleneck.
+//     share of a chunk's time. (kFin = 2, 768 threads for mixed sizes, measured slower than the staged kernel on IMIX
+//     and was removed in round 3)
 #ifndef DK_SPLIT_NT_RES
 #define DK_SPLIT_NT_RES true  // split kernels: result bursts nontemporal (C2 -0.3 %, C5 -1.4 %, steadier)
 #endif
-#ifndef DK_SPLIT2_STAGE_K
-#define DK_SPLIT2_STAGE_K 4
-#endif
 template <int kFin>
 struct SplitShape {
+    static_assert(kFin == 1, "one finish wave per stream wave");
     static constexpr int kThreads = 64 * kWaves * (1 + kFin);
-    static constexpr int kBufs = kFin == 1 ? 3 : kFin + 1;  // LDS buffers per stream wave
-    static constexpr int kStg = kFin == 1 ? 16 : kFin == 2 ? DK_SPLIT2_STAGE_K : 2;  // chunks of results a finish wave stages
+    static constexpr int kBufs = 3;   // LDS buffers per stream wave
+    static constexpr int kStg = 16;   // chunks of results a finish wave stages
 };
 constexpr int kSplitBlock = SplitShape<1>::kThreads;  // the TX split kernel's shape
 template <int kStgK>
@@ -2126,18 +1859,9 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     int blocks = 0;
     hipError_t e;
-    if (family == dk::kFamilySplit2)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 2>,
-                                                          dk::SplitShape<2>::kThreads, dyn_lds_bytes);
-    else if (family == dk::kFamilySplit)
+    if (family == dk::kFamilySplit)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 1>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
-    else if (family == dk::kFamilySmallPair)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_pair_kernel<true, true>,
-                                                          dk::kSmallBlock, dyn_lds_bytes);
-    else if (family == dk::kFamilySmallSplit)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_split_kernel<true, true>,
-                                                          dk::kSsBlock, dyn_lds_bytes);
     else if (family == dk::kFamilySmall)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kSmallBlock,
                                                           dyn_lds_bytes);
@@ -2155,30 +1879,12 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
-    if (p.small == 3 && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_small_pair_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
-    else if (p.small == 3 && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_pair_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
-    else if (p.small == 3)
-        hipLaunchKernelGGL((dk::dk_rx_small_pair_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
-    else if (p.small == 2 && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<false, true>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
-    else if (p.small == 2 && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<true, true>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
-    else if (p.small == 2)
-        hipLaunchKernelGGL((dk::dk_rx_small_split_kernel<true, false>), dim3(grid), dim3(dk::kSsBlock), dyn, s, p);
-    else if (p.small && p.aligned16)
+    if (p.small && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
-    else if (p.split == 2 && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 2>), dim3(grid), dim3(dk::SplitShape<2>::kThreads), dyn, s,
-                           p);
-    else if (p.split == 2)
-        hipLaunchKernelGGL((dk::dk_rx_split_kernel<true, 2>), dim3(grid), dim3(dk::SplitShape<2>::kThreads), dyn, s,
-                           p);
     else if (p.split && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 1>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split)

@@ -1,0 +1,274 @@
+"""The product's host-side code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only): ring_host.cpp (the
+TPACKET_V3 block walker over caller memory), demi_host.cpp (results -> demi_sgarray_t) and dk_rx_process_host's chunk
+planner (rx_plan.h), built into a standalone driver (tests/host_asan). Valid, corrupted and fuzzed inputs; every
+sanitizer report aborts the driver (-fno-sanitize-recover), and its outputs must equal the regular libdk_rx.so's on
+the same inputs (the reference's host side is catpowder/linux/mod.rs:138-159 and runtime/memory/mod.rs:38-54)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from demikernel_amd import _native as N
+from demikernel_amd import ring as RG
+from demikernel_amd import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "build", "host_asan")
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=0",
+           UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+
+@pytest.fixture(scope="module")
+def driver():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "host_asan")], check=True)
+    return EXE
+
+
+def run(driver, mode, payload: bytes, tmp_path):
+    i, o = tmp_path / "in.bin", tmp_path / "out.bin"
+    i.write_bytes(payload)
+    p = subprocess.run([driver, mode, str(i), str(o)], env=ENV, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr[-4000:]
+    return o.read_bytes()
+
+
+def frames(n, seed=3):
+    flows = synth.make_flows(32)
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=seed), flows, seed=seed)
+    return synth.build_numpy(tr)
+
+
+def lib_scan(ring, bs, first, nb, cap):
+    lib = N.load_library()
+    off = np.zeros(max(cap, 1), np.uint32)
+    ln = np.zeros(max(cap, 1), np.uint16)
+    nf, nbo = ctypes.c_uint32(), ctypes.c_uint32()
+    rc = lib.dk_ring_scan_tpacket3(ring.ctypes.data, ring.nbytes, bs, first, nb, off.ctypes.data if cap else None,
+                                   ln.ctypes.data if cap else None, cap, ctypes.byref(nf), ctypes.byref(nbo))
+    return rc, nf.value, nbo.value, off[: nf.value], ln[: nf.value]
+
+
+def asan_scan(driver, tmp_path, ring, bs, first, nb, cap):
+    hdr = np.array([ring.nbytes], np.uint64).tobytes() + np.array([bs, first, nb, cap], np.uint32).tobytes()
+    out = run(driver, "ring", hdr + ring.tobytes(), tmp_path)
+    rc, nf, nbo = np.frombuffer(out[:12], np.int32)
+    off = np.frombuffer(out[12:12 + 4 * nf], np.uint32)
+    ln = np.frombuffer(out[12 + 4 * nf:12 + 6 * nf], np.uint16)
+    return int(rc), int(nf), int(nbo), off, ln
+
+
+def corrupt_ring(ring, bs, used, rng):
+    """One random header corruption: block descriptors (status, num_pkts, offset_to_first_pkt) or packet headers
+    (tp_next_offset, tp_snaplen, tp_mac) set to random or extreme values."""
+    r = ring.copy()
+    b = int(rng.integers(0, used))
+    base = b * bs
+    what = int(rng.integers(0, 6))
+    w32 = lambda at, v: r.__setitem__(slice(at, at + 4), np.frombuffer(np.uint32(v).tobytes(), np.uint8))  # noqa
+    extreme = [0, 1, 0xFFFF, 0x10000, bs - 1, bs, bs + 1, 0x7FFFFFFF, 0xFFFFFFFF, int(rng.integers(0, 2**32))]
+    v = extreme[int(rng.integers(0, len(extreme)))]
+    if what == 0:
+        w32(base + 12, v)  # num_pkts
+    elif what == 1:
+        w32(base + 16, v)  # offset_to_first_pkt
+    else:
+        # a packet header of this block, found by walking the valid chain
+        first = int(r[base + 16: base + 20].view(np.uint32)[0])
+        npk = int(r[base + 12: base + 16].view(np.uint32)[0])
+        p = first
+        for _ in range(int(rng.integers(0, max(npk, 1)))):
+            nxt = int(r[base + p: base + p + 4].view(np.uint32)[0])
+            if nxt == 0 or p + nxt + 48 > bs:
+                break
+            p += nxt
+        if what == 2:
+            w32(base + p, v)  # tp_next_offset
+        elif what == 3:
+            w32(base + p + 12, v)  # tp_snaplen
+        elif what == 4:
+            r[base + p + 24: base + p + 26] = np.frombuffer(np.uint16(v & 0xFFFF).tobytes(), np.uint8)  # tp_mac
+        else:
+            w32(base + 8, v & 1)  # block_status
+    return r
+
+
+def test_ring_walker_valid_and_corrupted(driver, tmp_path):
+    blob, off, lens = frames(3000)
+    rng = np.random.default_rng(5)
+    for bs in (1 << 12, 1 << 16):
+        ring, used, _, _ = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+        cases = [(ring, 0, used, len(off)), (ring, used - 1, 2, len(off)), (ring, 0, used, 7), (ring, 0, used, 0),
+                 (ring, used + 3, 1, 10)]
+        for _ in range(150):
+            cases.append((corrupt_ring(ring, bs, used, rng), int(rng.integers(0, used)), int(rng.integers(1, used + 2)),
+                          int(rng.choice([0, 5, 100, len(off)]))))
+        for r, first, nb, cap in cases:
+            got = asan_scan(driver, tmp_path, r, bs, first, nb, cap)
+            exp = lib_scan(r, bs, first, nb, cap)
+            assert got[:3] == exp[:3], (bs, first, nb, cap, got[:3], exp[:3])
+            assert np.array_equal(got[3], exp[3]) and np.array_equal(got[4], exp[4])
+            if got[0] == 0:  # every descriptor the walker hands out lies inside the ring
+                assert np.all(got[3].astype(np.int64) + got[4] <= r.nbytes)
+
+
+def test_ring_release(driver, tmp_path):
+    blob, off, lens = frames(800)
+    bs = 1 << 12
+    ring, used, _, _ = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+    for first, nb in ((0, used), (used - 1, 2), (3, 0), (used, 1), (0, used + 1)):
+        hdr = np.array([ring.nbytes], np.uint64).tobytes() + np.array([bs, first, nb], np.uint32).tobytes()
+        out = run(driver, "release", hdr + ring.tobytes(), tmp_path)
+        rc = int(np.frombuffer(out[:4], np.int32)[0])
+        exp = ring.copy()
+        erc = N.load_library().dk_ring_release_tpacket3(exp.ctypes.data, exp.nbytes, bs, first, nb)
+        assert rc == erc and out[4:] == exp.tobytes()
+
+
+def sga_rows(raw, k, base):
+    """Parse k packed 40-byte demi_sgarray_t from the product lib into the driver's output row format."""
+    out = []
+    for j in range(k):
+        s = raw[40 * j: 40 * j + 40]
+        tok = int.from_bytes(s[0:8], "little")
+        ns = int.from_bytes(s[8:12], "little")
+        sb = int.from_bytes(s[12:20], "little")
+        sl = int.from_bytes(s[20:24], "little")
+        out.append((tok, (sb - base) if sb else 2**64 - 1, sl, ns, bytes(s[24:40])))
+    return out
+
+
+def drv_rows(out, k, with_addr=True):
+    rows, p = [], 0
+    for _ in range(k):
+        tok, sb = np.frombuffer(out[p:p + 16], np.uint64)
+        sl, ns = np.frombuffer(out[p + 16:p + 24], np.uint32)
+        addr = out[p + 24:p + 40] if with_addr else b""
+        rows.append((int(tok), int(sb), int(sl), int(ns), bytes(addr)))
+        p += 40 if with_addr else 24
+    return rows, p
+
+
+def test_udp_sgarrays_fuzzed(driver, tmp_path):
+    rng = np.random.default_rng(9)
+    lib = N.load_library()
+    for trial in range(60):
+        n = int(rng.integers(0, 300))
+        blob = rng.integers(0, 256, 4096 + 70000, dtype=np.uint8)
+        off = rng.integers(0, 4096, n, dtype=np.uint32)
+        meta = rng.choice(np.array([0, 1, 1, 1, 25, 32], np.uint32), n).astype(np.uint32) | (17 << 8)
+        src = rng.integers(0, 2**32, n, dtype=np.uint32)
+        ports = rng.integers(0, 2**32, n, dtype=np.uint32)
+        payload = rng.integers(0, 2**32, n, dtype=np.uint32)
+        cap = int(rng.choice([0, 1, n // 2, n + 5]))
+        tokens = int(trial % 2)
+        payload_in = (np.array([n, cap, tokens], np.uint32).tobytes() + np.array([blob.nbytes], np.uint64).tobytes()
+                      + b"".join(a.tobytes() for a in (off, meta, src, ports, payload)) + blob.tobytes())
+        out = run(driver, "udp", payload_in, tmp_path)
+        rc, nout = np.frombuffer(out[:8], np.int32)
+        idx = np.frombuffer(out[8:8 + 4 * nout], np.uint32)
+        rows, _ = drv_rows(out[8 + 4 * nout:], int(nout))
+        # the regular build on the same inputs
+        arrs = (N.DemiSgarray * max(cap, 1))()
+        eidx = np.zeros(max(cap, 1), np.uint32)
+        enout = ctypes.c_uint32()
+        tok = (ctypes.c_void_p * max(n, 1))(*[0x1000 + i for i in range(n)])
+        p = lambda a: a.ctypes.data if n else None  # noqa: E731
+        erc = lib.dk_rx_into_sgarrays(blob.ctypes.data, p(off), n, p(meta), p(src), p(ports), p(payload),
+                                      tok if tokens else None, arrs if cap else None, eidx.ctypes.data if cap else None,
+                                      cap, ctypes.byref(enout))
+        assert (int(rc), int(nout)) == (erc, enout.value)
+        assert np.array_equal(idx, eidx[: enout.value])
+        exp = sga_rows(bytes(arrs), enout.value, blob.ctypes.data)
+        if not tokens:  # the token is the frame address: compare relative to the blob
+            exp = [((t - blob.ctypes.data) if t else t, *rest) for t, *rest in exp]
+            rows = [((t - 0) if t else t, *rest) for t, *rest in rows]
+            rows = [(r[1] - (payload[i] & 0xFFFF), *r[1:]) for r, i in zip(rows, idx)]
+        assert rows == exp
+
+
+def test_tcp_sgarrays_fuzzed(driver, tmp_path):
+    rng = np.random.default_rng(10)
+    lib = N.load_library()
+    for trial in range(60):
+        n = int(rng.integers(0, 200))
+        count = int(rng.integers(0, 300))
+        blob = rng.integers(0, 256, 8192, dtype=np.uint8)
+        off = rng.integers(0, 4096, n, dtype=np.uint32)
+        deliv = np.zeros(count, N.VIEW_DTYPE)
+        deliv["ref"] = rng.integers(0, max(n, 1), count)
+        deliv["ref"][rng.random(count) < 0.05] = N.DK_TCP_REF_EOF
+        if trial % 7 == 3 and count:
+            deliv["ref"][int(rng.integers(0, count))] = n  # out of range: EINVAL before anything is written
+        deliv["off"] = rng.integers(0, 2000, count)
+        deliv["len"] = rng.integers(0, 2000, count)
+        cap = int(rng.choice([0, 1, count // 2, count + 3]))
+        tokens = int(trial % 2)
+        payload_in = (np.array([n, count, cap, tokens], np.uint32).tobytes()
+                      + np.array([blob.nbytes], np.uint64).tobytes() + off.tobytes() + deliv.tobytes() + blob.tobytes())
+        out = run(driver, "tcp", payload_in, tmp_path)
+        rc, nout = np.frombuffer(out[:8], np.int32)
+        rows, _ = drv_rows(out[8:], int(nout))
+        arrs = (N.DemiSgarray * max(cap, 1))()
+        enout = ctypes.c_uint32()
+        tok = (ctypes.c_void_p * max(n, 1))(*[0x1000 + i for i in range(n)])
+        erc = lib.dk_tcp_into_sgarrays(blob.ctypes.data, off.ctypes.data if n else None, n,
+                                       deliv.ctypes.data if count else None, count, tok if tokens else None,
+                                       arrs if cap else None, cap, ctypes.byref(enout))
+        assert (int(rc), int(nout)) == (erc, enout.value)
+        exp = sga_rows(bytes(arrs), enout.value, blob.ctypes.data)
+        if not tokens:
+            exp = [((t - blob.ctypes.data) if t else 0, *rest) for t, *rest in exp]
+            rows = [((r[1] - int(deliv["off"][k])) if r[0] else 0, *r[1:]) for k, r in enumerate(rows)]
+        assert rows == exp
+
+
+def plan_ref(off, ln, fb, chunk_n, zc, max_bytes):
+    """dk_rx_process_host's chunk rule (rx_plan.h), restated."""
+    chunks, a, n = [], 0, len(off)
+    chunk_n = max(chunk_n, 1)
+    while a < n:
+        lo, hi, e = None, 0, a
+        while e < n and e - a < chunk_n:
+            o, end = int(off[e]), int(off[e]) + int(ln[e])
+            if end <= fb:
+                nlo, nhi = (o & ~15) if lo is None else min(lo, o & ~15), max(hi, end)
+                if not zc and e > a and nhi - nlo > max_bytes:
+                    break
+                lo, hi = nlo, nhi
+            e += 1
+        if lo is None:
+            lo = hi = 0
+        chunks.append((a, e, lo, hi))
+        a = e
+    return chunks
+
+
+def test_host_chunk_planner(driver, tmp_path):
+    rng = np.random.default_rng(11)
+    for trial in range(80):
+        n = int(rng.integers(0, 3000))
+        fb = int(rng.integers(1, 1 << 22))
+        off = rng.integers(0, fb + 5000, n, dtype=np.uint64).astype(np.uint32)
+        if trial % 3 == 0:
+            off[rng.random(n) < 0.1] = 0xFFFFFF00
+        ln = rng.integers(0, 9000, n, dtype=np.uint16)
+        chunk_n, zc = int(rng.choice([0, 1, 7, 1000, 65536])), int(trial % 4 == 0)
+        max_bytes = int(rng.choice([1, 4096, 1 << 20, 256 << 20]))
+        payload_in = (np.array([n], np.uint32).tobytes() + np.array([fb], np.uint64).tobytes()
+                      + np.array([chunk_n, zc], np.uint32).tobytes() + np.array([max_bytes], np.uint64).tobytes()
+                      + off.tobytes() + ln.tobytes())
+        out = run(driver, "plan", payload_in, tmp_path)
+        span = int(np.frombuffer(out[:8], np.uint64)[0])
+        k = int(np.frombuffer(out[8:12], np.uint32)[0])
+        got = []
+        for j in range(k):
+            a, e = np.frombuffer(out[12 + 24 * j: 20 + 24 * j], np.uint32)
+            lo, hi = np.frombuffer(out[20 + 24 * j: 36 + 24 * j], np.uint64)
+            got.append((int(a), int(e), int(lo), int(hi)))
+        exp = plan_ref(off, ln, fb, chunk_n, zc, max_bytes)
+        assert got == exp
+        assert span == max([h - lo for _, _, lo, h in exp], default=0)
+        assert sum(e - a for a, e, _, _ in got) == n  # every frame in exactly one chunk, in order
