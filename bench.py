@@ -653,6 +653,9 @@ def main():
         out["tcp_rx"] = tcp_rate(stream)
         # few connections with many segments each (the wave-per-connection walk)
         out["tcp_rx_64conns"] = tcp_rate(stream, 1 << 20, 64, cpu_seconds=1.0)
+        # one connection with 1M segments: its window fills early, the rest is out of window (classified in the
+        # key pass, never walked)
+        out["tcp_rx_1conn"] = tcp_rate(stream, 1 << 20, 1, cpu_seconds=1.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None and hasattr(comm, "destroy"):

@@ -56,12 +56,14 @@ constexpr uint32_t kFlowGlobal = 2;  // per-frame u64 global atomics (tables too
 constexpr uint32_t kMaxLdsFlowWords = 16384;  // 64 KiB of LDS -> up to 32768 flows on the LDS path
 constexpr uint32_t kVerdictWords = (DK_V_COUNT + 3) & ~3u;  // verdict histogram columns of a scratch row
 constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
-// Counter rows are combined inside the launch (flush_counters, rx_kernels.hip): workgroups are grouped kCountGroup at a
-// time, each group has one arrival ticket, and the group's last arriver sums the group's rows into the caller's u64
-// counters. Rows are padded to whole 128-byte lines.
-// In-launch combining pays per workgroup (its row store drain and ticket round trip at exit); a second launch pays a
-// kernel boundary. Measured: in-launch is faster up to ~768 workgroups (C2 -1.3 us, IMIX -1 us), the
-// second launch at 1536 (C3 +2.3 us in-launch). The host picks per launch: in-launch when grid <= kFusedMaxGrid.
+// Counter rows are combined inside the launch (flush_counters, rx_kernels.hip) by a two-level tree: workgroups are
+// grouped kCountGroup at a time, each group has one arrival ticket, and the group's last arriver sums the group's rows
+// into a group row; groups are grouped kSuperGroup at a time, and the last group winner of each supergroup adds the
+// supergroup's sums to the caller's u64 counters (ceil(groups / kSuperGroup) same-address atomics per counter). Rows
+// are padded to whole 128-byte lines. Grids above kFusedMaxGrid (the small-frame kernel's 1,280 workgroups) store
+// plain rows and sum them in a second kernel (dk_flow_reduce_kernel): measured 27.1 us per C3 batch against 31.4 with
+// the two-level in-launch tree and 30.7 with one level — at that grid every workgroup's exit drain and
+// ticket round trip, all at once at the end of a uniform batch, cost more than one kernel boundary.
 #ifndef DK_FUSED_MAX_GRID
 #define DK_FUSED_MAX_GRID 1024
 #endif
@@ -70,7 +72,16 @@ constexpr uint32_t kFusedMaxGrid = DK_FUSED_MAX_GRID;
 #define DK_COUNT_GROUP 16
 #endif
 constexpr uint32_t kCountGroup = DK_COUNT_GROUP;
+#ifndef DK_SUPER_GROUP
+#define DK_SUPER_GROUP 8
+#endif
+constexpr uint32_t kSuperGroup = DK_SUPER_GROUP;
 constexpr uint32_t kRowAlignWords = 32;
+// Tickets of a launch of `grid` workgroups: one per group, then one per supergroup.
+DK_HD uint32_t count_tickets(uint32_t grid) {
+    const uint32_t ng = (grid + kCountGroup - 1) / kCountGroup;
+    return ng + (ng + kSuperGroup - 1) / kSuperGroup;
+}
 
 // Kernel parameters (passed by value).
 struct RxParams {
@@ -92,7 +103,9 @@ struct RxParams {
     uint32_t row_stride;     // row_words rounded up to kRowAlignWords
     uint32_t* flow_scratch;  // [grid][row_stride]: the packed-u16 flow histogram (kFlowLds), then the u32 verdict
                              // histogram; nullptr when row_words == 0
-    uint32_t* tickets;       // [ceil(grid / kCountGroup)] arrival tickets, 0 between launches (the last arriver resets)
+    uint32_t* tickets;       // [count_tickets(grid)] arrival tickets, 0 between launches (the last arrivers reset them)
+    uint32_t* group_rows;    // [groups][group_stride]: level-1 sums (u32 per flow, then per verdict)
+    uint32_t group_stride;   // 2 * flow_words + DK_V_COUNT rounded up to kRowAlignWords
     uint32_t fused;          // 1: rows combined in-launch (flush_counters); 0: plain rows + dk_flow_reduce_kernel
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
     uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave (tuning)

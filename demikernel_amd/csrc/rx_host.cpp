@@ -26,8 +26,8 @@ constexpr uint32_t kDefaultChunkFrames = 1u << 16;
 constexpr uint64_t kMaxChunkBytes = 256ull << 20;
 constexpr size_t kMaxStreamSlots = 8;
 
-// Counter scratch of one stream's launches: per-workgroup rows and the group arrival tickets of flush_counters
-// (rx_kernels.hip). Tickets are zeroed once at allocation; each launch's last arrivers reset theirs.
+// Counter scratch of one stream's launches: per-workgroup rows, the level-1 group rows and the arrival tickets of
+// flush_counters (rx_kernels.hip). Tickets are zeroed once at allocation; each launch's last arrivers reset theirs.
 struct CountScratch {
     uint32_t* rows = nullptr;
     size_t rows_words = 0;
@@ -189,11 +189,12 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
     return 0;
 }
 
-// Rows for `grid` workgroups and their group tickets. Growing waits for the slot's last launch before freeing.
-int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride) {
+// Rows for `grid` workgroups, their group rows and tickets. Growing waits for the slot's last launch before freeing.
+int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t group_stride) {
     CountScratch& cs = s.cs;
-    const size_t words = (size_t)grid * row_stride;
-    const uint32_t nt = (grid + dk::kCountGroup - 1) / dk::kCountGroup;
+    const size_t ngroups = (grid + dk::kCountGroup - 1) / dk::kCountGroup;
+    const size_t words = (size_t)grid * row_stride + ngroups * group_stride;
+    const uint32_t nt = dk::count_tickets(grid);
     if (cs.rows_words >= words && cs.ntickets >= nt) return 0;
     if (hipStreamSynchronize(s.stream) != hipSuccess) return EIO;  // launches still using the old buffers
     if (cs.rows_words < words) {
@@ -227,6 +228,8 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.row_stride = 0;
     p.flow_scratch = nullptr;
     p.tickets = nullptr;
+    p.group_rows = nullptr;
+    p.group_stride = 0;
     p.fused = 0;
     uint32_t dyn = 0;
     if (p.res.flow_counts && c->nflows) {
@@ -280,8 +283,11 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (p.row_words) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
         p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
-        if ((rc = ensure_counts(*slot, grid, p.row_stride))) return rc;
+        p.group_stride = (2 * p.flow_words + DK_V_COUNT + dk::kRowAlignWords - 1) / dk::kRowAlignWords *
+                         dk::kRowAlignWords;
+        if ((rc = ensure_counts(*slot, grid, p.row_stride, p.group_stride))) return rc;
         p.flow_scratch = slot->cs.rows;
+        p.group_rows = slot->cs.rows + (size_t)grid * p.row_stride;
         p.tickets = slot->cs.tickets;
         p.fused = grid <= dk::kFusedMaxGrid ? 1u : 0u;
     }

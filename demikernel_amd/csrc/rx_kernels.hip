@@ -1049,21 +1049,27 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
 }
 
 // Workgroup exit: the LDS histograms (flow words in kFlowLds mode, then the verdict words) reach the caller's u64
-// counters. Two forms, picked by the host per launch (P.fused, rx_common.h kFusedMaxGrid):
-// * in-launch (grids up to ~1k workgroups), no second kernel (a dependent launch costs a ~1.5-1.9 us boundary plus its
-//   own run):
+// counters, combined inside the launch (P.fused) by a two-level tree of arrival tickets:
 //   1. each workgroup writes its row write-through (sc1 stores: the line goes to memory and leaves this XCD's L2),
-//      every storing wave drains (s_waitcnt vmcnt(0)), then one lane adds 1 to its group's arrival ticket (agent
-//      scope);
-//   2. the workgroup whose add returns kCountGroup - 1 (the group's last) reads the group's rows with sc1 loads (L1
-//      bypassed; no other XCD has the lines cached: sc1 stores drop them) and adds the column sums to the caller's
-//      counters with device-scope atomics (kCountGroup rows per add: no same-address pile-up of every workgroup, which
-//      cost ~14 us at 1024 workgroups), then resets the ticket for the next launch.
-//   This is MI355X_MICROARCH.md §"inter-workgroup visibility", Valid forms row 1 (write-through payload, drained, one
-//   agent-scope add per storing workgroup, the last adder told by the returned value, sc1 loads): no release or
-//   acquire fence.
-// * larger grids (1536 workgroups of the small-frame kernel): plain row stores, dk_flow_reduce_kernel adds them up
-//   (measured faster there: every workgroup's exit drain and ticket round trip cost more than one boundary).
+//      every storing wave drains (s_waitcnt vmcnt(0)), then one lane adds 1 to its group's ticket (agent scope);
+//   2. the workgroup whose add returns gn - 1 (the last of its group of kCountGroup) sums the group's rows (sc1 loads)
+//      into one group row of u32 columns (flow f at column f, then the verdicts), stores it write-through, drains and
+//      adds 1 to its supergroup's ticket;
+//   3. the last group winner of each supergroup of kSuperGroup groups sums those group rows and adds the column sums to
+//      the caller's counters with device-scope atomics: ceil(groups / kSuperGroup) adds per counter (C3's 1,280
+//      workgroups: 80 groups, 10 supergroups, 10 adds per address instead of the 80 of one level, whose same-address
+//      atomics serialised at ~75 ns each); then it resets its tickets for the next launch.
+//   A grid of one group skips level 2. This is MI355X_MICROARCH.md §"inter-workgroup visibility", Valid forms row 1
+//   (write-through payload, drained, one agent-scope add per storing workgroup, the last adder told by the returned
+//   value, sc1 loads), applied per level. It relies on gfx9's memory pipeline — sc1 stores write through, and stores are
+//   counted by vmcnt, so the drain orders them before the ticket — rather than on release/acquire atomics, whose
+//   agent-scope forms here are a whole-L2 writeback (buffer_wbl2) and invalidate (buffer_inv) per workgroup; the guard
+//   below keeps the pattern on the architectures it was written and tested for.
+// P.fused == 0 (grids above kFusedMaxGrid, rx_common.h: the small-frame kernel's): plain row stores, and
+// dk_flow_reduce_kernel adds them up in a second launch.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "flush_counters: the in-launch combine's ordering is written for gfx942/gfx950 (sc1 write-through, vmcnt stores)"
+#endif
 typedef __attribute__((address_space(1))) uint32_t gu32;
 __device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
     __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1071,6 +1077,21 @@ __device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
     return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool arrive_last(uint32_t* ticket, uint32_t count, uint32_t tid, uint32_t* s_last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its write-through stores have landed
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = old == count - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool last = *s_last != 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    return last;
+}
+__device__ __forceinline__ void add_u64(uint64_t* p, uint64_t v) {
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
 }
 __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
                                                const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
@@ -1088,44 +1109,62 @@ __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, 
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += nthreads) st_wt(row + k, s_flow[k]);
     if (P.res.verdict_counts && tid < kVerdictWords) st_wt(row + P.flow_words + tid, tid < DK_V_COUNT ? s_vh[tid] : 0u);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its row stores have reached memory
-    __syncthreads();
+    const uint32_t ngroups = (gridDim.x + kCountGroup - 1) / kCountGroup;
     const uint32_t g = blockIdx.x / kCountGroup, r0 = g * kCountGroup;
     const uint32_t gn = min(kCountGroup, gridDim.x - r0);
-    if (tid == 0) {
-        const uint32_t old = __hip_atomic_fetch_add((gu32*)(P.tickets + g), 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = old == gn - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!*s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    if (!arrive_last(P.tickets + g, gn, tid, s_last)) return;
+    // level 1: the group's rows, column by column (all kCountGroup loads in flight; a short group re-reads its last)
+    const bool direct = ngroups == 1;  // one group: its winner adds to the caller's counters itself
+    const uint32_t fw2 = 2 * P.flow_words;
+    uint32_t* grow = P.group_rows + (size_t)g * P.group_stride;
     const uint32_t* rows = P.flow_scratch + (size_t)r0 * P.row_stride;
     for (uint32_t w = tid; w < P.row_words; w += nthreads) {
         uint32_t x[kCountGroup];
 #pragma unroll
-        for (uint32_t k = 0; k < kCountGroup; k++)  // all loads in flight (a short group re-reads its last row)
+        for (uint32_t k = 0; k < kCountGroup; k++)
             x[k] = ld_wt(rows + (size_t)min(k, gn - 1) * P.row_stride + w);
 #pragma unroll
         for (uint32_t k = 0; k < kCountGroup; k++) x[k] = k < gn ? x[k] : 0u;
-        uint64_t lo = 0, hi = 0;
+        uint32_t lo = 0, hi = 0;  // < kCountGroup * 65536 each
 #pragma unroll
         for (uint32_t k = 0; k < kCountGroup; k++) {
             lo += x[k] & 0xFFFFu;
             hi += x[k] >> 16;
         }
-        if (w >= P.flow_words) {  // verdict column: a plain u32 count
+        if (w >= P.flow_words) {  // verdict column: a plain u32 count (< 2^21 per group)
             const uint32_t v = w - P.flow_words;
-            const uint64_t t = lo + (hi << 16);
-            if (t && v < DK_V_COUNT)
-                atomicAdd(reinterpret_cast<unsigned long long*>(P.res.verdict_counts + v), (unsigned long long)t);
+            if (v >= DK_V_COUNT) continue;
+            if (direct) add_u64(P.res.verdict_counts + v, lo + ((uint64_t)hi << 16));
+            else st_wt(grow + fw2 + v, lo + (hi << 16));
+        } else if (direct) {
+            add_u64(P.res.flow_counts + 2 * w, lo);
+            if (2 * w + 1 < P.nflows) add_u64(P.res.flow_counts + 2 * w + 1, hi);
         } else {
-            if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + 2 * w), (unsigned long long)lo);
-            if (hi && 2 * w + 1 < P.nflows)
-                atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + 2 * w + 1), (unsigned long long)hi);
+            st_wt(grow + 2 * w, lo);
+            st_wt(grow + 2 * w + 1, hi);
         }
     }
     if (tid == 0) __hip_atomic_store((gu32*)(P.tickets + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (direct) return;
+    // level 2: the supergroup's group rows
+    const uint32_t sg = g / kSuperGroup, g0 = sg * kSuperGroup;
+    const uint32_t sgn = min(kSuperGroup, ngroups - g0);
+    uint32_t* t2 = P.tickets + ngroups + sg;
+    if (!arrive_last(t2, sgn, tid, s_last)) return;
+    const uint32_t gwords = fw2 + (P.res.verdict_counts ? (uint32_t)DK_V_COUNT : 0u);
+    const uint32_t* grows = P.group_rows + (size_t)g0 * P.group_stride;
+    for (uint32_t w = tid; w < gwords; w += nthreads) {
+        if (w < fw2 && (w >= P.nflows || !lds_flows)) continue;
+        uint32_t x[kSuperGroup];
+#pragma unroll
+        for (uint32_t k = 0; k < kSuperGroup; k++) x[k] = ld_wt(grows + (size_t)min(k, sgn - 1) * P.group_stride + w);
+        uint64_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSuperGroup; k++) t += k < sgn ? x[k] : 0u;
+        if (w < fw2) add_u64(P.res.flow_counts + w, t);
+        else add_u64(P.res.verdict_counts + (w - fw2), t);
+    }
+    if (tid == 0) __hip_atomic_store((gu32*)t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
@@ -1226,6 +1265,15 @@ struct SmallLds {
 #endif
 constexpr uint32_t kSmallWaves = DK_SMALL_WAVES;
 constexpr int kSmallBlock = 64 * DK_SMALL_WAVES;
+// The window lives in LDS swizzled: slot s holds window granule s ^ ((s >> 4) & 3) (an involution: it swaps granules
+// within aligned groups of 4 by bits 4-5 of the index, so each DMA piece still reads the same 64-byte pieces of the
+// blob). Unswizzled, 64 packed 64-byte frames read back as 4 ds_read_b128 at a 64-byte lane stride put lanes
+// {0, 12, 20, 24} of every lane group on the same 4 banks (MI355X_MICROARCH.md §LDS: 4-way, 3 extra cycles per group);
+// swizzled, the 16 lanes of a group cover the 64 banks once.
+#ifndef DK_WIN_SWIZZLE
+#define DK_WIN_SWIZZLE 1
+#endif
+__device__ __forceinline__ uint32_t win_slot(uint32_t g) { return DK_WIN_SWIZZLE ? g ^ ((g >> 4) & 3u) : g; }
 // Window plan of one chunk (wave-uniform): DMA'd into the wave's LDS slot, or per-lane loads.
 struct WinPlan {
     bool win;
@@ -1247,8 +1295,9 @@ __device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F
     const bool inwin = !use || (a >= lo && off + len <= hi);
     if (hi > lo && hi - lo <= kGran * 16 && !__ballot(live && !inwin)) {
         const uint32_t G = (hi - lo + 15) >> 4;  // wave-uniform
+        const uint32_t sl = win_slot(lane);  // the granule this lane's slot holds (slots 64 k + lane)
         for (uint32_t k = 0; k * 64 < G; k++) {
-            const uint32_t g = 64 * k + lane;
+            const uint32_t g = 64 * k + sl;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(B.rs, (lds_void*)&W.win[64 * k], 16, g < G ? lo + 16 * g : kOob,
                                                      0, 0, DK_NT_LOADS ? 2 : 0);
         }
@@ -1263,10 +1312,13 @@ template <bool kShift, class WL>
 __device__ __forceinline__ void small_window_read(const WinPlan& pl, const FrameDesc<kShift>& F, const Blob& B,
                                                   uint32_t off, WL& W, RegAcc& R) {
     if (pl.win) {
+        // The DMA pieces must have landed: wait for them explicitly (the compiler's own LDS-DMA tracking dropped
+        // this wait once the read addresses were computed, round 3).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t b = F.vec && !F.big ? (off - F.sh - pl.lo) >> 4 : 0u;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint4 q = W.win[b + k];
+            const uint4 q = W.win[win_slot(b + k)];
             R.w[4 * k + 0] = q.x;
             R.w[4 * k + 1] = q.y;
             R.w[4 * k + 2] = q.z;
@@ -1389,17 +1441,17 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
         const bool have2 = have1 && r.chunk(k + 2, c2, lim2);
-        uint32_t off2 = 0, len2 = 0;
-        if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead
-            off2 = P.off[c2 + r.lane_off];
-            len2 = P.len[c2 + r.lane_off];
-        }
         const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + r.lane_off < lim1, off1, len1);
         uint32_t v, fid;
         Rec rec;
         rec.meta = kNoRec;
         if (k == 0) DK_STAMP(1);
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
+        uint32_t off2 = 0, len2 = 0;
+        if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead (after the window wait)
+            off2 = P.off[c2 + r.lane_off];
+            len2 = P.len[c2 + r.lane_off];
+        }
         DK_STAMP(2 + 3 * k);
         small_big_frames(F, lane, off, B, W, C);
         rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,

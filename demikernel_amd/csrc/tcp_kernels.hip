@@ -14,6 +14,14 @@
 //      (latency-bound, lanes = connections); everything else is a pass over the batch.
 //   4'. dk_tcp_wave_walk_kernel instead, at >= kWaveWalkMinSegs segments per connection: one wave per connection,
 //      64 segments classified in parallel per step, the state machine only for the segments that need it.
+// Segments whose outcome cannot depend on their place in the connection's order are classified in step 1 and never
+// walked: RCV.NXT only moves forward, from its value at the start of the batch up to the window end (reader_next +
+// buffer size, fixed during the batch), so a segment starting past the window end is OUT_OF_WINDOW whenever it is
+// processed, and one ending before the starting RCV.NXT is a DUPLICATE (check_segment_in_window, ctrlblk.rs:447-567;
+// the bounds below keep every wrapping comparison on the same side). Only the connection's state decides between
+// that and UNPROCESSED (queued behind a close): the walks record the first frame index after the close, and
+// 5. dk_tcp_fix_kernel turns the classified segments from there on into UNPROCESSED. A connection whose window is
+// full (every later segment beyond it) then costs one coalesced pass instead of a serial walk.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -54,30 +62,63 @@ struct Params {
     uint32_t* skeys;
     uint32_t* svals;
     uint4* rec;        // [n] {seq, ack, meta, payload} in frame order
-    uint32_t* range;   // [nconns + 1]: connection c's segments are svals[range[c] .. range[c + 1])
+    uint32_t* range;   // [2 nconns + 1]: connection c's segments are svals[range[2c] .. range[2c + 2]), of which
+                       // [range[2c], range[2c + 1]) are walked and the rest were classified (sort key 2c + 1)
+    uint32_t* cls;     // [n]: the connection of a segment classified in the key kernel (never walked), else kNoConn
+    uint32_t* open_until;  // [nconns]: frames of the connection from this index on come after its close
     dk_tcp_out out;
 };
+constexpr uint32_t kNoConn = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(kBlock) void dk_tcp_key_kernel(Params P) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= P.n) return;
-    const uint32_t meta = P.meta[i], pay = P.payload[i];
-    uint32_t key = P.nconns;
+    const uint32_t meta = P.meta[i], pay = P.payload[i], seq = P.seq[i];
+    uint32_t key = 2 * P.nconns, cls = kNoConn;  // sort key: 2c walked, 2c + 1 classified, 2 nconns not c's
+    uint8_t act = DK_TCP_SKIP;
     if ((meta & 0xFFu) == DK_V_OK_TCP) {
         const uint32_t f = P.flow_id[i];
-        if (f < P.nconns && P.conns[f].state != DK_TCP_NONE) key = f;
+        if (f < P.nconns) {
+            const dk_tcp_conn& t = P.conns[f];
+            const uint32_t state = t.state;
+            if (state != DK_TCP_NONE) key = 2 * f;
+            const uint32_t bufsz = t.buffer_size, rn0 = t.receive_next, wend = t.reader_next + bufsz;
+            // order-independent outcomes (see the top of the file); the bounds keep (seq - RCV.NXT) and
+            // (seg_end - RCV.NXT) of every RCV.NXT in [rn0, wend] on one side of the wrap
+            if (state == DK_TCP_ESTABLISHED && wend - rn0 <= bufsz && bufsz < 0x40000000u) {
+                const uint32_t flags = (meta >> 16) & 0xFFu, len = pay >> 16;
+                const uint32_t full = len + ((flags >> 1) & 1u) + (flags & 1u);
+                const uint32_t seg_end = full ? seq + (full - 1) : seq;
+                const uint32_t lim = 0x7FFFFFFFu - bufsz - 0x20000u;
+                if (seq - wend - 1u < lim) act = DK_TCP_OUT_OF_WINDOW;  // seq - wend in [1, lim]
+                else if (rn0 - seg_end - 1u < lim) act = DK_TCP_DUPLICATE;  // seg_end - rn0 in [-lim, -1]
+                if (act != DK_TCP_SKIP) {
+                    cls = f;
+                    key = 2 * f + 1;
+                }
+            }
+        }
     }
     P.keys[i] = key;
-    P.rec[i] = make_uint4(P.seq[i], P.ack[i], meta, pay);
-    if (key == P.nconns) {  // the walk writes the outputs of every segment it owns
-        P.out.action[i] = DK_TCP_SKIP;
+    P.cls[i] = cls;
+    P.rec[i] = make_uint4(seq, P.ack[i], meta, pay);
+    if (key == 2 * P.nconns || cls != kNoConn) {  // the walk writes the outputs of every segment it owns
+        P.out.action[i] = act;
         P.out.view[i] = dk_tcp_view{i, pay & 0xFFFFu, pay >> 16};
     }
 }
 
+// Classified segments after their connection's close are UNPROCESSED (the walks' queued-behind-the-close rule).
+__global__ __launch_bounds__(kBlock) void dk_tcp_fix_kernel(Params P) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P.n) return;
+    const uint32_t c = P.cls[i];
+    if (c != kNoConn && i >= P.open_until[c]) P.out.action[i] = DK_TCP_UNPROCESSED;
+}
+
 __global__ __launch_bounds__(kBlock) void dk_tcp_range_kernel(Params P) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c > P.nconns) return;
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;  // a sort key value, 0 .. 2 nconns
+    if (c > 2 * P.nconns) return;
     uint32_t lo = 0, hi = P.n;  // first p with skeys[p] >= c
     while (lo < hi) {
         const uint32_t mid = lo + (hi - lo) / 2;
@@ -312,14 +353,15 @@ __global__ __launch_bounds__(kWalkBlock) void dk_tcp_walk_kernel(Params P) {
     const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
     if (c >= P.nconns) return;
     dk_tcp_conn* t = P.conns + c;
-    const uint32_t k0 = P.range[c], cnt = P.range[c + 1] - k0;
+    const uint32_t k0 = P.range[2 * c], cnt = P.range[2 * c + 1] - k0, all = P.range[2 * c + 2] - k0;
     const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c;
     P.out.deliv_start[c] = d0;
     Walk w{t->state, t->receive_next, t->reader_next, t->buffer_size, t->send_next, t->fin_pending, t->fin_seq,
            min(t->ooo_count, DK_TCP_OOO_MAX)};
     Store s{lds + threadIdx.x};
     for (uint32_t k = 0; k < w.nooo; k++) s.set(k, t->ooo_start[k], t->ooo[k]);
-    Out o{P.out.deliv + d0, 0, cnt + DK_TCP_DELIV_EXTRA};
+    uint32_t open_until = w.state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u;
+    Out o{P.out.deliv + d0, 0, all + DK_TCP_DELIV_EXTRA};
     // Software pipeline over batches of kBatch segments: frame indices two batches ahead, their records one batch
     // ahead, so neither load level waits in the loop (the walk is latency-bound: about one wave per SIMD).
     uint32_t ia[kBatch], ib[kBatch], ic[kBatch];
@@ -361,8 +403,10 @@ __global__ __launch_bounds__(kWalkBlock) void dk_tcp_walk_kernel(Params P) {
             dk_tcp_view v;
             P.out.action[ic[j]] = (uint8_t)process(s, w, gc[j], ic[j], o, v);
             P.out.view[ic[j]] = v;
+            if (w.state != DK_TCP_ESTABLISHED) open_until = ic[j] + 1;  // this segment closed the connection
         }
     }
+    P.open_until[c] = open_until;
     t->state = w.state;
     t->receive_next = w.rn;
     t->fin_pending = w.fin_pending;
@@ -397,7 +441,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     __shared__ WaveScan::storage_type scan_tmp;
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     dk_tcp_conn* t = P.conns + c;
-    const uint32_t k0 = P.range[c], cnt = P.range[c + 1] - k0;
+    const uint32_t k0 = P.range[2 * c], cnt = P.range[2 * c + 1] - k0, all = P.range[2 * c + 2] - k0;
     const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c;
     // the connection's scalar state, wave-uniform: held in scalar registers
 #define DK_U(x) (uint32_t) __builtin_amdgcn_readfirstlane((int)(x))
@@ -409,8 +453,9 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
         const dk_tcp_view v = t->ooo[lane];
         s = RegStore{t->ooo_start[lane], v.ref, v.off, v.len, lane};
     }
-    Out o{P.out.deliv + d0, 0, cnt + DK_TCP_DELIV_EXTRA};
+    Out o{P.out.deliv + d0, 0, all + DK_TCP_DELIV_EXTRA};
     const uint32_t wend = w.reader + w.bufsz;
+    uint32_t open_until = w.state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u;
     // Software pipeline over windows: frame indices kAhead + 1 windows ahead, records kAhead windows ahead (register
     // rings iq / gq: slot j holds window base / 64 + j).
     uint32_t iq[kAhead + 1];
@@ -515,11 +560,13 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
                 P.out.action[i_f] = (uint8_t)a_f;
                 P.out.view[i_f] = v;
             }
+            if (w.state != DK_TCP_ESTABLISHED) open_until = i_f + 1;  // this segment closed the connection
             lo = f + 1;
         }
     }
     if (lane == 0) {
         P.out.deliv_start[c] = d0;
+        P.open_until[c] = open_until;
         t->state = w.state;
         t->receive_next = w.rn;
         t->fin_pending = w.fin_pending;
@@ -586,8 +633,8 @@ struct dk_tcp_ctx {
     hipEvent_t last = nullptr;
     hipStream_t last_stream = nullptr;
     bool used = false;
-    uint32_t *keys = nullptr, *skeys = nullptr, *svals = nullptr, *range = nullptr;
-    size_t keys_cap = 0, skeys_cap = 0, svals_cap = 0, range_cap = 0;
+    uint32_t *keys = nullptr, *skeys = nullptr, *svals = nullptr, *range = nullptr, *cls = nullptr, *open_until = nullptr;
+    size_t keys_cap = 0, skeys_cap = 0, svals_cap = 0, range_cap = 0, cls_cap = 0, open_cap = 0;
     uint4* rec = nullptr;
     size_t rec_cap = 0;
     uint8_t* temp = nullptr;
@@ -617,7 +664,8 @@ void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     if (!t) return;
     dk_tcp::DeviceGuard g(t->device);
     if (t->used) (void)hipEventSynchronize(t->last);
-    for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp})
+    for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp,
+                    (void*)t->cls, (void*)t->open_until})
         if (p) (void)hipFree(p);
     (void)hipEventDestroy(t->last);
     delete t;
@@ -638,14 +686,16 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     const hipStream_t s = (hipStream_t)stream;
     int rc = 0;
     if (t->used && t->last_stream != s && hipStreamWaitEvent(s, t->last, 0) != hipSuccess) return EINVAL;
-    const bool grows = t->keys_cap < n || t->rec_cap < n || t->range_cap < (size_t)nconns + 1;
+    const bool grows = t->keys_cap < n || t->rec_cap < n || t->range_cap < 2 * (size_t)nconns + 1 || t->cls_cap < n ||
+                       t->open_cap < nconns;
     if (t->used && grows && hipEventSynchronize(t->last) != hipSuccess) return EINVAL;  // in-flight work on the scratch
     if ((rc = grow(t->keys, t->keys_cap, n)) || (rc = grow(t->skeys, t->skeys_cap, n)) ||
         (rc = grow(t->svals, t->svals_cap, n)) || (rc = grow(t->rec, t->rec_cap, n)) ||
-        (rc = grow(t->range, t->range_cap, (size_t)nconns + 1)))
+        (rc = grow(t->range, t->range_cap, 2 * (size_t)nconns + 1)) || (rc = grow(t->cls, t->cls_cap, n)) ||
+        (rc = grow(t->open_until, t->open_cap, nconns)))
         return rc;
     int bits = 1;
-    while (bits < 32 && (1ull << bits) <= nconns) bits++;  // keys are 0 .. nconns
+    while (bits < 32 && (1ull << bits) <= 2ull * nconns) bits++;  // keys are 0 .. 2 nconns
     const rocprim::counting_iterator<uint32_t> index(0);
     size_t sort_bytes = 0;
     if (rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, t->keys, t->skeys, index, t->svals, n, 0, bits,
@@ -668,8 +718,10 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     P.svals = t->svals;
     P.rec = t->rec;
     P.range = t->range;
+    P.cls = t->cls;
+    P.open_until = t->open_until;
     P.out = *out;
-    const dim3 gn((n + kBlock - 1) / kBlock), gr((nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
+    const dim3 gn((n + kBlock - 1) / kBlock), gr((2 * nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
     if (n) {
         hipLaunchKernelGGL(dk_tcp_key_kernel, gn, dim3(kBlock), 0, s, P);
         size_t b = t->temp_cap;
@@ -687,6 +739,7 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
         else
             hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
     }
+    if (n && nconns) hipLaunchKernelGGL(dk_tcp_fix_kernel, gn, dim3(kBlock), 0, s, P);
     if (hipGetLastError() != hipSuccess) return EINVAL;
     if (hipEventRecord(t->last, s) != hipSuccess) return EINVAL;
     t->last_stream = s;
