@@ -738,6 +738,9 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WL& W, ui
         return C.fsum - pre - post;
     }
     resum = true;
+#ifdef DK_ABL_FASTONLY
+    return 0;
+#endif
     return MemAcc{f}.sum_le16(34, (uint32_t)E);
 }
 
@@ -819,7 +822,9 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     } else if (fast) {
         parse_fast(R, len, P, L);
     } else {
+#ifndef DK_ABL_FASTONLY  // ablation (tuning only, wrong for other batches): C3-shaped batches need no byte path
         parse_headers(MemAcc{f}, len, P, L);
+#endif
     }
     DK_SUB_STAMP(0);
     // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
@@ -839,7 +844,11 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
 #endif
     St.h1 = h1;
+#ifdef DK_ABL_FASTONLY
+    if (L.need) L.lsum = seg_sum_fast(C, W, lane, f, (int)L.E, resum);
+#else
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
+#endif
     DK_SUB_STAMP(1);
 }
 
@@ -873,7 +882,11 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
             const uint32_t c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
             if (c != L.stored) L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
         }
+#ifdef DK_ABL_FASTONLY
+        if (false) {
+#else
         if (L.v == kPendTcp && L.hlen > 20) {
+#endif
             const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20,
                                            kOpt && live && P.res.tcp_opts ? P.res.tcp_opts + i : nullptr);
             if (e) L.v = e;
@@ -1337,6 +1350,9 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
     uint32_t x[4] = {0, 0, 0, 0};
     C.fsum = 0;
     uint64_t bm = __ballot(F.big);
+#ifdef DK_ABL_FASTONLY
+    bm = 0;
+#endif
     if (bm) {
         while (bm) {
             const uint32_t j = (uint32_t)__builtin_ctzll(bm);
@@ -1931,8 +1947,10 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
-    if (p.small && p.aligned16)
+    if (p.small && p.aligned16 && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small)
