@@ -107,6 +107,8 @@ struct RxParams {
     uint32_t* group_rows;    // [groups][group_stride]: level-1 sums (u32 per flow, then per verdict)
     uint32_t group_stride;   // 2 * flow_words + DK_V_COUNT rounded up to kRowAlignWords
     uint32_t fused;          // 1: rows combined in-launch (flush_counters); 0: plain rows + dk_flow_reduce_kernel
+    uint64_t* defer;         // small-frame kernel: [ceil(n / 64)] masks of the frames each 64-frame chunk left to the
+                             // general path after its main loop
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)
     uint32_t sched;          // 0: round-robin 256-frame tiles; 1: one contiguous share per wave (tuning)
     uint32_t aligned16;      // DK_RX_BATCH_ALIGNED16 hint: launch the instantiation without the realignment path

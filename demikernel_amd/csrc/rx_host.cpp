@@ -33,6 +33,8 @@ struct CountScratch {
     size_t rows_words = 0;
     uint32_t* tickets = nullptr;
     uint32_t ntickets = 0;
+    uint64_t* defer = nullptr;  // the small-frame kernel's per-chunk deferral masks
+    size_t ndefer = 0;
 };
 
 // A context's scratch is keyed by stream: calls on different streams never share counter rows or tickets, so their
@@ -131,6 +133,7 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
 void free_slot(StreamSlot& s) {  // the caller has waited for the slot's launches
     if (s.cs.rows) (void)hipFree(s.cs.rows);
     if (s.cs.tickets) (void)hipFree(s.cs.tickets);
+    if (s.cs.defer) (void)hipFree(s.cs.defer);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
 }
@@ -189,13 +192,14 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
     return 0;
 }
 
-// Rows for `grid` workgroups, their group rows and tickets. Growing waits for the slot's last launch before freeing.
-int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t group_stride) {
+// Rows for `grid` workgroups, their group rows and tickets, and `ndefer` deferral masks. Growing waits for the slot's
+// last launch before freeing.
+int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t group_stride, size_t ndefer) {
     CountScratch& cs = s.cs;
     const size_t ngroups = (grid + dk::kCountGroup - 1) / dk::kCountGroup;
-    const size_t words = (size_t)grid * row_stride + ngroups * group_stride;
-    const uint32_t nt = dk::count_tickets(grid);
-    if (cs.rows_words >= words && cs.ntickets >= nt) return 0;
+    const size_t words = row_stride ? (size_t)grid * row_stride + ngroups * group_stride : 0;
+    const uint32_t nt = row_stride ? dk::count_tickets(grid) : 0;
+    if (cs.rows_words >= words && cs.ntickets >= nt && cs.ndefer >= ndefer) return 0;
     if (hipStreamSynchronize(s.stream) != hipSuccess) return EIO;  // launches still using the old buffers
     if (cs.rows_words < words) {
         if (cs.rows) (void)hipFree(cs.rows);
@@ -211,6 +215,13 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t gr
         if (hipMalloc(&cs.tickets, nt * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
         if (hipMemset(cs.tickets, 0, nt * sizeof(uint32_t)) != hipSuccess) return EIO;
         cs.ntickets = nt;
+    }
+    if (cs.ndefer < ndefer) {
+        if (cs.defer) (void)hipFree(cs.defer);
+        cs.defer = nullptr;
+        cs.ndefer = 0;
+        if (hipMalloc(&cs.defer, ndefer * sizeof(uint64_t)) != hipSuccess) return ENOMEM;
+        cs.ndefer = ndefer;
     }
     return 0;
 }
@@ -231,6 +242,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.group_rows = nullptr;
     p.group_stride = 0;
     p.fused = 0;
+    p.defer = nullptr;
     uint32_t dyn = 0;
     if (p.res.flow_counts && c->nflows) {
         const uint32_t words = (c->nflows + 1) / 2;
@@ -275,21 +287,28 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
-    // Per-workgroup histogram rows (flow pairs, then verdicts), combined in-launch per group of workgroups. Only a
-    // launch with counters uses the stream's scratch slot.
+    // Per-workgroup histogram rows (flow pairs, then verdicts), combined in-launch per group of workgroups, and the
+    // small-frame kernel's deferral masks: a launch that needs either uses the stream's scratch slot.
     StreamSlot* slot = nullptr;
     int rc = 0;
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
-    if (p.row_words) {
+    // per (wave, chunk): at most ceil(n / 64) + 2 chunks per wave of the grid (sched 1's partial chunks)
+    const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * dk_rx_small_block_waves() : 0;
+    if (p.row_words || ndefer) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
-        p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
-        p.group_stride = (2 * p.flow_words + DK_V_COUNT + dk::kRowAlignWords - 1) / dk::kRowAlignWords *
-                         dk::kRowAlignWords;
-        if ((rc = ensure_counts(*slot, grid, p.row_stride, p.group_stride))) return rc;
-        p.flow_scratch = slot->cs.rows;
-        p.group_rows = slot->cs.rows + (size_t)grid * p.row_stride;
-        p.tickets = slot->cs.tickets;
-        p.fused = grid <= dk::kFusedMaxGrid ? 1u : 0u;
+        if (p.row_words) {
+            p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
+            p.group_stride = (2 * p.flow_words + DK_V_COUNT + dk::kRowAlignWords - 1) / dk::kRowAlignWords *
+                             dk::kRowAlignWords;
+        }
+        if ((rc = ensure_counts(*slot, grid, p.row_stride, p.group_stride, ndefer))) return rc;
+        if (p.row_words) {
+            p.flow_scratch = slot->cs.rows;
+            p.group_rows = slot->cs.rows + (size_t)grid * p.row_stride;
+            p.tickets = slot->cs.tickets;
+            p.fused = grid <= dk::kFusedMaxGrid ? 1u : 0u;
+        }
+        p.defer = slot->cs.defer;
     }
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "

@@ -1403,6 +1403,112 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
     C.nblk = F.nblk;
 }
 
+// The small-frame kernel's main loop takes a frame only when it lies in its 64-byte register window (vector path, not
+// streamed), has the whole Ethernet + 20-byte IPv4 header, is not ARP and, for TCP, carries no options: then phase C
+// is the Appendix A chain from registers (parse_fast), one socket-table load, the segment sum from the window, the
+// verdict, demux and result stores — no byte path, no wave-wide big-frame sum, no option walk (a call) in the loop.
+// Every other frame is left to a second pass after the loop (per-chunk masks in the launch scratch, P.defer), which
+// runs the general phase C (rx_finish) on them; results and counts are the same either way. Keeping the general path
+// out of the loop took the loop's code from 95 VGPRs and 71 spilled SGPRs to the fast path's own.
+#ifndef DK_SMALL_DEFER
+#define DK_SMALL_DEFER 1
+#endif
+template <bool kShift>
+__device__ __forceinline__ bool small_fast_eligible(const FrameDesc<kShift>& F, uint32_t len, const RegAcc& R) {
+    const bool ihl5 = ((R.w[3] >> 16) & 0x0Fu) == 5u;
+    const bool arp = (R.w[3] & 0xFFFFu) == 0x0608u;
+    const bool topt = R.b8(23) == 6u && (R.b8(46) >> 4) > 5u;
+    return F.vec && !F.big && len >= 34 && ihl5 && !arp && !topt;
+}
+template <bool kOpt>
+__device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool live, uint32_t lane, const RegAcc& R,
+                                           uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
+    Lane L;
+    parse_fast(R, len, P, L);
+    if (!live) {
+        L.v = kNone;
+        L.need = 0;
+    }
+    // first socket-table load before the checksum arithmetic (as rx_front)
+    const ProbeKey k1{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)};
+    uint32_t h1 = 0;
+    uint4 s1 = make_uint4(0, 0, 0, 0);
+    if (L.v == kPendTcp) {
+        h1 = probe_slot(P, k1);
+        s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+    }
+    if (L.v == kPendUdp) s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+    uint32_t lsum = 0;
+    if (L.need) {  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
+        if (!__ballot(L.E != 64u)) {
+            lsum = hsum2(R.w[8] & 0xFFFF0000u, 0);
+#pragma unroll
+            for (int k = 9; k < 16; k++) lsum = hsum2(R.w[k], lsum);
+        } else {
+            const int t = 32 - 8 * (int)L.E;
+#pragma unroll
+            for (int k = 8; k < 16; k++) {
+                const uint32_t sh = (uint32_t)min(max(t + 32 * k, 0), 32);
+                uint32_t m = (uint32_t)(0xFFFFFFFFull >> sh);
+                if (k == 8) m &= 0xFFFF0000u;
+                lsum = hsum2(R.w[k] & m, lsum);
+            }
+        }
+    }
+    uint32_t fid = DK_FLOW_NONE;
+    if (L.v == kPendIcmp) {  // as rx_back (icmpv4/header.rs:55-57, protocol.rs:37-56)
+        const uint32_t type = (L.mhi >> 8) & 0xFFu;
+        L.v = mod_ffff(lsum) != 0 ? (uint32_t)DK_V_ICMP_CSUM
+              : (type < 15 && ((kIcmpTypes >> type) & 1u)) ? (uint32_t)DK_V_ICMP : (uint32_t)DK_V_ICMP_TYPE;
+    } else if (L.v == kPendTcp || L.v == kPendUdp) {
+        const bool tcp = L.v == kPendTcp;
+        if (L.need) {  // T4 / U3 (tcp/header.rs:203-207, udp/header.rs:78-88)
+            const uint32_t sm = lsum - bswap16(L.stored);
+            const uint32_t lip = P.local_ip;
+            const uint32_t pseudo = bswap16(L.src & 0xFFFFu) + bswap16(L.src >> 16) + bswap16(lip & 0xFFFFu) +
+                                    bswap16(lip >> 16) + (tcp ? 6u : 17u) + (L.E - L.S);
+            if (csum_from_residue(mod_ffff(be_residue(sm) + pseudo)) != L.stored)
+                L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
+        }
+        const uint32_t dport = L.ports >> 16;
+        if (L.v == kPendTcp) {  // Active(local, remote), then Passive(local) (tcp/peer.rs:241-251)
+            fid = probe_finish(P, k1, h1, s1);
+            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortTcpPassive, dport);
+            L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
+        } else if (L.v == kPendUdp) {  // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
+            fid = s1.x;
+            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortUdpAny, dport);
+            L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
+        }
+    }
+    const uint32_t v = L.v;
+    if (live) {
+        const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;
+        const bool is_tcp = v == DK_V_OK_TCP || v == DK_V_TCP_NOSOCK;
+        const uint32_t poff = L.S + L.hlen;
+        st_res<true>(P.res.meta + i, full ? v | L.mhi << 8 : v);
+        st_res<true>(P.res.src_ip + i, full ? L.src : 0u);
+        if (P.res.dst_ip) st_res<true>(P.res.dst_ip + i, full ? L.dst : 0u);
+        st_res<true>(P.res.ports + i, full ? L.ports : 0u);
+        st_res<true>(P.res.payload + i, full ? poff | ((L.E - poff) << 16) : 0u);
+        st_res<true>(P.res.flow_id + i, fid);
+        if (kOpt) {
+            const bool t = full && is_tcp;
+            if (P.res.tcp_seq) P.res.tcp_seq[i] = t ? L.seq : 0u;
+            if (P.res.tcp_ack) P.res.tcp_ack[i] = t ? L.ack : 0u;
+            if (P.res.tcp_win) P.res.tcp_win[i] = t ? L.winurg : 0u;
+        }
+    }
+#ifndef DK_DIAG_STAMPS
+    if (kOpt && P.path_stats) {  // diagnostics (dk_diag.h): every frame taken here is a register-window frame (path 0)
+        const uint64_t m = __ballot(live);
+        if (m && lane == 0) atomicAdd(P.path_stats + 0, (unsigned long long)__popcll(m));
+    }
+#endif
+    v_out = v;
+    fid_out = fid;
+}
+
 #ifdef DK_DIAG_STAMPS  // diagnostic build (tuning only): per-wave s_memrealtime stamps after the path counters
 // s_memtime (shader clock, per XCD) for durations; slots 12/13 hold s_memrealtime (100 MHz, global) at entry/exit.
 #define DK_STAMP_T(slot, t)                                                                                         \
@@ -1453,6 +1559,8 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     }
     Chunk C;
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
+    const uint32_t nw = gridDim.x * kSmallWaves, gw = blockIdx.x * kSmallWaves + wv;  // deferral mask index k nw + gw
+    bool deferred = false;  // wave-uniform: a chunk left frames to the general pass
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1469,11 +1577,25 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
             len2 = P.len[c2 + r.lane_off];
         }
         DK_STAMP(2 + 3 * k);
+#if DK_SMALL_DEFER
+        if (kShift && __ballot(live && F.vec && !F.big && F.sh != 0)) {  // realign the windows of shifted frames
+            uint32_t x[4] = {0, 0, 0, 0};
+            if (F.vec && !F.big && F.sh != 0) realign(C.R.w, x, F.sh);
+        }
+        const bool take = live && small_fast_eligible(F, len, C.R);
+        const uint64_t dm = __ballot(live && !take);
+        if (lane == 0) P.defer[k * nw + gw] = dm;  // every chunk's mask, read back by this wave after the loop
+        deferred = deferred || dm != 0;
+        small_fast<kOpt>(P, i, take, lane, C.R, len, v, fid);
+        DK_STAMP(3 + 3 * k);
+        count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
+#else
         small_big_frames(F, lane, off, B, W, C);
         rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,
                                                        k < 3 ? 16 + 5 * k : ~0u);
         DK_STAMP(3 + 3 * k);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+#endif
         DK_STAMP(4 + 3 * k);
         // rotate the pipeline
         have = have1;
@@ -1488,6 +1610,27 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
+#if DK_SMALL_DEFER
+    if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
+        uint32_t cd, limd;
+        for (uint32_t k = 0; r.chunk(k, cd, limd); k++) {
+            const uint64_t m = P.defer[k * nw + gw];  // wave-uniform
+            if (!m) continue;
+            const uint32_t i = cd + r.lane_off;
+            const bool mine = (m >> lane) & 1u;
+            const uint32_t o = mine ? P.off[i] : 0u, ln = mine ? P.len[i] : 0u;
+            const FrameDesc<kShift> Fd(P.frames, P.frames_bytes, mine, o, ln);
+            small_load(Fd, B, o, C.R);
+            small_big_frames(Fd, lane, o, B, W, C);
+            uint32_t v, fid;
+            Rec rec;
+            rec.meta = kNoRec;
+            rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, mine, lane, W, o, ln, C, v, fid, rec);
+            count_chunk(P, mine, lane, v, fid, lds_flows, s_flow, s_vh);
+        }
+    }
+#endif
 #ifdef DK_DIAG_STAMPS
     DK_STAMP_T(14, __builtin_amdgcn_s_memtime());
 #endif
