@@ -1799,6 +1799,9 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
                                                                 uint32_t nflows, uint64_t* counts,
                                                                 uint64_t* verdicts) {
     __shared__ uint64_t s_part[kWaves][2][kReduceCols];
+#ifdef DK_ABL_REDUCE_EMPTY  // ablation (tuning only): the cost of the second launch alone
+    return;
+#endif
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t w = blockIdx.x * kReduceCols + lane;
     const uint32_t r0 = blockIdx.y * kReduceRows, r1 = min(rows, r0 + kReduceRows);
@@ -1825,6 +1828,10 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
         lo += s_part[k][0][lane];
         hi += s_part[k][1][lane];
     }
+#ifdef DK_ABL_REDUCE_NOATOMIC  // ablation (tuning only): loads and sums, no atomics
+    if (lo == 0x123456789ull) counts[0] = hi;
+    return;
+#endif
     if (w >= flow_words) {  // verdict column: a plain u32 count
         const uint32_t v = w - flow_words;
         const uint64_t t = lo + (hi << 16);
