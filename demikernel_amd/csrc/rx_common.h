@@ -77,10 +77,16 @@ constexpr uint32_t kCountGroup = DK_COUNT_GROUP;
 #endif
 constexpr uint32_t kSuperGroup = DK_SUPER_GROUP;
 constexpr uint32_t kRowAlignWords = 32;
-// Tickets of a launch of `grid` workgroups: one per group, then one per supergroup.
+// Tickets of a launch of `grid` workgroups: one per group, then one per supergroup, each on a 128-byte line of its own
+// (kTicketStride words): device-scope atomics to one line serialise at ~12 ns each (MI355X_MICROARCH.md, fanin), so
+// tickets sharing lines made every group's arrivals queue behind every other group's (C3: 1,280 adds on 3 lines).
+#ifndef DK_TICKET_STRIDE
+#define DK_TICKET_STRIDE 32
+#endif
+constexpr uint32_t kTicketStride = DK_TICKET_STRIDE;
 DK_HD uint32_t count_tickets(uint32_t grid) {
     const uint32_t ng = (grid + kCountGroup - 1) / kCountGroup;
-    return ng + (ng + kSuperGroup - 1) / kSuperGroup;
+    return (ng + (ng + kSuperGroup - 1) / kSuperGroup) * kTicketStride;
 }
 
 // Kernel parameters (passed by value).

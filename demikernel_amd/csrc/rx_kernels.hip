@@ -1092,7 +1092,12 @@ __device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
                              __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool arrive_last(uint32_t* ticket, uint32_t count, uint32_t tid, uint32_t* s_last) {
+#ifdef DK_ABL_NOTICKET  // ablation (tuning only, counts wrong): rows stored, no combine
+    return false;
+#endif
+#ifndef DK_ABL_NODRAIN  // ablation (tuning only, unordered): no drain before the ticket
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its write-through stores have landed
+#endif
     __syncthreads();
     if (tid == 0) {
         const uint32_t old = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1125,7 +1130,7 @@ __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, 
     const uint32_t ngroups = (gridDim.x + kCountGroup - 1) / kCountGroup;
     const uint32_t g = blockIdx.x / kCountGroup, r0 = g * kCountGroup;
     const uint32_t gn = min(kCountGroup, gridDim.x - r0);
-    if (!arrive_last(P.tickets + g, gn, tid, s_last)) return;
+    if (!arrive_last(P.tickets + g * kTicketStride, gn, tid, s_last)) return;
     // level 1: the group's rows, column by column (all kCountGroup loads in flight; a short group re-reads its last)
     const bool direct = ngroups == 1;  // one group: its winner adds to the caller's counters itself
     const uint32_t fw2 = 2 * P.flow_words;
@@ -1157,12 +1162,16 @@ __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, 
             st_wt(grow + 2 * w + 1, hi);
         }
     }
-    if (tid == 0) __hip_atomic_store((gu32*)(P.tickets + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0)
+        __hip_atomic_store((gu32*)(P.tickets + g * kTicketStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (direct) return;
+#ifdef DK_ABL_L1ONLY  // ablation (tuning only, counts wrong): level 1 only
+    return;
+#endif
     // level 2: the supergroup's group rows
     const uint32_t sg = g / kSuperGroup, g0 = sg * kSuperGroup;
     const uint32_t sgn = min(kSuperGroup, ngroups - g0);
-    uint32_t* t2 = P.tickets + ngroups + sg;
+    uint32_t* t2 = P.tickets + (ngroups + sg) * kTicketStride;
     if (!arrive_last(t2, sgn, tid, s_last)) return;
     const uint32_t gwords = fw2 + (P.res.verdict_counts ? (uint32_t)DK_V_COUNT : 0u);
     const uint32_t* grows = P.group_rows + (size_t)g0 * P.group_stride;
