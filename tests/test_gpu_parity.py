@@ -384,17 +384,20 @@ def test_tx_checksum_large_frames_schedule(torch_cuda):
     tx_check(blob, off, lens, "large")
 
 
+@pytest.mark.parametrize("sizes", ["imix", "min64"])
 @pytest.mark.parametrize("mem", ["pageable", "pinned_staged", "pinned_zero_copy"])
-def test_host_pipeline_matches_device_path(torch_cuda, monkeypatch, mem):
+def test_host_pipeline_matches_device_path(torch_cuda, monkeypatch, mem, sizes):
     """dk_rx_process_host gives the oracle's results from pageable memory (staged copies), from pinned memory with
-    staging forced (DK_RX_HOST_ZC=0), and from pinned, GPU-mapped memory read in place (the default there)."""
+    staging forced (DK_RX_HOST_ZC=0), and from pinned, GPU-mapped memory read in place (the default there); IMIX
+    sizes (staged kernel) and 64-byte frames (small-frame kernel with its deferred general pass, per chunk)."""
     import torch
 
     from demikernel_amd import RxResults
 
     flows = synth.make_flows(256)
     n = 50000
-    tr = synth.traffic(n, synth.imix_ip_lengths(n), flows)
+    ipl = synth.imix_ip_lengths(n) if sizes == "imix" else np.full(n, 46, np.int64)
+    tr = synth.traffic(n, ipl, flows)
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr))
     exp = run_oracle(blob, off, lens, flows)
