@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 
 #include "../../include/dk_tcp.h"
@@ -79,10 +80,14 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_key_kernel(Params P) {
     if ((meta & 0xFFu) == DK_V_OK_TCP) {
         const uint32_t f = P.flow_id[i];
         if (f < P.nconns) {
-            const dk_tcp_conn& t = P.conns[f];
-            const uint32_t state = t.state;
+            // state, receive_next, reader_next, buffer_size: the first 16 bytes of dk_tcp_conn, one load
+            static_assert(offsetof(dk_tcp_conn, state) == 0 && offsetof(dk_tcp_conn, receive_next) == 4 &&
+                              offsetof(dk_tcp_conn, reader_next) == 8 && offsetof(dk_tcp_conn, buffer_size) == 12,
+                          "dk_tcp_conn layout");
+            const uint4 h = *reinterpret_cast<const uint4*>(P.conns + f);
+            const uint32_t state = h.x;
             if (state != DK_TCP_NONE) key = 2 * f;
-            const uint32_t bufsz = t.buffer_size, rn0 = t.receive_next, wend = t.reader_next + bufsz;
+            const uint32_t bufsz = h.w, rn0 = h.y, wend = h.z + bufsz;
             // order-independent outcomes (see the top of the file); the bounds keep (seq - RCV.NXT) and
             // (seg_end - RCV.NXT) of every RCV.NXT in [rn0, wend] on one side of the wrap
             if (state == DK_TCP_ESTABLISHED && wend - rn0 <= bufsz && bufsz < 0x40000000u) {
@@ -678,6 +683,7 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     if (n && (!rx->meta || !rx->flow_id || !rx->payload || !rx->tcp_seq || !rx->tcp_ack || !out->action || !out->view))
         return EINVAL;
     if (nconns && (!conns || !out->deliv || !out->deliv_start || !out->deliv_count)) return EINVAL;
+    if (reinterpret_cast<uintptr_t>(conns) & 15) return EINVAL;  // the key kernel reads each entry's head as 16 bytes
     if (n > 0x7FFFFFFFu || nconns > 0x7FFFFFFFu ||
         (uint64_t)n + (uint64_t)DK_TCP_DELIV_EXTRA * nconns > 0xFFFFFFFFull)
         return EINVAL;

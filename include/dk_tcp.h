@@ -106,7 +106,8 @@ void dk_tcp_ctx_destroy(dk_tcp_ctx* ctx);
 
 /* Run the TCP segments of one dk_rx_process batch through their connections: rx = that call's device results (meta,
  * flow_id, payload, tcp_seq and tcp_ack are required), conns[0 .. nconns) = the connections by flow_id (device,
- * updated in place). Asynchronous on `stream`. Returns 0, EINVAL or ENOMEM. */
+ * 16-byte aligned as hipMalloc returns it, updated in place). Asynchronous on `stream`. Returns 0, EINVAL (also for a
+ * misaligned conns) or ENOMEM. */
 int dk_tcp_rx_process(dk_tcp_ctx* ctx, const dk_rx_results* rx, uint32_t n, dk_tcp_conn* conns, uint32_t nconns,
                       const dk_tcp_out* out, void* stream);
 
