@@ -67,6 +67,7 @@ struct Stage {  // device staging for one pipeline stream
 // the launch path.
 struct Tuning {
     int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
+    int32_t lds_table = -1;  // 0: Active lookups never use the LDS table (DK_RX_LDS_TABLE)
     int32_t host_zc = -1;  // dk_rx_process_host: read mapped pinned frames in place (-1/1 when mapped, 0 never)
 };
 
@@ -74,8 +75,11 @@ struct Tuning {
 
 struct dk_rx_ctx {
     dk_rx_cfg cfg{};
-    uint32_t* table = nullptr;  // device: (mask + 1) * 4 u32 of Active slots, then the kPortTabWords port table
+    uint32_t* table = nullptr;  // device: (mask + 1) * 4 u32 of Active slots, the kPortTabWords port table, then the
+                                // LDS Active table's lt_words (rx_common.h; 0 when it was not built)
     uint32_t table_mask = 0;
+    uint32_t lt_n = 0, lt_b = 0, lt_words = 0;
+    uint32_t lt_occ_dyn = ~0u, lt_occ_family = ~0u, lt_occ_blocks = 0;  // occupancy cache with the LDS table
     uint32_t nflows = 0;
     // host pipeline state (lazily allocated)
     Stage stages[kPipeStreams];
@@ -117,6 +121,68 @@ int32_t env_knob(const char* name) {
     return e ? (int32_t)atoi(e) : -1;
 }
 
+// The LDS Active table (rx_common.h): a minimal perfect hash of the Active connections with local_ip == cfg_ip, taken
+// from the built open-addressing slots (so duplicates resolve exactly as there). Buckets are placed largest first,
+// each with the smallest displacement that puts all its keys on free slots. Returns false (no LDS table: lookups probe
+// the global table) for no keys, too many, or keys whose 32-bit hashes collide (never separable).
+bool build_lds_table(const std::vector<uint32_t>& slots, uint32_t cap, uint32_t cfg_ip, std::vector<uint32_t>& out,
+                     uint32_t& n_out, uint32_t& b_out) {
+    struct Key {
+        uint32_t h, rip, ports, fid;
+    };
+    std::vector<Key> keys;
+    for (uint32_t i = 0; i < cap; i++) {
+        const uint32_t* sl = &slots[(size_t)i * 4];
+        if (sl[0] == 0 || (sl[0] >> 24) != DK_FLOW_TCP_ACTIVE || sl[1] != cfg_ip) continue;
+        if (keys.size() >= dk::kLtMaxKeys) return false;
+        keys.push_back({dk::flow_hash(DK_FLOW_TCP_ACTIVE, cfg_ip, sl[2], sl[3]), sl[2], sl[3], sl[0] & 0xFFFFFFu});
+    }
+    const uint32_t n = (uint32_t)keys.size();
+    if (n == 0) return false;
+    const uint32_t nb = (n + 3) / 4;
+    std::vector<std::vector<uint32_t>> bucket(nb);
+    for (uint32_t k = 0; k < n; k++) bucket[dk::lt_bucket(keys[k].h, nb)].push_back(k);
+    std::vector<uint32_t> order(nb);
+    for (uint32_t b = 0; b < nb; b++) order[b] = b;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return bucket[a].size() > bucket[b].size(); });
+    std::vector<uint8_t> taken(n, 0);
+    std::vector<uint32_t> disp(nb, 0), slot_of(n, 0), at;
+    for (uint32_t b : order) {
+        if (bucket[b].empty()) break;
+        uint32_t d = 0;
+        for (;; d++) {
+            if (d >= (1u << 20)) return false;
+            at.clear();
+            bool ok = true;
+            for (uint32_t k : bucket[b]) {
+                const uint32_t sl = dk::lt_slot(keys[k].h, d, n);
+                if (taken[sl] || std::find(at.begin(), at.end(), sl) != at.end()) {
+                    ok = false;
+                    break;
+                }
+                at.push_back(sl);
+            }
+            if (ok) break;
+        }
+        disp[b] = d;
+        for (size_t j = 0; j < at.size(); j++) {
+            taken[at[j]] = 1;
+            slot_of[bucket[b][j]] = at[j];
+        }
+    }
+    out.assign(dk::lt_words(n, nb), 0u);
+    for (uint32_t k = 0; k < n; k++) {
+        out[slot_of[k]] = keys[k].rip;
+        out[n + slot_of[k]] = keys[k].ports;
+        out[2 * n + slot_of[k]] = keys[k].fid;
+    }
+    std::copy(disp.begin(), disp.end(), out.begin() + 3 * n);
+    n_out = n;
+    b_out = nb;
+    return true;
+}
+
 int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask) {
     uint32_t* d = nullptr;
     if (hipMalloc(&d, slots.size() * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
@@ -127,6 +193,8 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
     if (c->table) (void)hipFree(c->table);
     c->table = d;
     c->table_mask = mask;
+    c->lt_n = c->lt_b = c->lt_words = 0;
+    c->lt_occ_family = ~0u;
     return 0;
 }
 
@@ -279,7 +347,24 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
         c->occ_dyn = dyn;
         c->occ_family = family;
     }
-    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u);
+    const uint32_t fam_cap = p.small ? 8u : p.split ? 1u : p.stage ? 3u : 4u;
+    uint32_t per_cu = std::min<uint32_t>(c->occ_blocks, fam_cap);
+    // The LDS Active table (not the small-frame kernel: its five workgroups per CU have no LDS to spare, and its
+    // batches are UDP-bound) when it costs no occupancy.
+    if (c->lt_words && !p.small && T.lds_table != 0) {
+        const uint32_t off = (dyn / 4 + 3) & ~3u;
+        const uint32_t dyn2 = (off + c->lt_words) * 4;
+        if (c->lt_occ_dyn != dyn2 || c->lt_occ_family != family) {
+            c->lt_occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn2, family), 0);
+            c->lt_occ_dyn = dyn2;
+            c->lt_occ_family = family;
+        }
+        if (std::min(c->lt_occ_blocks, fam_cap) >= per_cu) {
+            p.lt_words = c->lt_words;
+            p.lt_off = off;
+            dyn = dyn2;
+        }
+    }
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
     const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
@@ -312,9 +397,9 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     }
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
-                        "small=%u fused=%u\n",
+                        "small=%u fused=%u lds_table=%u\n",
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
-                p.small, p.fused);
+                p.small, p.fused, p.lt_words ? p.lt_n : 0u);
     rc = dk_launch_rx(p, grid, stream);
     if (rc == 0 && slot && (DK_SLOT_EVENTS || c->saturated)) {
         if (hipEventRecord(slot->last, stream) != hipSuccess) return EIO;
@@ -381,6 +466,10 @@ dk::RxParams base_params(const dk_rx_ctx* c) {
     p.table = c->table;
     p.table_mask = c->table_mask;
     p.port_tab = c->table + (size_t)(c->table_mask + 1) * 4;
+    p.lt = p.port_tab + dk::kPortTabWords;
+    p.lt_words = p.lt_off = 0;
+    p.lt_n = c->lt_n;
+    p.lt_b = c->lt_b;
     p.nflows = c->nflows;
     return p;
 }
@@ -418,6 +507,7 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     t.grid_per_cu = env_knob("DK_RX_GRID_PER_CU");
     t.debug = env_knob("DK_RX_DEBUG");
     t.host_zc = env_knob("DK_RX_HOST_ZC");
+    t.lds_table = env_knob("DK_RX_LDS_TABLE");
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
     std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
@@ -491,9 +581,22 @@ int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
             h = (h + 1) & mask;
         }
     }
+    uint32_t lt_n = 0, lt_b = 0, lt_w = 0;
+    {
+        std::vector<uint32_t> lt;
+        if (build_lds_table(slots, cap, cfg_ip, lt, lt_n, lt_b)) {
+            lt_w = (uint32_t)lt.size();
+            slots.insert(slots.end(), lt.begin(), lt.end());
+        }
+    }
     DeviceGuard g(c->cfg.device);
     int rc = upload_table(c, slots, mask);
-    if (rc == 0) c->nflows = n;
+    if (rc == 0) {
+        c->nflows = n;
+        c->lt_n = lt_n;
+        c->lt_b = lt_b;
+        c->lt_words = lt_w;
+    }
     return rc;
 }
 
@@ -711,8 +814,19 @@ int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
 int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t knobs[DK_DIAG_RX_KNOBS]) {
     if (!c || !knobs) return EINVAL;
     const int32_t zc = c->tune.host_zc;  // not a diag knob: kept from DK_RX_HOST_ZC
-    c->tune = Tuning{knobs[0], knobs[1], knobs[2], knobs[3], knobs[4], knobs[5], knobs[6], zc};
+    Tuning t;
+    t.stage = knobs[0];
+    t.split = knobs[1];
+    t.small = knobs[2];
+    t.sched = knobs[3];
+    t.grid = knobs[4];
+    t.grid_per_cu = knobs[5];
+    t.debug = knobs[6];
+    t.lds_table = knobs[7];
+    t.host_zc = zc;
+    c->tune = t;
     c->occ_family = ~0u;
+    c->lt_occ_family = ~0u;
     return 0;
 }
 

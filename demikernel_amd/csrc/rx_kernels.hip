@@ -387,6 +387,26 @@ __device__ __forceinline__ uint32_t port_lookup(const RxParams& P, uint32_t base
     return P.port_tab[base + port];
 }
 
+// The LDS Active table (rx_common.h): copied from global memory at the kernel start (before the workgroup's first
+// barrier), then a lookup is two dependent LDS reads and a key compare. Returns the slot the global probe would have
+// hit first ({kind << 24 | flow_id, local_ip, remote_ip, ports}), or zeros (an empty slot: probe_finish stops there,
+// and the Passive lookup follows as it would after a miss in the global table).
+extern __shared__ __attribute__((aligned(16))) uint32_t dk_dyn_lds[];
+__device__ __forceinline__ void lt_load(const RxParams& P, uint32_t tid, uint32_t nthreads) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.lt);
+    uint4* dst = reinterpret_cast<uint4*>(dk_dyn_lds + P.lt_off);
+    for (uint32_t k = tid; k < P.lt_words / 4; k += nthreads) dst[k] = src[k];
+}
+__device__ __forceinline__ uint4 lt_lookup(const RxParams& P, uint32_t rip, uint32_t ports) {
+    const uint32_t* T = dk_dyn_lds + P.lt_off;
+    const uint32_t h = flow_hash(DK_FLOW_TCP_ACTIVE, P.local_ip, rip, ports);
+    const uint32_t n = P.lt_n;
+    const uint32_t sl = lt_slot(h, T[3 * n + lt_bucket(h, P.lt_b)], n);
+    const uint32_t kr = T[sl], kp = T[n + sl], fid = T[2 * n + sl];
+    return kr == rip && kp == ports ? make_uint4(DK_FLOW_TCP_ACTIVE << 24 | fid, P.local_ip, rip, ports)
+                                    : make_uint4(0, 0, 0, 0);
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // One frame per lane, 256 frames per workgroup tile: phases A, B, C and the result stores. Every lane of the
@@ -834,14 +854,20 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     St.k1 = k1;
     St.s1 = make_uint4(0, 0, 0, 0);
     uint32_t h1 = 0;
-    if (L.v == kPendTcp) {  // the hash only for TCP lanes (a wave of UDP frames skips it)
+    if (L.v == kPendTcp && P.lt_words) {  // the LDS table: no global load
+        St.s1 = lt_lookup(P, k1.rip, k1.lport_rport);
+    } else if (L.v == kPendTcp) {  // the hash only for TCP lanes (a wave of UDP frames skips it)
         h1 = probe_slot(P, k1);
 #ifndef DK_ABL_NOPROBE
         St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+#else  // ablation (tuning only): a first-slot hit without the load
+        St.s1 = make_uint4(k1.kind << 24 | (h1 & 1023u), k1.lip, k1.rip, k1.lport_rport);
 #endif
     }
 #ifndef DK_ABL_NOPROBE
     if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+#else
+    if (L.v == kPendUdp) St.s1.x = (L.ports >> 16) & 1023u;
 #endif
     St.h1 = h1;
 #ifdef DK_ABL_FASTONLY
@@ -894,7 +920,9 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
         const uint32_t dport = L.ports >> 16;
         if (L.v == kPendTcp) {
             // SocketId::Active(local=(local_ip, dport), remote=(src, sport)), then Passive(local) (tcp/peer.rs:241-251)
-            fid = probe_finish(P, k1, h1, s1);  // Active(local, remote)
+            // Active(local, remote): the LDS table's answer is exact (a hit or an empty slot), the global table's
+            // first slot may need the rest of the probe walk
+            fid = P.lt_words ? (s1.x ? s1.x & 0xFFFFFFu : DK_FLOW_NONE) : probe_finish(P, k1, h1, s1);
             if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortTcpPassive, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
         } else if (L.v == kPendUdp) {
@@ -1212,6 +1240,7 @@ void dk_rx_kernel(RxParams P) {
     for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
+    lt_load(P, tid, kBlock);
     __syncthreads();
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
@@ -1730,6 +1759,7 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
         (&s_ready[0][0])[tid] = 0;
         (&s_free[0][0])[tid] = 0;
     }
+    lt_load(P, tid, S::kThreads);
     __syncthreads();
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
@@ -2103,7 +2133,8 @@ uint32_t dk_rx_small_block_waves() { return dk::kSmallWaves; }
 
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
-    const size_t dyn = p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
+    const size_t dyn = p.lt_words ? (size_t)(p.lt_off + p.lt_words) * 4
+                       : p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
     if (p.small && p.aligned16 && opt)

@@ -126,6 +126,44 @@ def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
     assert ("dst_ip" in got) == (sched != "1")
 
 
+@pytest.mark.parametrize("sizes", ["imix", "1500"])
+@pytest.mark.parametrize("nact", [1, 7, 1024, 2600, 4096, 5000])
+def test_lds_active_table(torch_cuda, monkeypatch, capfd, nact, sizes):
+    """The LDS copy of the Active table (rx_common.h: minimal perfect hash, staged and split kernels) against the
+    oracle, and against the global table (DK_RX_LDS_TABLE=0): 20 % of the TCP segments come from remote endpoints that
+    are not in the table (they land on another key's slot and must fail its compare, then take the Passive listener),
+    plus a duplicated Active key (the last one wins) and Active entries on another local address (never found). 5,000
+    keys exceed kLtMaxKeys (global table only); the debug line says which path ran."""
+    flows = synth.make_flows(nact)
+    dup = flows[: min(nact, 3)].copy()
+    other = flows[: min(nact, 5)].copy()
+    other["local_ip"] = ipv4("192.168.1.77")
+    flows = np.concatenate([flows, dup, other, synth.make_flows(8, kind="udp")])
+    n = 30000
+    ip_len = synth.imix_ip_lengths(n, seed=21) if sizes == "imix" else 1486
+    tr = synth.traffic(n, ip_len, flows, seed=22)
+    rng = np.random.default_rng(23)
+    stray = (tr.proto == 6) & (rng.random(n) < 0.2)
+    tr.src_ip[stray] = (10 | 200 << 8 | rng.integers(0, 256, int(stray.sum()), dtype=np.uint32) << 16
+                        | (rng.integers(0, 255, int(stray.sum()), dtype=np.uint32) + 1) << 24)
+    tr.sport[stray] = rng.integers(1024, 65535, int(stray.sum()), dtype=np.uint16)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr))
+    exp = run_oracle(blob, off, lens, flows)
+    monkeypatch.setenv("DK_RX_DEBUG", "1")
+    for lt in ("-1", "0"):
+        monkeypatch.setenv("DK_RX_LDS_TABLE", lt)
+        got = run_gpu(blob, off, lens, flows)
+        assert_same(got, exp, f"nact={nact} {sizes} lds_table={lt}")
+        used = [int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("lds_table=")]
+        assert used, "no debug line"
+        # the staged kernel (IMIX, 3 workgroups per CU) has LDS for ~1,800 keys, the split kernel (1 per CU) for all
+        fits = nact <= (1024 if sizes == "imix" else 4096)
+        want = nact if (lt == "-1" and fits) else 0
+        assert used == [want] * len(used), (nact, sizes, lt, used)
+    assert (got["meta"] & 0xFF == V["OK_TCP"]).sum() > (tr.proto == 6).sum() // 2
+
+
 def test_misaligned_and_offsets(torch_cuda):
     """Frames at every offset mod 16 (fast path only at 0 mod 16) and in shuffled, gapped order."""
     flows = synth.make_flows(64)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--knob", default="", help="NAME=v1,v2,...: interleave values of one more env knob (e.g. DK_RX_SPLIT=0,1)")
     ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
     ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
+    ap.add_argument("--check", action="store_true", help="also compare every variant's results and counters with the "
+                                                          "first variant's on one fresh launch")
     args = ap.parse_args()
     import torch
 
@@ -76,6 +78,21 @@ def main():
                 ev1.record()
                 torch.cuda.synchronize()
                 times[(k, g, cf)].append(ev0.elapsed_time(ev1) / args.iters)
+    if args.check and not args.tx:
+        ref = None
+        for k, (e, _) in engines.items():
+            os.environ.pop("DK_RX_GRID_PER_CU", None)
+            r = e.results(batch.n)
+            e.receive_batch(batch, r)
+            torch.cuda.synchronize()
+            got = r.to_numpy()
+            if ref is None:
+                ref = (k, got)
+                continue
+            bad = [f for f in got if not np.array_equal(np.asarray(got[f]), np.asarray(ref[1][f]))]
+            print(json.dumps({"check": k, "vs": ref[0], "mismatched": bad}), flush=True)
+            if bad:
+                sys.exit(5)
     for (k, g, cf), ts in sorted(times.items(), key=lambda x: (x[0][1], str(x[0][2]), x[0][0])):
         ms = float(np.median(ts))
         name = k if cf[1] is None else f"{k}[{kname}={cf[1]}]"
