@@ -4,6 +4,7 @@ planner (rx_plan.h), built into a standalone driver (tests/host_asan). Valid, co
 sanitizer report aborts the driver (-fno-sanitize-recover), and its outputs must equal the regular libdk_rx.so's on
 the same inputs (the reference's host side is catpowder/linux/mod.rs:138-159 and runtime/memory/mod.rs:38-54)."""
 import ctypes
+import fcntl
 import os
 import subprocess
 
@@ -22,7 +23,11 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_err
 
 @pytest.fixture(scope="module")
 def driver():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "host_asan")], check=True)
+    # one build at a time: pytest-xdist workers would otherwise race on the same output file
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".host_asan.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "host_asan")], check=True)
     return EXE
 
 
