@@ -100,6 +100,20 @@ constexpr uint32_t kCountGroup = DK_COUNT_GROUP;
 #endif
 constexpr uint32_t kSuperGroup = DK_SUPER_GROUP;
 constexpr uint32_t kRowAlignWords = 32;
+// How a launch's per-workgroup counter rows reach the caller's u64 counters (RxParams::fused):
+//   kCombineReduce   plain row stores, then dk_flow_reduce_kernel (a second launch);
+//   kCombineTree     the two-level ticket tree above, inside the launch;
+//   kCombineReplica  inside the launch, through replica rows: each workgroup adds its nonzero row words to the replica
+//                    row of its run of rep_wgs consecutive workgroups with no-return u32 atomics (they execute at the
+//                    memory side: nothing is re-read, MI355X_MICROARCH.md "Global atomics"), drains, and takes a ticket
+//                    of that replica; the replica's last arriver swaps the row back to zero (returning atomics) and adds
+//                    it to the caller's counters, one u64 atomic per counter per replica. Packed u16 flow pairs stay
+//                    packed in the replica, so the host bounds a replica's frames below 65536.
+constexpr uint32_t kCombineReduce = 0, kCombineTree = 1, kCombineReplica = 2;
+#ifndef DK_REPLICA_WGS
+#define DK_REPLICA_WGS 16
+#endif
+constexpr uint32_t kReplicaWgs = DK_REPLICA_WGS;
 // Tickets of a launch of `grid` workgroups: one per group, then one per supergroup, each on a 128-byte line of its own
 // (kTicketStride words): device-scope atomics to one line serialise at ~12 ns each (MI355X_MICROARCH.md, fanin), so
 // tickets sharing lines made every group's arrivals queue behind every other group's (C3: 1,280 adds on 3 lines).
@@ -139,7 +153,9 @@ struct RxParams {
     uint32_t* tickets;       // [count_tickets(grid)] arrival tickets, 0 between launches (the last arrivers reset them)
     uint32_t* group_rows;    // [groups][group_stride]: level-1 sums (u32 per flow, then per verdict)
     uint32_t group_stride;   // 2 * flow_words + DK_V_COUNT rounded up to kRowAlignWords
-    uint32_t fused;          // 1: rows combined in-launch (flush_counters); 0: plain rows + dk_flow_reduce_kernel
+    uint32_t fused;          // kCombine*: how the rows reach the caller's counters
+    uint32_t* reps;          // kCombineReplica: [ceil(grid / rep_wgs)][row_stride] u32 replica rows, zero between launches
+    uint32_t rep_wgs;        // kCombineReplica: workgroups per replica row (consecutive blockIdx)
     uint64_t* defer;         // small-frame kernel: [ceil(n / 64)] masks of the frames each 64-frame chunk left to the
                              // general path after its main loop
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)

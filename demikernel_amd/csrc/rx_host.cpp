@@ -35,6 +35,8 @@ struct CountScratch {
     uint32_t ntickets = 0;
     uint64_t* defer = nullptr;  // the small-frame kernel's per-chunk deferral masks
     size_t ndefer = 0;
+    uint32_t* reps = nullptr;  // kCombineReplica rows: zeroed at allocation, each launch's last arrivers re-zero theirs
+    size_t reps_words = 0;
 };
 
 // A context's scratch is keyed by stream: calls on different streams never share counter rows or tickets, so their
@@ -68,6 +70,7 @@ struct Stage {  // device staging for one pipeline stream
 struct Tuning {
     int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
     int32_t lds_table = -1;  // 0: Active lookups never use the LDS table (DK_RX_LDS_TABLE)
+    int32_t combine = -1;    // dk::kCombine* (DK_RX_COMBINE)
     int32_t host_zc = -1;  // dk_rx_process_host: read mapped pinned frames in place (-1/1 when mapped, 0 never)
 };
 
@@ -202,6 +205,7 @@ void free_slot(StreamSlot& s) {  // the caller has waited for the slot's launche
     if (s.cs.rows) (void)hipFree(s.cs.rows);
     if (s.cs.tickets) (void)hipFree(s.cs.tickets);
     if (s.cs.defer) (void)hipFree(s.cs.defer);
+    if (s.cs.reps) (void)hipFree(s.cs.reps);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
 }
@@ -262,12 +266,14 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
 
 // Rows for `grid` workgroups, their group rows and tickets, and `ndefer` deferral masks. Growing waits for the slot's
 // last launch before freeing.
-int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t group_stride, size_t ndefer) {
+int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t group_stride, size_t ndefer,
+                  uint32_t nreps) {
     CountScratch& cs = s.cs;
     const size_t ngroups = (grid + dk::kCountGroup - 1) / dk::kCountGroup;
     const size_t words = row_stride ? (size_t)grid * row_stride + ngroups * group_stride : 0;
-    const uint32_t nt = row_stride ? dk::count_tickets(grid) : 0;
-    if (cs.rows_words >= words && cs.ntickets >= nt && cs.ndefer >= ndefer) return 0;
+    const uint32_t nt = row_stride ? std::max(dk::count_tickets(grid), nreps * dk::kTicketStride) : 0;
+    const size_t rwords = (size_t)nreps * row_stride;
+    if (cs.rows_words >= words && cs.ntickets >= nt && cs.ndefer >= ndefer && cs.reps_words >= rwords) return 0;
     if (hipStreamSynchronize(s.stream) != hipSuccess) return EIO;  // launches still using the old buffers
     if (cs.rows_words < words) {
         if (cs.rows) (void)hipFree(cs.rows);
@@ -283,6 +289,14 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t gr
         if (hipMalloc(&cs.tickets, nt * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
         if (hipMemset(cs.tickets, 0, nt * sizeof(uint32_t)) != hipSuccess) return EIO;
         cs.ntickets = nt;
+    }
+    if (cs.reps_words < rwords) {
+        if (cs.reps) (void)hipFree(cs.reps);
+        cs.reps = nullptr;
+        cs.reps_words = 0;
+        if (hipMalloc(&cs.reps, rwords * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+        if (hipMemset(cs.reps, 0, rwords * sizeof(uint32_t)) != hipSuccess) return EIO;
+        cs.reps_words = rwords;
     }
     if (cs.ndefer < ndefer) {
         if (cs.defer) (void)hipFree(cs.defer);
@@ -309,7 +323,9 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.tickets = nullptr;
     p.group_rows = nullptr;
     p.group_stride = 0;
-    p.fused = 0;
+    p.fused = dk::kCombineReduce;
+    p.reps = nullptr;
+    p.rep_wgs = 0;
     p.defer = nullptr;
     uint32_t dyn = 0;
     if (p.res.flow_counts && c->nflows) {
@@ -381,17 +397,29 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * dk_rx_small_block_waves() : 0;
     if (p.row_words || ndefer) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
+        uint32_t nreps = 0;
         if (p.row_words) {
             p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
             p.group_stride = (2 * p.flow_words + DK_V_COUNT + dk::kRowAlignWords - 1) / dk::kRowAlignWords *
                              dk::kRowAlignWords;
+            p.fused = grid <= dk::kFusedMaxGrid ? dk::kCombineTree : dk::kCombineReduce;
+            if (T.combine >= 0) p.fused = (uint32_t)std::min(T.combine, 2);
+            if (p.fused == dk::kCombineReplica) {
+                // a replica's packed u16 flow halves must not carry: frames per replica < 65536 (a workgroup takes at
+                // most ceil(tiles / grid) + 1 tiles of 256 frames under either schedule)
+                const uint32_t per_wg = ((ntiles + grid - 1) / grid + 1) * 256u;
+                p.rep_wgs = std::max(1u, std::min(dk::kReplicaWgs, 65535u / per_wg));
+                if (p.flow_mode != dk::kFlowLds) p.rep_wgs = dk::kReplicaWgs;
+                if (p.flow_mode == dk::kFlowLds && per_wg > 65535u) p.fused = dk::kCombineReduce;
+                else nreps = (grid + p.rep_wgs - 1) / p.rep_wgs;
+            }
         }
-        if ((rc = ensure_counts(*slot, grid, p.row_stride, p.group_stride, ndefer))) return rc;
+        if ((rc = ensure_counts(*slot, grid, p.row_stride, p.group_stride, ndefer, nreps))) return rc;
         if (p.row_words) {
             p.flow_scratch = slot->cs.rows;
             p.group_rows = slot->cs.rows + (size_t)grid * p.row_stride;
             p.tickets = slot->cs.tickets;
-            p.fused = grid <= dk::kFusedMaxGrid ? 1u : 0u;
+            p.reps = slot->cs.reps;
         }
         p.defer = slot->cs.defer;
     }
@@ -508,6 +536,7 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     t.debug = env_knob("DK_RX_DEBUG");
     t.host_zc = env_knob("DK_RX_HOST_ZC");
     t.lds_table = env_knob("DK_RX_LDS_TABLE");
+    t.combine = env_knob("DK_RX_COMBINE");
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
     std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
@@ -823,6 +852,7 @@ int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t knobs[DK_DIAG_RX_KNOBS]) {
     t.grid_per_cu = knobs[5];
     t.debug = knobs[6];
     t.lds_table = knobs[7];
+    t.combine = knobs[8];
     t.host_zc = zc;
     c->tune = t;
     c->occ_family = ~0u;

@@ -1139,14 +1139,48 @@ __device__ __forceinline__ bool arrive_last(uint32_t* ticket, uint32_t count, ui
 __device__ __forceinline__ void add_u64(uint64_t* p, uint64_t v) {
     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
 }
+// kCombineReplica (rx_common.h): the workgroup's nonzero histogram words go to its replica row by no-return atomic adds,
+// which the drain in arrive_last waits for (vmcnt counts them); the replica's last arriver swaps each word back to zero
+// with a returning atomic (read at the memory side, where the adds were performed: no stale L2 copy can be seen) and adds
+// it to the caller's counters.
+__device__ __forceinline__ void flush_replica(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
+                                              const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
+    const uint32_t r = blockIdx.x / P.rep_wgs;
+    const uint32_t rn = min(P.rep_wgs, gridDim.x - r * P.rep_wgs);
+    uint32_t* rep = P.reps + (size_t)r * P.row_stride;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += nthreads) {
+            const uint32_t x = s_flow[k];
+            if (x) __hip_atomic_fetch_add((gu32*)(rep + k), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
+        __hip_atomic_fetch_add((gu32*)(rep + P.flow_words + tid), s_vh[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!arrive_last(P.tickets + r * kTicketStride, rn, tid, s_last)) return;
+    for (uint32_t w = tid; w < P.row_words; w += nthreads) {
+        const bool flow = w < P.flow_words;
+        if (flow ? !lds_flows : w - P.flow_words >= DK_V_COUNT) continue;
+        const uint32_t x = __hip_atomic_exchange((gu32*)(rep + w), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!flow) {
+            add_u64(P.res.verdict_counts + (w - P.flow_words), x);
+        } else {
+            add_u64(P.res.flow_counts + 2 * w, x & 0xFFFFu);
+            if (2 * w + 1 < P.nflows) add_u64(P.res.flow_counts + 2 * w + 1, x >> 16);
+        }
+    }
+    if (tid == 0) __hip_atomic_store((gu32*)(P.tickets + r * kTicketStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
                                                const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
     if (!P.row_words) return;
 #ifdef DK_ABL_NOFLUSH  // ablation (tuning only): counters never leave LDS, no combine
     return;
 #endif
+    if (P.fused == kCombineReplica) {
+        flush_replica(P, tid, nthreads, lds_flows, s_flow, s_vh, s_last);
+        return;
+    }
     uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_stride;
-    if (!P.fused) {  // rows with plain stores; dk_flow_reduce_kernel (a second launch) adds them up
+    if (P.fused == kCombineReduce) {  // rows with plain stores; dk_flow_reduce_kernel (a second launch) adds them up
         if (lds_flows)
             for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
         if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
@@ -1475,7 +1509,11 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
         h1 = probe_slot(P, k1);
         s1 = reinterpret_cast<const uint4*>(P.table)[h1];
     }
+#ifdef DK_ABL_NOPROBE  // ablation (tuning only, flows wrong): no table load
+    if (L.v == kPendUdp) s1.x = (L.ports >> 16) & 1023u;
+#else
     if (L.v == kPendUdp) s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+#endif
     uint32_t lsum = 0;
     if (L.need) {  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
         if (!__ballot(L.E != 64u)) {
@@ -2161,7 +2199,7 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
 #ifdef DK_ABL_NOFLUSH
     if (false) {
 #else
-    if (p.row_words && !p.fused) {
+    if (p.row_words && p.fused == dk::kCombineReduce) {
 #endif
         const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
                       (grid + dk::kReduceRows - 1) / dk::kReduceRows);

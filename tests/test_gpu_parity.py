@@ -791,6 +791,47 @@ def test_flow_counter_modes_and_wrap_guard(torch_cuda, monkeypatch):
     assert int(got["flow_counts"][0]) == n and int(got["verdict_counts"][0]) == n
 
 
+@pytest.mark.parametrize("combine", ["0", "1", "2"])
+@pytest.mark.parametrize("family", ["staged", "split", "small"])
+def test_counter_combine_modes(torch_cuda, monkeypatch, family, combine):
+    """Every way the per-workgroup counter rows reach the caller's u64 counters (dk_diag.h combine: a second reduce
+    kernel, the in-launch ticket tree, in-launch replica rows), per kernel family, on grids of 7 workgroups, the default
+    and 1,500 (above the tree's 1,024): three launches on one context accumulate exactly 3x the oracle's counts (the
+    replica rows and tickets are back to zero after each launch); also with > 32,768 flows (verdict rows only) and with
+    a grid whose replicas must shrink to keep their packed u16 halves below 65,536."""
+    import torch
+
+    monkeypatch.setenv("DK_RX_COMBINE", combine)
+    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
+    monkeypatch.setenv("DK_RX_STAGE", "1")
+    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
+    cases = [(20000, 700, None), (20000, 700, "7"), (400000, 700, "1500"), (9000, 40000, None), (300000, 1, "20")]
+    for n, nflows, grid in cases:
+        if grid is None:
+            monkeypatch.delenv("DK_RX_GRID", raising=False)
+        else:
+            monkeypatch.setenv("DK_RX_GRID", grid)
+        flows = np.concatenate([synth.make_flows(nflows, passive=False), synth.make_flows(8, kind="udp")])
+        ip_len = 50 if family == "small" else synth.imix_ip_lengths(n, seed=n)
+        tr = synth.traffic(n, ip_len, flows, seed=nflows)
+        blob, off, lens = synth.build_numpy(tr)
+        synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
+        eng = RxEngine(Config(LOCAL), device=0)
+        eng.set_sockets(flows)
+        b = FrameBatch.from_numpy(blob, off, lens, device=0)
+        r = eng.results(n)
+        for _ in range(3):
+            eng.receive_batch(b, r)
+        torch.cuda.synchronize()
+        got = r.to_numpy()
+        eng.close()
+        exp = run_oracle(blob, off, lens, flows)
+        ctx = f"{family} combine={combine} n={n} flows={nflows} grid={grid}"
+        assert np.array_equal(got["flow_counts"], 3 * exp["flow_counts"][: len(got["flow_counts"])]), ctx
+        assert np.array_equal(got["verdict_counts"], 3 * exp["verdict_counts"]), ctx
+        assert np.array_equal(got["meta"], exp["meta"]) and np.array_equal(got["flow_id"], exp["flow_id"]), ctx
+
+
 @pytest.mark.parametrize("mix", ["tcp1500", "udp64", "imix"])
 def test_aligned_traffic_stays_on_vector_path(torch_cuda, mix):
     """Performance guard (dk_diag path counters): well-formed 64-byte-slot traffic never falls back to the byte-load
