@@ -79,52 +79,7 @@ constexpr uint32_t kFlowGlobal = 2;  // per-frame u64 global atomics (tables too
 constexpr uint32_t kMaxLdsFlowWords = 16384;  // 64 KiB of LDS -> up to 32768 flows on the LDS path
 constexpr uint32_t kVerdictWords = (DK_V_COUNT + 3) & ~3u;  // verdict histogram columns of a scratch row
 constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
-// Counter rows are combined inside the launch (flush_counters, rx_kernels.hip) by a two-level tree: workgroups are
-// grouped kCountGroup at a time, each group has one arrival ticket, and the group's last arriver sums the group's rows
-// into a group row; groups are grouped kSuperGroup at a time, and the last group winner of each supergroup adds the
-// supergroup's sums to the caller's u64 counters (ceil(groups / kSuperGroup) same-address atomics per counter). Rows
-// are padded to whole 128-byte lines. Grids above kFusedMaxGrid (the small-frame kernel's 1,280 workgroups) store
-// plain rows and sum them in a second kernel (dk_flow_reduce_kernel): measured 27.1 us per C3 batch against 31.4 with
-// the two-level in-launch tree and 30.7 with one level — at that grid every workgroup's exit drain and
-// ticket round trip, all at once at the end of a uniform batch, cost more than one kernel boundary.
-#ifndef DK_FUSED_MAX_GRID
-#define DK_FUSED_MAX_GRID 1024
-#endif
-constexpr uint32_t kFusedMaxGrid = DK_FUSED_MAX_GRID;
-#ifndef DK_COUNT_GROUP
-#define DK_COUNT_GROUP 16
-#endif
-constexpr uint32_t kCountGroup = DK_COUNT_GROUP;
-#ifndef DK_SUPER_GROUP
-#define DK_SUPER_GROUP 8
-#endif
-constexpr uint32_t kSuperGroup = DK_SUPER_GROUP;
-constexpr uint32_t kRowAlignWords = 32;
-// How a launch's per-workgroup counter rows reach the caller's u64 counters (RxParams::fused):
-//   kCombineReduce   plain row stores, then dk_flow_reduce_kernel (a second launch);
-//   kCombineTree     the two-level ticket tree above, inside the launch;
-//   kCombineReplica  inside the launch, through replica rows: each workgroup adds its nonzero row words to the replica
-//                    row of its run of rep_wgs consecutive workgroups with no-return u32 atomics (they execute at the
-//                    memory side: nothing is re-read, MI355X_MICROARCH.md "Global atomics"), drains, and takes a ticket
-//                    of that replica; the replica's last arriver swaps the row back to zero (returning atomics) and adds
-//                    it to the caller's counters, one u64 atomic per counter per replica. Packed u16 flow pairs stay
-//                    packed in the replica, so the host bounds a replica's frames below 65536.
-constexpr uint32_t kCombineReduce = 0, kCombineTree = 1, kCombineReplica = 2;
-#ifndef DK_REPLICA_WGS
-#define DK_REPLICA_WGS 16
-#endif
-constexpr uint32_t kReplicaWgs = DK_REPLICA_WGS;
-// Tickets of a launch of `grid` workgroups: one per group, then one per supergroup, each on a 128-byte line of its own
-// (kTicketStride words): device-scope atomics to one line serialise at ~12 ns each (MI355X_MICROARCH.md, fanin), so
-// tickets sharing lines made every group's arrivals queue behind every other group's (C3: 1,280 adds on 3 lines).
-#ifndef DK_TICKET_STRIDE
-#define DK_TICKET_STRIDE 32
-#endif
-constexpr uint32_t kTicketStride = DK_TICKET_STRIDE;
-DK_HD uint32_t count_tickets(uint32_t grid) {
-    const uint32_t ng = (grid + kCountGroup - 1) / kCountGroup;
-    return (ng + (ng + kSuperGroup - 1) / kSuperGroup) * kTicketStride;
-}
+constexpr uint32_t kRowAlignWords = 32;  // counter rows padded to whole 128-byte lines
 
 // Kernel parameters (passed by value).
 struct RxParams {
@@ -149,13 +104,7 @@ struct RxParams {
     uint32_t row_words;      // words per workgroup row of flow_scratch: flow_words + (verdict_counts ? kVerdictWords : 0)
     uint32_t row_stride;     // row_words rounded up to kRowAlignWords
     uint32_t* flow_scratch;  // [grid][row_stride]: the packed-u16 flow histogram (kFlowLds), then the u32 verdict
-                             // histogram; nullptr when row_words == 0
-    uint32_t* tickets;       // [count_tickets(grid)] arrival tickets, 0 between launches (the last arrivers reset them)
-    uint32_t* group_rows;    // [groups][group_stride]: level-1 sums (u32 per flow, then per verdict)
-    uint32_t group_stride;   // 2 * flow_words + DK_V_COUNT rounded up to kRowAlignWords
-    uint32_t fused;          // kCombine*: how the rows reach the caller's counters
-    uint32_t* reps;          // kCombineReplica: [ceil(grid / rep_wgs)][row_stride] u32 replica rows, zero between launches
-    uint32_t rep_wgs;        // kCombineReplica: workgroups per replica row (consecutive blockIdx)
+                             // histogram; nullptr when row_words == 0. dk_flow_reduce_kernel adds the rows up.
     uint64_t* defer;         // small-frame kernel: [ceil(n / 64)] masks of the frames each 64-frame chunk left to the
                              // general path after its main loop
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)

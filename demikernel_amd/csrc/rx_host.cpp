@@ -26,20 +26,16 @@ constexpr uint32_t kDefaultChunkFrames = 1u << 16;
 constexpr uint64_t kMaxChunkBytes = 256ull << 20;
 constexpr size_t kMaxStreamSlots = 8;
 
-// Counter scratch of one stream's launches: per-workgroup rows, the level-1 group rows and the arrival tickets of
-// flush_counters (rx_kernels.hip). Tickets are zeroed once at allocation; each launch's last arrivers reset theirs.
+// Counter scratch of one stream's launches: the per-workgroup counter rows (flush_counters, rx_kernels.hip), which
+// dk_flow_reduce_kernel adds up after the receive kernel, and the small-frame kernel's deferral masks.
 struct CountScratch {
     uint32_t* rows = nullptr;
     size_t rows_words = 0;
-    uint32_t* tickets = nullptr;
-    uint32_t ntickets = 0;
     uint64_t* defer = nullptr;  // the small-frame kernel's per-chunk deferral masks
     size_t ndefer = 0;
-    uint32_t* reps = nullptr;  // kCombineReplica rows: zeroed at allocation, each launch's last arrivers re-zero theirs
-    size_t reps_words = 0;
 };
 
-// A context's scratch is keyed by stream: calls on different streams never share counter rows or tickets, so their
+// A context's scratch is keyed by stream: calls on different streams never share counter rows, so their
 // launches may run concurrently. Past kMaxStreamSlots streams the least recently used slot is taken over, and the new
 // stream first waits for the slot's last launch (its event). Streams must outlive the context or be released with
 // dk_rx_stream_forget (dk_rx.h), so the handle a slot keeps is valid whenever it is used.
@@ -70,7 +66,6 @@ struct Stage {  // device staging for one pipeline stream
 struct Tuning {
     int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
     int32_t lds_table = -1;  // 0: Active lookups never use the LDS table (DK_RX_LDS_TABLE)
-    int32_t combine = -1;    // dk::kCombine* (DK_RX_COMBINE)
     int32_t host_zc = -1;  // dk_rx_process_host: read mapped pinned frames in place (-1/1 when mapped, 0 never)
 };
 
@@ -203,9 +198,7 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
 
 void free_slot(StreamSlot& s) {  // the caller has waited for the slot's launches
     if (s.cs.rows) (void)hipFree(s.cs.rows);
-    if (s.cs.tickets) (void)hipFree(s.cs.tickets);
     if (s.cs.defer) (void)hipFree(s.cs.defer);
-    if (s.cs.reps) (void)hipFree(s.cs.reps);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
 }
@@ -264,16 +257,11 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
     return 0;
 }
 
-// Rows for `grid` workgroups, their group rows and tickets, and `ndefer` deferral masks. Growing waits for the slot's
-// last launch before freeing.
-int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t group_stride, size_t ndefer,
-                  uint32_t nreps) {
+// Rows for `grid` workgroups and `ndefer` deferral masks. Growing waits for the slot's last launch before freeing.
+int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, size_t ndefer) {
     CountScratch& cs = s.cs;
-    const size_t ngroups = (grid + dk::kCountGroup - 1) / dk::kCountGroup;
-    const size_t words = row_stride ? (size_t)grid * row_stride + ngroups * group_stride : 0;
-    const uint32_t nt = row_stride ? std::max(dk::count_tickets(grid), nreps * dk::kTicketStride) : 0;
-    const size_t rwords = (size_t)nreps * row_stride;
-    if (cs.rows_words >= words && cs.ntickets >= nt && cs.ndefer >= ndefer && cs.reps_words >= rwords) return 0;
+    const size_t words = (size_t)grid * row_stride;
+    if (cs.rows_words >= words && cs.ndefer >= ndefer) return 0;
     if (hipStreamSynchronize(s.stream) != hipSuccess) return EIO;  // launches still using the old buffers
     if (cs.rows_words < words) {
         if (cs.rows) (void)hipFree(cs.rows);
@@ -281,22 +269,6 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, uint32_t gr
         cs.rows_words = 0;
         if (hipMalloc(&cs.rows, words * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
         cs.rows_words = words;
-    }
-    if (cs.ntickets < nt) {
-        if (cs.tickets) (void)hipFree(cs.tickets);
-        cs.tickets = nullptr;
-        cs.ntickets = 0;
-        if (hipMalloc(&cs.tickets, nt * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
-        if (hipMemset(cs.tickets, 0, nt * sizeof(uint32_t)) != hipSuccess) return EIO;
-        cs.ntickets = nt;
-    }
-    if (cs.reps_words < rwords) {
-        if (cs.reps) (void)hipFree(cs.reps);
-        cs.reps = nullptr;
-        cs.reps_words = 0;
-        if (hipMalloc(&cs.reps, rwords * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
-        if (hipMemset(cs.reps, 0, rwords * sizeof(uint32_t)) != hipSuccess) return EIO;
-        cs.reps_words = rwords;
     }
     if (cs.ndefer < ndefer) {
         if (cs.defer) (void)hipFree(cs.defer);
@@ -320,12 +292,6 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.row_words = 0;
     p.row_stride = 0;
     p.flow_scratch = nullptr;
-    p.tickets = nullptr;
-    p.group_rows = nullptr;
-    p.group_stride = 0;
-    p.fused = dk::kCombineReduce;
-    p.reps = nullptr;
-    p.rep_wgs = 0;
     p.defer = nullptr;
     uint32_t dyn = 0;
     if (p.res.flow_counts && c->nflows) {
@@ -388,8 +354,8 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
-    // Per-workgroup histogram rows (flow pairs, then verdicts), combined in-launch per group of workgroups, and the
-    // small-frame kernel's deferral masks: a launch that needs either uses the stream's scratch slot.
+    // Per-workgroup histogram rows (flow pairs, then verdicts; dk_flow_reduce_kernel adds them up) and the small-frame
+    // kernel's deferral masks: a launch that needs either uses the stream's scratch slot.
     StreamSlot* slot = nullptr;
     int rc = 0;
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
@@ -397,37 +363,17 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * dk_rx_small_block_waves() : 0;
     if (p.row_words || ndefer) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
-        uint32_t nreps = 0;
-        if (p.row_words) {
+        if (p.row_words)
             p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
-            p.group_stride = (2 * p.flow_words + DK_V_COUNT + dk::kRowAlignWords - 1) / dk::kRowAlignWords *
-                             dk::kRowAlignWords;
-            p.fused = grid <= dk::kFusedMaxGrid ? dk::kCombineTree : dk::kCombineReduce;
-            if (T.combine >= 0) p.fused = (uint32_t)std::min(T.combine, 2);
-            if (p.fused == dk::kCombineReplica) {
-                // a replica's packed u16 flow halves must not carry: frames per replica < 65536 (a workgroup takes at
-                // most ceil(tiles / grid) + 1 tiles of 256 frames under either schedule)
-                const uint32_t per_wg = ((ntiles + grid - 1) / grid + 1) * 256u;
-                p.rep_wgs = std::max(1u, std::min(dk::kReplicaWgs, 65535u / per_wg));
-                if (p.flow_mode != dk::kFlowLds) p.rep_wgs = dk::kReplicaWgs;
-                if (p.flow_mode == dk::kFlowLds && per_wg > 65535u) p.fused = dk::kCombineReduce;
-                else nreps = (grid + p.rep_wgs - 1) / p.rep_wgs;
-            }
-        }
-        if ((rc = ensure_counts(*slot, grid, p.row_stride, p.group_stride, ndefer, nreps))) return rc;
-        if (p.row_words) {
-            p.flow_scratch = slot->cs.rows;
-            p.group_rows = slot->cs.rows + (size_t)grid * p.row_stride;
-            p.tickets = slot->cs.tickets;
-            p.reps = slot->cs.reps;
-        }
+        if ((rc = ensure_counts(*slot, grid, p.row_stride, ndefer))) return rc;
+        if (p.row_words) p.flow_scratch = slot->cs.rows;
         p.defer = slot->cs.defer;
     }
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
-                        "small=%u fused=%u lds_table=%u\n",
+                        "small=%u lds_table=%u\n",
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
-                p.small, p.fused, p.lt_words ? p.lt_n : 0u);
+                p.small, p.lt_words ? p.lt_n : 0u);
     rc = dk_launch_rx(p, grid, stream);
     if (rc == 0 && slot && (DK_SLOT_EVENTS || c->saturated)) {
         if (hipEventRecord(slot->last, stream) != hipSuccess) return EIO;
@@ -536,7 +482,6 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     t.debug = env_knob("DK_RX_DEBUG");
     t.host_zc = env_knob("DK_RX_HOST_ZC");
     t.lds_table = env_knob("DK_RX_LDS_TABLE");
-    t.combine = env_knob("DK_RX_COMBINE");
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
     std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
@@ -852,7 +797,6 @@ int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t knobs[DK_DIAG_RX_KNOBS]) {
     t.grid_per_cu = knobs[5];
     t.debug = knobs[6];
     t.lds_table = knobs[7];
-    t.combine = knobs[8];
     t.host_zc = zc;
     c->tune = t;
     c->occ_family = ~0u;

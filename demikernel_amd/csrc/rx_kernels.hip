@@ -1089,173 +1089,29 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
     }
 }
 
-// Workgroup exit: the LDS histograms (flow words in kFlowLds mode, then the verdict words) reach the caller's u64
-// counters, combined inside the launch (P.fused) by a two-level tree of arrival tickets:
-//   1. each workgroup writes its row write-through (sc1 stores: the line goes to memory and leaves this XCD's L2),
-//      every storing wave drains (s_waitcnt vmcnt(0)), then one lane adds 1 to its group's ticket (agent scope);
-//   2. the workgroup whose add returns gn - 1 (the last of its group of kCountGroup) sums the group's rows (sc1 loads)
-//      into one group row of u32 columns (flow f at column f, then the verdicts), stores it write-through, drains and
-//      adds 1 to its supergroup's ticket;
-//   3. the last group winner of each supergroup of kSuperGroup groups sums those group rows and adds the column sums to
-//      the caller's counters with device-scope atomics: ceil(groups / kSuperGroup) adds per counter (C3's 1,280
-//      workgroups: 80 groups, 10 supergroups, 10 adds per address instead of the 80 of one level, whose same-address
-//      atomics serialised at ~75 ns each); then it resets its tickets for the next launch.
-//   A grid of one group skips level 2. This is MI355X_MICROARCH.md §"inter-workgroup visibility", Valid forms row 1
-//   (write-through payload, drained, one agent-scope add per storing workgroup, the last adder told by the returned
-//   value, sc1 loads), applied per level. It relies on gfx9's memory pipeline — sc1 stores write through, and stores are
-//   counted by vmcnt, so the drain orders them before the ticket — rather than on release/acquire atomics, whose
-//   agent-scope forms here are a whole-L2 writeback (buffer_wbl2) and invalidate (buffer_inv) per workgroup; the guard
-//   below keeps the pattern on the architectures it was written and tested for.
-// P.fused == 0 (grids above kFusedMaxGrid, rx_common.h: the small-frame kernel's): plain row stores, and
-// dk_flow_reduce_kernel adds them up in a second launch.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
-#error "flush_counters: the in-launch combine's ordering is written for gfx942/gfx950 (sc1 write-through, vmcnt stores)"
-#endif
-typedef __attribute__((address_space(1))) uint32_t gu32;
-__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
-    __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
-    return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool arrive_last(uint32_t* ticket, uint32_t count, uint32_t tid, uint32_t* s_last) {
-#ifdef DK_ABL_NOTICKET  // ablation (tuning only, counts wrong): rows stored, no combine
-    return false;
-#endif
-#ifndef DK_ABL_NODRAIN  // ablation (tuning only, unordered): no drain before the ticket
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its write-through stores have landed
-#endif
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t old = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = old == count - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    const bool last = *s_last != 0;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
-    return last;
-}
-__device__ __forceinline__ void add_u64(uint64_t* p, uint64_t v) {
-    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
-}
-// kCombineReplica (rx_common.h): the workgroup's nonzero histogram words go to its replica row by no-return atomic adds,
-// which the drain in arrive_last waits for (vmcnt counts them); the replica's last arriver swaps each word back to zero
-// with a returning atomic (read at the memory side, where the adds were performed: no stale L2 copy can be seen) and adds
-// it to the caller's counters.
-__device__ __forceinline__ void flush_replica(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
-                                              const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
-    const uint32_t r = blockIdx.x / P.rep_wgs;
-    const uint32_t rn = min(P.rep_wgs, gridDim.x - r * P.rep_wgs);
-    uint32_t* rep = P.reps + (size_t)r * P.row_stride;
-    if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += nthreads) {
-            const uint32_t x = s_flow[k];
-            if (x) __hip_atomic_fetch_add((gu32*)(rep + k), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    if (P.res.verdict_counts && tid < DK_V_COUNT && s_vh[tid])
-        __hip_atomic_fetch_add((gu32*)(rep + P.flow_words + tid), s_vh[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!arrive_last(P.tickets + r * kTicketStride, rn, tid, s_last)) return;
-    for (uint32_t w = tid; w < P.row_words; w += nthreads) {
-        const bool flow = w < P.flow_words;
-        if (flow ? !lds_flows : w - P.flow_words >= DK_V_COUNT) continue;
-        const uint32_t x = __hip_atomic_exchange((gu32*)(rep + w), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!flow) {
-            add_u64(P.res.verdict_counts + (w - P.flow_words), x);
-        } else {
-            add_u64(P.res.flow_counts + 2 * w, x & 0xFFFFu);
-            if (2 * w + 1 < P.nflows) add_u64(P.res.flow_counts + 2 * w + 1, x >> 16);
-        }
-    }
-    if (tid == 0) __hip_atomic_store((gu32*)(P.tickets + r * kTicketStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// Workgroup exit: the LDS histograms (flow words in kFlowLds mode, then the verdict words) become this workgroup's row
+// of the launch scratch (plain stores), and dk_flow_reduce_kernel, a second launch on the same stream, adds the rows to
+// the caller's u64 counters. Round 3 measured every in-launch form against it on two boxes: a two-level
+// tree of arrival tickets (write-through rows, drained, the last arriver of each group summing its group) was slower on
+// every workload (C2 +0.8 %, IMIX +2.3 %, C5 +3.3 %, C3 +23 %) and on small batches too, and replica rows filled by
+// memory-side atomics tied with the second launch; the kernels hold no inter-workgroup hand-off at all.
 __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
-                                               const uint32_t* s_flow, const uint32_t* s_vh, uint32_t* s_last) {
+                                               const uint32_t* s_flow, const uint32_t* s_vh) {
     if (!P.row_words) return;
-#ifdef DK_ABL_NOFLUSH  // ablation (tuning only): counters never leave LDS, no combine
+#ifdef DK_ABL_NOFLUSH  // ablation (tuning only): counters never leave LDS
     return;
 #endif
-    if (P.fused == kCombineReplica) {
-        flush_replica(P, tid, nthreads, lds_flows, s_flow, s_vh, s_last);
-        return;
-    }
     uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_stride;
-    if (P.fused == kCombineReduce) {  // rows with plain stores; dk_flow_reduce_kernel (a second launch) adds them up
-        if (lds_flows)
-            for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
-        if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
-        return;
-    }
     if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += nthreads) st_wt(row + k, s_flow[k]);
-    if (P.res.verdict_counts && tid < kVerdictWords) st_wt(row + P.flow_words + tid, tid < DK_V_COUNT ? s_vh[tid] : 0u);
-    const uint32_t ngroups = (gridDim.x + kCountGroup - 1) / kCountGroup;
-    const uint32_t g = blockIdx.x / kCountGroup, r0 = g * kCountGroup;
-    const uint32_t gn = min(kCountGroup, gridDim.x - r0);
-    if (!arrive_last(P.tickets + g * kTicketStride, gn, tid, s_last)) return;
-    // level 1: the group's rows, column by column (all kCountGroup loads in flight; a short group re-reads its last)
-    const bool direct = ngroups == 1;  // one group: its winner adds to the caller's counters itself
-    const uint32_t fw2 = 2 * P.flow_words;
-    uint32_t* grow = P.group_rows + (size_t)g * P.group_stride;
-    const uint32_t* rows = P.flow_scratch + (size_t)r0 * P.row_stride;
-    for (uint32_t w = tid; w < P.row_words; w += nthreads) {
-        uint32_t x[kCountGroup];
-#pragma unroll
-        for (uint32_t k = 0; k < kCountGroup; k++)
-            x[k] = ld_wt(rows + (size_t)min(k, gn - 1) * P.row_stride + w);
-#pragma unroll
-        for (uint32_t k = 0; k < kCountGroup; k++) x[k] = k < gn ? x[k] : 0u;
-        uint32_t lo = 0, hi = 0;  // < kCountGroup * 65536 each
-#pragma unroll
-        for (uint32_t k = 0; k < kCountGroup; k++) {
-            lo += x[k] & 0xFFFFu;
-            hi += x[k] >> 16;
-        }
-        if (w >= P.flow_words) {  // verdict column: a plain u32 count (< 2^21 per group)
-            const uint32_t v = w - P.flow_words;
-            if (v >= DK_V_COUNT) continue;
-            if (direct) add_u64(P.res.verdict_counts + v, lo + ((uint64_t)hi << 16));
-            else st_wt(grow + fw2 + v, lo + (hi << 16));
-        } else if (direct) {
-            add_u64(P.res.flow_counts + 2 * w, lo);
-            if (2 * w + 1 < P.nflows) add_u64(P.res.flow_counts + 2 * w + 1, hi);
-        } else {
-            st_wt(grow + 2 * w, lo);
-            st_wt(grow + 2 * w + 1, hi);
-        }
-    }
-    if (tid == 0)
-        __hip_atomic_store((gu32*)(P.tickets + g * kTicketStride), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (direct) return;
-#ifdef DK_ABL_L1ONLY  // ablation (tuning only, counts wrong): level 1 only
-    return;
-#endif
-    // level 2: the supergroup's group rows
-    const uint32_t sg = g / kSuperGroup, g0 = sg * kSuperGroup;
-    const uint32_t sgn = min(kSuperGroup, ngroups - g0);
-    uint32_t* t2 = P.tickets + (ngroups + sg) * kTicketStride;
-    if (!arrive_last(t2, sgn, tid, s_last)) return;
-    const uint32_t gwords = fw2 + (P.res.verdict_counts ? (uint32_t)DK_V_COUNT : 0u);
-    const uint32_t* grows = P.group_rows + (size_t)g0 * P.group_stride;
-    for (uint32_t w = tid; w < gwords; w += nthreads) {
-        if (w < fw2 && (w >= P.nflows || !lds_flows)) continue;
-        uint32_t x[kSuperGroup];
-#pragma unroll
-        for (uint32_t k = 0; k < kSuperGroup; k++) x[k] = ld_wt(grows + (size_t)min(k, sgn - 1) * P.group_stride + w);
-        uint64_t t = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kSuperGroup; k++) t += k < sgn ? x[k] : 0u;
-        if (w < fw2) add_u64(P.res.flow_counts + w, t);
-        else add_u64(P.res.verdict_counts + (w - fw2), t);
-    }
-    if (tid == 0) __hip_atomic_store((gu32*)t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
+    if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
 }
 
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
 // per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
-// wraps). At exit both histograms reach the caller's u64 counters through flush_counters (in-launch, per group of
-// kCountGroup workgroups). kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
+// wraps). At exit both histograms reach the caller's u64 counters through flush_counters and dk_flow_reduce_kernel.
+// kFlowGlobal (tables too large for LDS): one u64 atomic per delivered frame.
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
@@ -1264,7 +1120,6 @@ __global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_
 void dk_rx_kernel(RxParams P) {
     __shared__ WaveLds s_wave[kWaves];        // per-wave phase B/C exchange
     __shared__ uint32_t s_vh[DK_V_COUNT];     // verdict histogram
-    __shared__ uint32_t s_last;               // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
     const uint32_t tid = threadIdx.x;
@@ -1319,7 +1174,7 @@ void dk_rx_kernel(RxParams P) {
 
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     __syncthreads();
-    flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh, &s_last);
+    flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
 }
 
 // Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
@@ -1601,7 +1456,6 @@ template <bool kShift, bool kOpt>
 __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
     __shared__ SmallLds s_wave[kSmallWaves];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
-    __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
     const uint32_t tid = threadIdx.x;
@@ -1711,7 +1565,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     DK_STAMP_T(14, __builtin_amdgcn_s_memtime());
 #endif
     __syncthreads();
-    flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh, &s_last);
+    flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh);
 #ifdef DK_DIAG_STAMPS
     DK_STAMP_T(15, __builtin_amdgcn_s_memtime());
     DK_STAMP_T(13, __builtin_amdgcn_s_memrealtime());
@@ -1781,7 +1635,6 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     __shared__ WaveLds s_buf[kBufs][kWaves];  // [chunk % kBufs][stream wave]
     __shared__ uint32_t s_ready[kWaves][kBufs], s_free[kWaves][kBufs];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
-    __shared__ uint32_t s_last;            // flush_counters: this workgroup arrived last in its group
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
     const uint32_t tid = threadIdx.x;
@@ -1858,7 +1711,7 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     }
     __syncthreads();
     if (finisher && nstg) flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
-    flush_counters(P, tid, S::kThreads, lds_flows, s_flow, s_vh, &s_last);
+    flush_counters(P, tid, S::kThreads, lds_flows, s_flow, s_vh);
 }
 
 // Adds the per-workgroup rows of flow_scratch[rows][row_words] into the caller's u64 counters: columns
@@ -2199,7 +2052,7 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
 #ifdef DK_ABL_NOFLUSH
     if (false) {
 #else
-    if (p.row_words && p.fused == dk::kCombineReduce) {
+    if (p.row_words) {
 #endif
         const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
                       (grid + dk::kReduceRows - 1) / dk::kReduceRows);

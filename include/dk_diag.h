@@ -29,13 +29,12 @@ int dk_diag_path_stats_read(struct dk_rx_ctx* ctx, uint64_t out[4]); /* synchron
 
 /* Tuning overrides for A/B measurements and tests (-1 = the engine's own rule). A receive context reads them once from
  * the environment when it is created (DK_RX_STAGE, DK_RX_SPLIT, DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID,
- * DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE, DK_RX_COMBINE), never on the launch path; this call replaces them.
- * knobs[] = {stage, split, small, sched, grid, grid_per_cu, debug, lds_table, combine}: stage/split/small force a kernel
+ * DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE), never on the launch path; this call replaces them.
+ * knobs[] = {stage, split, small, sched, grid, grid_per_cu, debug, lds_table}: stage/split/small force a kernel
  * family on (1) or off (0), sched picks the wave schedule (0 round-robin tiles, 1 one contiguous share per wave),
  * grid / grid_per_cu fix the persistent grid, debug > 0 prints each launch's choice to stderr, lds_table 0 keeps Active
- * lookups on the global socket table (no LDS copy), combine picks how the per-workgroup counters reach the caller's
- * (0 a second reduce kernel, 1 the in-launch ticket tree, 2 in-launch replica rows). */
-#define DK_DIAG_RX_KNOBS 9
+ * lookups on the global socket table (no LDS copy). */
+#define DK_DIAG_RX_KNOBS 8
 int dk_diag_rx_set_tuning(struct dk_rx_ctx* ctx, const int32_t knobs[DK_DIAG_RX_KNOBS]); /* 0 or EINVAL */
 /* The same for dk_tx_checksum (process-wide; first read from DK_TX_SPLIT, DK_RX_SCHED, DK_RX_GRID_PER_CU). */
 int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu); /* 0 */

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--knob", default="", help="NAME=v1,v2,...: interleave values of one more env knob (e.g. DK_RX_SPLIT=0,1)")
     ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
     ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
+    ap.add_argument("--frames", type=int, default=0, help="frames per batch (0: the workload's own)")
     ap.add_argument("--check", action="store_true", help="also compare every variant's results and counters with the "
                                                           "first variant's on one fresh launch")
     args = ap.parse_args()
@@ -36,8 +37,9 @@ def main():
     from demikernel_amd import _native as N
 
     base = RxEngine(Config(synth.BOB_IPV4))
-    batch, flows, tr = bench.make_batch(base, args.workload, 0, synth.SEED, 1)
-    rot = [batch] + [bench.make_batch(base, args.workload, 0, synth.SEED + 1000 * k, 1)[0] for k in range(1, args.rotate)]
+    batch, flows, tr = bench.make_batch(base, args.workload, 0, synth.SEED, 1, frames=args.frames)
+    rot = [batch] + [bench.make_batch(base, args.workload, 0, synth.SEED + 1000 * k, 1, frames=args.frames)[0]
+                     for k in range(1, args.rotate)]
     engines = {}
     for v in args.variants:
         e = RxEngine(Config(synth.BOB_IPV4), lib_path=os.path.abspath(v))
