@@ -62,6 +62,13 @@ constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave 
 #define DK_ROUNDS_PER_STEP 2
 #endif
 constexpr uint32_t kRoundsPerStep = DK_ROUNDS_PER_STEP;  // phase-B rounds whose loads are in flight together
+// The result-staging kernel (mixed sizes, IMIX) streams one round per step: half the load registers (144 VGPRs with
+// 8 staged chunks, no spills beyond the option walk's frame) for twice the steps; with kStageK 8 IMIX -2.5...-3.5 % on
+// three boxes (round 3).
+#ifndef DK_ROUNDS_STAGED
+#define DK_ROUNDS_STAGED 1
+#endif
+constexpr uint32_t kRoundsStaged = DK_ROUNDS_STAGED;
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
@@ -651,7 +658,7 @@ __device__ __forceinline__ void coop_finish(uint32_t k0, uint32_t k1, uint32_t m
 }
 
 // Phase B of one chunk: the medium frames' steps, then the large frames' steps.
-template <bool kShift, bool kHdrT = false>
+template <bool kShift, bool kHdrT = false, uint32_t kR = kRoundsPerStep>
 __device__ __forceinline__ void coop_stream(const CoopPlan& pl, uint32_t lane, WaveLds& W, const Blob& B) {
 #if DK_COOP_MED_U > 0
     for (uint32_t r = 0; r * 4 < pl.nmed; r += kMedR) {
@@ -660,10 +667,10 @@ __device__ __forceinline__ void coop_stream(const CoopPlan& pl, uint32_t lane, W
         coop_finish<kShift, kMedU, kMedR, kHdrT>(0, pl.nmed, 1, r, lane, W, B, S);
     }
 #endif
-    for (uint32_t r = 0; r * 4 < pl.ncoop - pl.nmed; r += kRoundsPerStep) {
-        CoopStep<kCoopU, kRoundsPerStep> S;
-        coop_issue<kCoopU, kRoundsPerStep, kHdrT>(pl.nmed, pl.ncoop, r, lane, W, B, S, 0);
-        coop_finish<kShift, kCoopU, kRoundsPerStep, kHdrT>(pl.nmed, pl.ncoop, pl.maxit, r, lane, W, B, S);
+    for (uint32_t r = 0; r * 4 < pl.ncoop - pl.nmed; r += kR) {
+        CoopStep<kCoopU, kR> S;
+        coop_issue<kCoopU, kR, kHdrT>(pl.nmed, pl.ncoop, r, lane, W, B, S, 0);
+        coop_finish<kShift, kCoopU, kR, kHdrT>(pl.nmed, pl.ncoop, pl.maxit, r, lane, W, B, S);
     }
 }
 
@@ -709,14 +716,14 @@ __device__ __forceinline__ void coop_gather(const FrameDesc<kShift>& F, const Co
 // Phases A and B of one 64-frame chunk, shared by the RX and TX kernels; every lane of the wave calls it.
 // On return the owner lane holds frame bytes [0, 64) in C.R (realigned when sh != 0) and, for big frames, the LE-half
 // sum of frame bytes [0, 16 * nblk - sh) in C.fsum and the last granule in W.tail[lane].
-template <bool kShift, bool kHdrT = false>
+template <bool kShift, bool kHdrT = false, uint32_t kR = kRoundsPerStep>
 __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t lane,
                                              WaveLds& W, uint32_t off, uint32_t len, Chunk& C) {
     const FrameDesc<kShift> F(frames, frames_bytes, live, off, len);
     const Blob B(frames, frames_bytes);
     small_load(F, B, off, C.R);
     const CoopPlan pl = coop_plan(F, lane, off, W);
-    coop_stream<kShift, kHdrT>(pl, lane, W, B);
+    coop_stream<kShift, kHdrT, kR>(pl, lane, W, B);
     coop_gather(F, pl, lane, W, C);
 }
 
@@ -790,10 +797,10 @@ struct Rec {
 // L2-resident window instead recovers it all). The staged kernels hold the last kStageK chunks' results in registers
 // and store them together, so a wave's writes leave in one burst per kStageK chunks (at exit for C2 at 3 WG/CU).
 #ifndef DK_STAGE_K
-#define DK_STAGE_K 6
+#define DK_STAGE_K 8
 #endif
 #ifndef DK_MIN_WAVES_STAGED
-#define DK_MIN_WAVES_STAGED 3  // 6 x 6 staged words fit in 168 VGPRs without spills
+#define DK_MIN_WAVES_STAGED 3  // 8 x 6 staged words and one round of loads fit in 168 VGPRs without spills
 #endif
 constexpr int kStageK = DK_STAGE_K;
 
@@ -1158,7 +1165,8 @@ void dk_rx_kernel(RxParams P) {
         Rec rec;
         rec.meta = kNoRec;
         Chunk C;
-        stream_chunk<kShift>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
+        stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
+                                                                              len, C);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (kStage) {  // shift register of the last kStageK chunks' results; stored when full and at exit
 #pragma unroll
