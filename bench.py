@@ -78,8 +78,35 @@ def make_batch(eng, name, rank, seed_base, world=1, frames=0):
     return batch, flows, tr
 
 
+PREHEAT_S = 0.25  # untimed clock ramp before each measurement (bench --preheat-seconds)
+
+
+def set_preheat(seconds: float) -> None:
+    global PREHEAT_S
+    PREHEAT_S = max(float(seconds), 0.0)
+
+
+def preheat(eng, batch, stream, seconds):
+    """Untimed, before the warmup steps: the receive kernel over this batch for `seconds` of wall time, into a scratch
+    result record without counters (the measured steps' counters see none of it). A fresh process measured its first
+    ~10 ms of launches 4-7 % slower than steady state (C2 246.7 vs 240.5 us, IMIX 157.0 vs 144.9 us: the GPU's clocks
+    ramping, not caches: 300 ms of copies over unrelated buffers removed it too, tools/timing_check.py), and 5 warmup
+    steps are ~1 ms of work."""
+    import torch
+
+    if seconds <= 0:
+        return
+    scratch = eng.results(batch.n, counts=False)
+    t = time.perf_counter()
+    while time.perf_counter() - t < seconds:
+        for _ in range(8):
+            eng.receive_batch(batch, scratch, stream=stream)
+        torch.cuda.synchronize()
+    del scratch
+
+
 def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
-    """Run warmup + timed steps. A step = the receive pass over one batch (+ for N > 1 the all-reduce of this step's
+    """Run the untimed preheat, then warmup + timed steps. A step = the receive pass over one batch (+ for N > 1 the all-reduce of this step's
     counters over RCCL: ShardedReceiver, double-buffered counters, the collective on a side stream so step k's
     reduction overlaps step k+1's kernel). Returns (wall seconds for `steps`, per-launch kernel seconds from HIP
     events on the launch stream around the timed region, per-step collective seconds measured unoverlapped)."""
@@ -88,6 +115,7 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
     from demikernel_amd.shard import ShardedReceiver
 
     sr = ShardedReceiver(eng, res, comm, stream)
+    preheat(eng, batches[0], stream, PREHEAT_S)
     for k in range(warmup):
         sr.step(batches[k % len(batches)])
     sr.drain()
@@ -480,6 +508,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-frames", type=int, default=1 << 19)
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--preheat-seconds", type=float, default=PREHEAT_S,
+                    help="untimed receive launches before each measurement's warmup steps (GPU clock ramp)")
     ap.add_argument("--backend", default="gloo", choices=["nccl", "gloo"],
                     help="N > 1: process group for the barrier and the max-over-ranks timing only (the counters are "
                          "reduced by dk_rx_flow_counts_allreduce_to over RCCL)")
@@ -491,6 +521,7 @@ def main():
     ap.add_argument("--counts-out", default="",
                     help="write the node-wide flow / verdict counters after the timed steps to this .npz (rank 0)")
     args = ap.parse_args()
+    set_preheat(args.preheat_seconds)
 
     import torch
 
@@ -567,6 +598,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "untimed_preheat_s": PREHEAT_S,
         "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
