@@ -1608,8 +1608,14 @@ template <int kFin>
 struct SplitShape {
     static_assert(kFin == 1, "one finish wave per stream wave");
     static constexpr int kThreads = 64 * kWaves * (1 + kFin);
-    static constexpr int kBufs = 3;   // LDS buffers per stream wave
-    static constexpr int kStg = 16;   // chunks of results a finish wave stages
+#ifndef DK_SPLIT_BUFS
+#define DK_SPLIT_BUFS 3
+#endif
+#ifndef DK_SPLIT_STG
+#define DK_SPLIT_STG 16
+#endif
+    static constexpr int kBufs = DK_SPLIT_BUFS;  // LDS buffers per stream wave
+    static constexpr int kStg = DK_SPLIT_STG;    // chunks of results a finish wave stages
 };
 constexpr int kSplitBlock = SplitShape<1>::kThreads;  // the TX split kernel's shape
 template <int kStgK>

@@ -53,6 +53,9 @@ def main():
     configs = [(sc, kv) for sc in scheds for kv in kvals]
     times = {(k, g, cf): [] for k in engines for g in grids for cf in configs}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if not args.tx:  # untimed clock ramp (bench.preheat): the first ~10 ms of a fresh process run slow
+        e0, r0 = next(iter(engines.values()))
+        bench.preheat(e0, batch, torch.cuda.current_stream(), 0.25)
     for rep in range(args.reps):
         for g, cf in [(g, cf) for g in grids for cf in configs]:
             sc, kv = cf
