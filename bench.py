@@ -40,6 +40,9 @@ WORKLOADS = {
     "c4_imix": ("IMIX 40/576/1500 at 7:4:1, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, "imix", "tcp", 1024),
     "c4_imix_tilesorted": ("IMIX with each 256-frame tile sorted by size (tuning probe, not a bench line)", 1 << 21,
                            "imix_tilesorted", "tcp", 1024),
+    "c4_imix_periodic": ("IMIX with one shuffled 64-frame pattern (37 x 40 B, 21 x 576 B, 6 x 1500 B) repeated: every "
+                         "chunk the same bytes (tuning probe for load balance, not a bench line)", 1 << 21,
+                         "imix_periodic", "tcp", 1024),
     "c5_tcp1500_10k": ("1500B IPv4/TCP, 10k flows, 2M frames per GPU (16M over 8 GPUs)", 1 << 21, 1486, "tcp", 10000),
 }
 
@@ -65,6 +68,10 @@ def make_batch(eng, name, rank, seed_base, world=1, frames=0):
         if ip_len == "imix_tilesorted":
             m = total // 256 * 256
             ip_all[:m] = np.sort(ip_all[:m].reshape(-1, 256), axis=1).reshape(-1)
+        elif ip_len == "imix_periodic":
+            pat = np.random.default_rng(seed_base).permutation(np.repeat(np.array([40, 576, 1500], np.uint16),
+                                                                         [37, 21, 6]))
+            ip_all = np.resize(pat, total).astype(np.uint16)
     else:
         ip_all = np.full(total, ip_len, np.uint16)
     frame_all = np.maximum(ip_all.astype(np.int64) + 14, synth.ETH_MIN_FRAME)
