@@ -540,13 +540,13 @@ struct CoopPlan {  // wave-uniform
     uint32_t nmed;   // of which medium (<= kMedGran granules): ranks [0, nmed), streamed by the medium step shape
     uint32_t maxit;  // iterations per round of the large shape (1 unless a frame exceeds kCoopSpan granules)
 };
-// Step shapes, both with kRoundsPerStep * kCoopU = 12 loads in flight per lane: kCoopU = 6 slots per lane (a 1536-byte
-// quarter-wave span) for every big frame, or (DK_COOP_MED_U = 3) medium frames (<= kMedGran granules, IMIX 576 B)
-// ranked first and streamed with half the span at twice the rounds. A 590-byte frame fills 37 of the 96 slots of
-// the large shape, but the medium shape measured no gain (IMIX +0.7 %, C2 ±0): the slots at kOob cost
-// neither memory traffic nor, it turns out, time.
+// Step shapes: kCoopU = 6 slots per lane (a 1536-byte quarter-wave span) for large frames, kRoundsPerStep (the
+// staged kernel: kRoundsStaged) rounds of 4 frames per step; medium frames (<= kMedGran granules, IMIX 576 B) ranked
+// first and streamed with a DK_COOP_MED_U-load span, (kRoundsPerStep * kCoopU) / DK_COOP_MED_U rounds per step, i.e.
+// 12 medium frames in flight per wave step instead of 4 (a 590-byte frame fills 37 of the large shape's 96 slots).
 #ifndef DK_COOP_MED_U
-#define DK_COOP_MED_U 0  // 3: medium frames take the half-span shape (measured IMIX +0.7 %, C2 ±0: off)
+#define DK_COOP_MED_U 4  // medium frames (<= 1 KiB) take a 4-load span, 12 of them per step (round 3: IMIX -1.1 %,
+                         // C2 ±0; 3 loads: -0.8 %; round 2, before the one-round staged steps: 3 loads +0.7 %)
 #endif
 constexpr uint32_t kMedU = DK_COOP_MED_U > 0 ? DK_COOP_MED_U : 1;
 [[maybe_unused]] constexpr uint32_t kMedR = (kRoundsPerStep * kCoopU) / kMedU;
