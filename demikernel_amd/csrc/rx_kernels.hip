@@ -62,9 +62,8 @@ constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave 
 #define DK_ROUNDS_PER_STEP 2
 #endif
 constexpr uint32_t kRoundsPerStep = DK_ROUNDS_PER_STEP;  // phase-B rounds whose loads are in flight together
-// The result-staging kernel (mixed sizes, IMIX) streams one round per step: half the load registers (144 VGPRs with
-// 8 staged chunks, no spills beyond the option walk's frame) for twice the steps; with kStageK 8 IMIX -2.5...-3.5 % on
-// three boxes (round 3).
+// The result-staging kernel (mixed sizes, IMIX) streams one round of large frames per step: half the load registers
+// for twice the steps, which pays for 9 staged chunks (round 3).
 #ifndef DK_ROUNDS_STAGED
 #define DK_ROUNDS_STAGED 1
 #endif
@@ -521,7 +520,10 @@ __device__ __forceinline__ void small_load(const FrameDesc<kShift>& F, const Blo
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const bool use = F.vec && !F.big && (uint32_t)(16 * k) < F.span;
-        const uint4 q = B.template ld<false>(use ? off - F.sh + 16 * k : kOob);
+#ifndef DK_SMALL_LOAD_NT
+#define DK_SMALL_LOAD_NT 0
+#endif
+        const uint4 q = B.template ld<DK_SMALL_LOAD_NT != 0>(use ? off - F.sh + 16 * k : kOob);
         R.w[4 * k + 0] = q.x;
         R.w[4 * k + 1] = q.y;
         R.w[4 * k + 2] = q.z;
@@ -545,8 +547,8 @@ struct CoopPlan {  // wave-uniform
 // first and streamed with a DK_COOP_MED_U-load span, (kRoundsPerStep * kCoopU) / DK_COOP_MED_U rounds per step, i.e.
 // 12 medium frames in flight per wave step instead of 4 (a 590-byte frame fills 37 of the large shape's 96 slots).
 #ifndef DK_COOP_MED_U
-#define DK_COOP_MED_U 4  // medium frames (<= 1 KiB) take a 4-load span, 12 of them per step (round 3: IMIX -1.1 %,
-                         // C2 ±0; 3 loads: -0.8 %; round 2, before the one-round staged steps: 3 loads +0.7 %)
+#define DK_COOP_MED_U 5  // medium frames (<= 1,280 B) take a 5-load span, 8 of them per step (round 3, with 9 staged
+                         // chunks: IMIX -2.5 % over a 6-load span; 4 loads: -1.1 %, 3: -0.8 % at 8 chunks; C2 ±0)
 #endif
 constexpr uint32_t kMedU = DK_COOP_MED_U > 0 ? DK_COOP_MED_U : 1;
 [[maybe_unused]] constexpr uint32_t kMedR = (kRoundsPerStep * kCoopU) / kMedU;
@@ -797,10 +799,10 @@ struct Rec {
 // L2-resident window instead recovers it all). The staged kernels hold the last kStageK chunks' results in registers
 // and store them together, so a wave's writes leave in one burst per kStageK chunks (at exit for C2 at 3 WG/CU).
 #ifndef DK_STAGE_K
-#define DK_STAGE_K 8
+#define DK_STAGE_K 9
 #endif
 #ifndef DK_MIN_WAVES_STAGED
-#define DK_MIN_WAVES_STAGED 3  // 8 x 6 staged words and one round of loads fit in 168 VGPRs without spills
+#define DK_MIN_WAVES_STAGED 3  // 9 x 6 staged words and one round of loads fit in 168 VGPRs without spills
 #endif
 constexpr int kStageK = DK_STAGE_K;
 
