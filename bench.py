@@ -673,8 +673,11 @@ def main():
         del e
         # C1's shape (the reference's own CPU-runnable case: 1078 B frames, one 4-tuple to port 12345) on the GPU; 3
         # rotating batches (141 MB each) so they do not sit in the 256 MB MALL
-        out["c1_tcp1078"], e, _, _ = rx_extra("c1_tcp1078", dev, stream, rotate=3)
-        del e
+        try:
+            out["c1_tcp1078"], e, _, _ = rx_extra("c1_tcp1078", dev, stream, rotate=3)
+            del e
+        except Exception as exc:  # noqa: BLE001 — an extra field must not cost the headline line; the error is reported
+            out["c1_tcp1078"] = {"error": repr(exc)}
         out["c4_imix"], e, _, _ = rx_extra("c4_imix", dev, stream)
         del e
         out["c5_device"], e5, b5, f5 = rx_extra("c5_tcp1500_10k", dev, stream)
