@@ -113,10 +113,12 @@ def preheat(eng, batch, stream, seconds):
 
 
 def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
-    """Run the untimed preheat, then warmup + timed steps. A step = the receive pass over one batch (+ for N > 1 the all-reduce of this step's
-    counters over RCCL: ShardedReceiver, double-buffered counters, the collective on a side stream so step k's
-    reduction overlaps step k+1's kernel). Returns (wall seconds for `steps`, per-launch kernel seconds from HIP
-    events on the launch stream around the timed region, per-step collective seconds measured unoverlapped)."""
+    """Run the untimed preheat, then warmup + timed steps. A step = the receive pass over one batch, whose counter
+    rows the next step's kernel completes (DK_RX_BATCH_DEFER_COUNTS; the last step's by one flush launch inside the
+    timed region), + for N > 1 the all-reduce of each step's counters over RCCL (ShardedReceiver: double-buffered
+    counters, the collective on a side stream overlapping the following kernels). Returns (wall seconds for `steps`,
+    per-step seconds on the launch stream from HIP events around the timed region incl. the flush, per-step collective
+    seconds measured unoverlapped)."""
     import torch
 
     from demikernel_amd.shard import ShardedReceiver
@@ -137,6 +139,7 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
     e0.record(stream)
     for k in range(steps):
         sr.step(batches[k % len(batches)])
+    sr.flush()  # the last step's deferred counters (one small launch on the stream, inside the timed region)
     e1.record(stream)
     sr.drain()
     torch.cuda.synchronize()

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("DK_RX_LIB_VARIANT", LIB_PATH)
 
 DK_FLOW_NONE = 0xFFFFFFFF
 DK_RX_BATCH_ALIGNED16 = 1  # dk_rx_batch.flags
+DK_RX_BATCH_DEFER_COUNTS = 2
 DK_FLOW_TCP_ACTIVE, DK_FLOW_TCP_PASSIVE, DK_FLOW_UDP = 1, 2, 3
 
 # enum dk_verdict (include/dk_rx.h), SURVEY.md Appendix A.
@@ -83,6 +84,7 @@ FUNCTIONS = [
     ("dk_rx_process", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_void_p]),
     ("dk_rx_process_host", c_int, [c_void_p, POINTER(DkRxBatch), POINTER(DkRxResults), c_uint32]),
     ("dk_rx_stream_forget", c_int, [c_void_p, c_void_p]),
+    ("dk_rx_counts_flush", c_int, [c_void_p, c_void_p]),
     ("dk_rx_flow_counts_allreduce", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p]),
     ("dk_rx_flow_counts_allreduce_to", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p, c_void_p,
                                                c_void_p]),
@@ -90,6 +92,7 @@ FUNCTIONS = [
     ("dk_rx_verdict_name", c_char_p, [c_int]),
     ("dk_rx_verdict_errno", c_int, [c_int]),
     ("dk_rx_abi_version", c_uint32, []),
+    ("dk_rx_build_id", c_char_p, []),
     ("dk_rx_device_count", c_int, []),
 ]
 
@@ -181,7 +184,7 @@ DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
     ("dk_diag_path_stats_enable", c_int, [c_void_p, c_int]),
     ("dk_diag_path_stats_read", c_int, [c_void_p, c_void_p]),
-    ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p]),
+    ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p, c_uint32]),
     ("dk_diag_tx_set_tuning", c_int, [c_int32, c_int32, c_int32]),
 ]
 DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table"]

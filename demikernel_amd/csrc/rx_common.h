@@ -81,6 +81,26 @@ constexpr uint32_t kVerdictWords = (DK_V_COUNT + 3) & ~3u;  // verdict histogram
 constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
 constexpr uint32_t kRowAlignWords = 32;  // counter rows padded to whole 128-byte lines
 
+// Counter rows a previous launch on the same stream left pending (DK_RX_BATCH_DEFER_COUNTS), added to that launch's
+// counters inside this launch: waves with nothing else to do (the split kernel's finish waves before their first chunk,
+// every other kernel's waves after their last one) take blocks of the rows by tickets from a
+// monotonically increasing device word. Every wave that runs the loop ends it with exactly one ticket past the last
+// block, so the word advances by nblk + waves per launch and the host knows the next launch's base without reading it.
+// Blocks are 64 columns x rpb rows (a multiple of kCombRows, the loads per lane in flight together): 16 rows for
+// narrow rows (many blocks for many waves), 64 for wide ones (C5's 10k flows: 4x fewer u64 atomics).
+constexpr uint32_t kCombRows = 16;
+constexpr uint32_t kCombCols = 64;
+struct RowCombine {
+    const uint32_t* rows;  // nullptr: nothing pending
+    uint32_t nrows, row_words, row_stride, flow_words, nflows;
+    uint64_t* counts;      // the pending launch's flow_counts / verdict_counts (either may be nullptr)
+    uint64_t* verdicts;
+    uint32_t* ticket;      // device word (per stream slot)
+    uint32_t base;         // its value when this launch starts
+    uint32_t rpb;          // rows per block
+    uint32_t ncolblk, nblk;
+};
+
 // Kernel parameters (passed by value).
 struct RxParams {
     const uint8_t* frames;
@@ -113,6 +133,8 @@ struct RxParams {
     uint32_t stage;          // launch the instantiation that stages result stores in registers (large frames)
     uint32_t split;          // launch the split (stream waves / finish waves) kernel (large frames)
     uint32_t small;          // launch the small-frame kernel (minimum-size frames)
+    uint32_t defer_rows;     // leave this launch's counter rows pending (no dk_flow_reduce_kernel after it)
+    RowCombine comb;         // a previous launch's pending rows, combined in this launch
     dk_rx_results res;
 };
 
@@ -136,6 +158,9 @@ constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFa
 }
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
+// dk_flow_reduce_kernel over rows left pending by a deferred launch (dk_rx_counts_flush and the scratch paths).
+int dk_launch_reduce(const dk::RowCombine& q, void* stream);
 uint32_t dk_rx_small_block_waves();  // waves per workgroup of the small-frame kernel
+uint32_t dk_rx_comb_waves(uint32_t family);  // waves per workgroup that run the pending-rows combine loop
 int dk_tx_resident_blocks();  // occupancy of dk_tx_kernel per CU (0 on error)
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream);

@@ -26,13 +26,21 @@ constexpr uint32_t kDefaultChunkFrames = 1u << 16;
 constexpr uint64_t kMaxChunkBytes = 256ull << 20;
 constexpr size_t kMaxStreamSlots = 8;
 
-// Counter scratch of one stream's launches: the per-workgroup counter rows (flush_counters, rx_kernels.hip), which
-// dk_flow_reduce_kernel adds up after the receive kernel, and the small-frame kernel's deferral masks.
+// Counter scratch of one stream's launches: the per-workgroup counter rows (flush_counters, rx_kernels.hip) in two
+// halves (a launch writes one while the previous launch's rows may still be pending in the other), the small-frame
+// kernel's deferral masks, and the pending-rows state of DK_RX_BATCH_DEFER_COUNTS: the rows of the last deferred launch,
+// which the next launch on the stream adds to that launch's counters in-kernel (RowCombine, rx_common.h), or
+// dk_rx_counts_flush with dk_flow_reduce_kernel.
 struct CountScratch {
     uint32_t* rows = nullptr;
-    size_t rows_words = 0;
+    size_t rows_words = 0;   // words per half
+    uint32_t half = 0;       // the half the next launch writes
     uint64_t* defer = nullptr;  // the small-frame kernel's per-chunk deferral masks
     size_t ndefer = 0;
+    uint32_t* ticket = nullptr;  // the combine's ticket word (device)
+    uint32_t ticket_base = 0;    // its value once every launch issued so far has run
+    bool pending = false;
+    dk::RowCombine pend{};       // rows, nrows, row_words, row_stride, flow_words, nflows, counts, verdicts
 };
 
 // A context's scratch is keyed by stream: calls on different streams never share counter rows, so their
@@ -196,11 +204,21 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
     return 0;
 }
 
-void free_slot(StreamSlot& s) {  // the caller has waited for the slot's launches
+void free_slot(StreamSlot& s) {  // the caller has flushed and waited for the slot's launches
     if (s.cs.rows) (void)hipFree(s.cs.rows);
     if (s.cs.defer) (void)hipFree(s.cs.defer);
+    if (s.cs.ticket) (void)hipFree(s.cs.ticket);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
+}
+
+// Add the slot's pending counter rows (a deferred launch's) to their counters: dk_flow_reduce_kernel on the slot's
+// stream, after that launch.
+int flush_pending(StreamSlot& s) {
+    if (!s.used || !s.cs.pending) return 0;
+    s.cs.pending = false;
+    s.recorded = false;  // the slot's event no longer follows its last launch
+    return dk_launch_reduce(s.cs.pend, s.stream) ? EIO : 0;
 }
 
 // Wait (host side) for every launch that used the slot: its recorded event, else its stream; if neither can be waited
@@ -241,6 +259,8 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
         for (StreamSlot& s : c->slots)
             if (s.stamp < pick->stamp) pick = &s;
         c->saturated = true;
+        if (flush_pending(*pick)) return EIO;  // its deferred rows reach their counters on the old stream first
+        pick->recorded = false;
         bool ordered = pick->recorded;
         if (!ordered && hipEventRecord(pick->last, pick->stream) == hipSuccess) ordered = true;
         if (ordered) {
@@ -257,17 +277,27 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
     return 0;
 }
 
-// Rows for `grid` workgroups and `ndefer` deferral masks. Growing waits for the slot's last launch before freeing.
+// Rows for `grid` workgroups (two halves) and `ndefer` deferral masks, and the combine's ticket word. Growing flushes
+// the slot's pending rows and waits for its launches before freeing.
 int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, size_t ndefer) {
     CountScratch& cs = s.cs;
+    if (!cs.ticket) {
+        if (hipMalloc(&cs.ticket, sizeof(uint32_t)) != hipSuccess) {
+            cs.ticket = nullptr;
+            return ENOMEM;
+        }
+        if (hipMemsetAsync(cs.ticket, 0, sizeof(uint32_t), s.stream) != hipSuccess) return EIO;
+        cs.ticket_base = 0;
+    }
     const size_t words = (size_t)grid * row_stride;
     if (cs.rows_words >= words && cs.ndefer >= ndefer) return 0;
+    if (flush_pending(s)) return EIO;
     if (hipStreamSynchronize(s.stream) != hipSuccess) return EIO;  // launches still using the old buffers
     if (cs.rows_words < words) {
         if (cs.rows) (void)hipFree(cs.rows);
         cs.rows = nullptr;
         cs.rows_words = 0;
-        if (hipMalloc(&cs.rows, words * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+        if (hipMalloc(&cs.rows, 2 * words * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
         cs.rows_words = words;
     }
     if (cs.ndefer < ndefer) {
@@ -283,7 +313,7 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, size_t ndef
 // Choose the flow-count mode and the persistent grid, then launch on `stream` with that stream's counter scratch.
 // size_hint = bytes of blob the batch covers (the family and grid follow the mean bytes per frame).
 
-int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t stream) {
+int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t stream, bool defer) {
     if (p.n == 0) return 0;
     const Tuning& T = c->tune;
     const uint32_t ntiles = (p.n + 255) / 256;
@@ -354,27 +384,63 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
-    // Per-workgroup histogram rows (flow pairs, then verdicts; dk_flow_reduce_kernel adds them up) and the small-frame
-    // kernel's deferral masks: a launch that needs either uses the stream's scratch slot.
+    // Per-workgroup histogram rows (flow pairs, then verdicts; dk_flow_reduce_kernel adds them up, or the next launch
+    // on the stream when this one defers them) and the small-frame kernel's deferral masks: a launch that needs either,
+    // or that has a previous launch's rows to combine, uses the stream's scratch slot.
     StreamSlot* slot = nullptr;
     int rc = 0;
+    bool has_pending = false;
+    for (StreamSlot& s : c->slots)
+        if (s.used && s.stream == stream && s.cs.pending) has_pending = true;
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
     // per (wave, chunk): at most ceil(n / 64) + 2 chunks per wave of the grid (sched 1's partial chunks)
     const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * dk_rx_small_block_waves() : 0;
-    if (p.row_words || ndefer) {
+    if (p.row_words || ndefer || has_pending) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
         if (p.row_words)
             p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
         if ((rc = ensure_counts(*slot, grid, p.row_stride, ndefer))) return rc;
-        if (p.row_words) p.flow_scratch = slot->cs.rows;
+        if (p.row_words) p.flow_scratch = slot->cs.rows + (size_t)slot->cs.half * slot->cs.rows_words;
         p.defer = slot->cs.defer;
     }
+    CountScratch* cs = slot ? &slot->cs : nullptr;
+    p.comb = dk::RowCombine{};
+    if (cs && cs->pending) {  // the previous deferred launch's rows (in the other half) are added inside this launch
+        p.comb = cs->pend;
+        p.comb.ticket = cs->ticket;
+        p.comb.base = cs->ticket_base;
+        p.comb.rpb = p.comb.row_words > 16 * dk::kCombCols ? 4 * dk::kCombRows : dk::kCombRows;
+        p.comb.ncolblk = (p.comb.row_words + dk::kCombCols - 1) / dk::kCombCols;
+        p.comb.nblk = p.comb.ncolblk * ((p.comb.nrows + p.comb.rpb - 1) / p.comb.rpb);
+    }
+    p.defer_rows = defer && p.row_words ? 1u : 0u;
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
-                        "small=%u lds_table=%u\n",
+                        "small=%u lds_table=%u defer=%u combine=%u\n",
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
-                p.small, p.lt_words ? p.lt_n : 0u);
+                p.small, p.lt_words ? p.lt_n : 0u, p.defer_rows, p.comb.nblk);
     rc = dk_launch_rx(p, grid, stream);
+    if (rc == 0 && cs) {
+        if (p.comb.rows) {  // every wave of the grid that runs the combine loop ends it with one ticket past the blocks
+            cs->ticket_base += p.comb.nblk + grid * dk_rx_comb_waves(family);
+            cs->pending = false;
+        }
+        if (p.row_words) {
+            if (p.defer_rows) {
+                cs->pend = dk::RowCombine{};
+                cs->pend.rows = p.flow_scratch;
+                cs->pend.nrows = grid;
+                cs->pend.row_words = p.row_words;
+                cs->pend.row_stride = p.row_stride;
+                cs->pend.flow_words = p.flow_words;
+                cs->pend.nflows = p.nflows;
+                cs->pend.counts = p.flow_mode == dk::kFlowLds ? p.res.flow_counts : nullptr;
+                cs->pend.verdicts = p.res.verdict_counts;
+                cs->pending = true;
+            }
+            cs->half ^= 1u;
+        }
+    }
     if (rc == 0 && slot && (DK_SLOT_EVENTS || c->saturated)) {
         if (hipEventRecord(slot->last, stream) != hipSuccess) return EIO;
         slot->recorded = true;
@@ -454,6 +520,13 @@ extern "C" {
 
 uint32_t dk_rx_abi_version(void) { return DK_RX_ABI_VERSION; }
 
+#ifndef DK_BUILD_ID
+#define DK_BUILD_ID "unversioned"
+#endif
+// The marker prefix lets __graft_entry__ read the id from the file without loading the library.
+static const char kBuildIdMarker[] = "DK_BUILD_ID=" DK_BUILD_ID;
+const char* dk_rx_build_id(void) { return kBuildIdMarker + 12; }
+
 int dk_rx_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -497,8 +570,9 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
 void dk_rx_ctx_destroy(dk_rx_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->cfg.device);
-    // Wait for this context's launches only: each slot's stream (or its last recorded event) and the pipeline's own
-    // streams; then free the scratch.
+    // Deferred counter rows reach their counters first; then wait for this context's launches only: each slot's
+    // stream (or its last recorded event) and the pipeline's own streams; then free the scratch.
+    for (StreamSlot& s : c->slots) (void)flush_pending(s);
     for (StreamSlot& s : c->slots) wait_slot(s);
     for (Stage& s : c->stages)
         if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -590,7 +664,15 @@ int dk_rx_process(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, vo
     p.n = b->n;
     p.aligned16 = (b->flags & DK_RX_BATCH_ALIGNED16) ? 1u : 0u;
     p.res = *r;
-    return launch_batch(c, p, b->frames_bytes, (hipStream_t)stream);
+    return launch_batch(c, p, b->frames_bytes, (hipStream_t)stream, (b->flags & DK_RX_BATCH_DEFER_COUNTS) != 0);
+}
+
+int dk_rx_counts_flush(dk_rx_ctx* c, void* stream) {
+    if (!c) return EINVAL;
+    DeviceGuard g(c->cfg.device);
+    for (StreamSlot& s : c->slots)
+        if (s.used && s.stream == (hipStream_t)stream) return flush_pending(s);
+    return 0;
 }
 
 int dk_rx_stream_forget(dk_rx_ctx* c, void* stream) {
@@ -598,6 +680,7 @@ int dk_rx_stream_forget(dk_rx_ctx* c, void* stream) {
     DeviceGuard g(c->cfg.device);
     for (StreamSlot& s : c->slots) {
         if (!s.used || s.stream != (hipStream_t)stream) continue;
+        if (flush_pending(s)) return EIO;
         const bool ok = s.recorded ? hipEventSynchronize(s.last) == hipSuccess
                                    : hipStreamSynchronize(s.stream) == hipSuccess;
         if (!ok) return EIO;
@@ -715,7 +798,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
         }
         p.res.flow_counts = r->flow_counts ? c->d_flow_counts : nullptr;
         p.res.verdict_counts = r->verdict_counts ? c->d_verdict_counts : nullptr;
-        rc = launch_batch(c, p, ch.hi - ch.lo, st.stream);
+        rc = launch_batch(c, p, ch.hi - ch.lo, st.stream, false);  // synchronous: counters current at return
         if (rc) break;
         uint32_t* outs[9] = {r->meta, r->src_ip, r->dst_ip, r->ports, r->payload, r->flow_id,
                              r->tcp_seq, r->tcp_ack, r->tcp_win};
@@ -785,18 +868,20 @@ int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
     return hipMemcpy(out, c->d_path_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : EIO;
 }
 
-int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t knobs[DK_DIAG_RX_KNOBS]) {
-    if (!c || !knobs) return EINVAL;
+int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t* knobs, uint32_t nknobs) {
+    if (!c || (nknobs && !knobs)) return EINVAL;
     const int32_t zc = c->tune.host_zc;  // not a diag knob: kept from DK_RX_HOST_ZC
+    int32_t k[DK_DIAG_RX_KNOBS];
+    for (uint32_t i = 0; i < DK_DIAG_RX_KNOBS; i++) k[i] = i < nknobs ? knobs[i] : -1;
     Tuning t;
-    t.stage = knobs[0];
-    t.split = knobs[1];
-    t.small = knobs[2];
-    t.sched = knobs[3];
-    t.grid = knobs[4];
-    t.grid_per_cu = knobs[5];
-    t.debug = knobs[6];
-    t.lds_table = knobs[7];
+    t.stage = k[0];
+    t.split = k[1];
+    t.small = k[2];
+    t.sched = k[3];
+    t.grid = k[4];
+    t.grid_per_cu = k[5];
+    t.debug = k[6] < 0 ? 0 : k[6];
+    t.lds_table = k[7];
     t.host_zc = zc;
     c->tune = t;
     c->occ_family = ~0u;

@@ -1071,17 +1071,38 @@ __device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)
 
 // Per-chunk counters: the delivered frame's flow (packed-u16 LDS histogram, or a u64 global atomic for tables too
 // large for LDS) and one LDS add per distinct verdict per wave.
+// Flow counts are wave-aggregated while that pays: the first undone lane's flow takes every lane of the same flow in
+// one add of the popcount, and the rounds go on while a round gathers >= kFlowAggMin lanes; the lanes left over add
+// one each. One elephant flow (the tcp-echo shape, C1) is then one LDS add per chunk instead of 64 serialised adds on
+// one LDS word; many flows (C2, C5) pay one extra round.
+constexpr uint32_t kFlowAggMin = 4;
+__device__ __forceinline__ void flow_add(const RxParams& P, bool lds_flows, uint32_t* s_flow, uint32_t fid,
+                                         uint32_t cnt) {
+    if (lds_flows) atomicAdd(&s_flow[fid >> 1], cnt << ((fid & 1u) * 16));
+    else if (P.flow_mode == kFlowGlobal)
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), (unsigned long long)cnt);
+}
 __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32_t lane, uint32_t v, uint32_t fid,
                                             bool lds_flows, uint32_t* s_flow, uint32_t* s_vh) {
 #ifdef DK_ABL_NOCOUNT  // ablation (tuning only): no flow / verdict counting
     return;
 #endif
 #ifndef DK_ABL_NOFLOWCOUNT  // ablation (tuning only)
-    if (live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP)) {
-        if (lds_flows) atomicAdd(&s_flow[fid >> 1], 1u << ((fid & 1u) * 16));
-        else if (P.flow_mode == kFlowGlobal)
-            atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), 1ull);
+    const bool dl = live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP);
+#ifndef DK_FLOW_AGG_OFF  // ablation (tuning only): one add per delivered lane
+    uint64_t todo = __ballot(dl);
+    while (todo) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+        const uint32_t f0 = __builtin_amdgcn_readlane(fid, leader);
+        const uint64_t m = __ballot(fid == f0) & todo;
+        if (lane == leader) flow_add(P, lds_flows, s_flow, f0, (uint32_t)__popcll(m));
+        todo &= ~m;
+        if (__popcll(m) < kFlowAggMin) break;
     }
+    if ((todo >> lane) & 1u) flow_add(P, lds_flows, s_flow, fid, 1u);
+#else
+    if (dl) flow_add(P, lds_flows, s_flow, fid, 1u);
+#endif
 #endif
 #ifdef DK_ABL_NOVCOUNT  // ablation (tuning only)
     return;
@@ -1114,6 +1135,55 @@ __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, 
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
     if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
+}
+
+// Sum of one 64-column x rpb-row block of counter rows into the destination counters (the column sums of the
+// packed-u16 flow pairs, or a u32 verdict column), lane = column: kCombRows loads per lane in flight together per
+// batch, then one device-scope u64 atomic per nonzero counter.
+__device__ __forceinline__ void comb_block(const RowCombine& Q, uint32_t t, uint32_t lane) {
+    const uint32_t w = (t % Q.ncolblk) * kCombCols + lane;
+    const uint32_t r0 = (t / Q.ncolblk) * Q.rpb;
+    if (w >= Q.row_words) return;
+    const uint32_t r1 = min(Q.nrows, r0 + Q.rpb);
+    uint64_t lo = 0, hi = 0;
+    for (uint32_t rb = r0; rb < r1; rb += kCombRows) {
+        uint32_t x[kCombRows];
+#pragma unroll
+        for (uint32_t k = 0; k < kCombRows; k++) {
+            const uint32_t r = rb + k;
+            x[k] = r < r1 ? Q.rows[(size_t)r * Q.row_stride + w] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kCombRows; k++) {
+            lo += x[k] & 0xFFFFu;
+            hi += x[k] >> 16;
+        }
+    }
+    if (w >= Q.flow_words) {  // verdict column: a plain u32 count
+        const uint32_t v = w - Q.flow_words;
+        const uint64_t s = lo + (hi << 16);
+        if (s && v < DK_V_COUNT && Q.verdicts)
+            atomicAdd(reinterpret_cast<unsigned long long*>(Q.verdicts + v), (unsigned long long)s);
+        return;
+    }
+    if (!Q.counts) return;
+    if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(Q.counts + 2 * w), (unsigned long long)lo);
+    if (hi && 2 * w + 1 < Q.nflows)
+        atomicAdd(reinterpret_cast<unsigned long long*>(Q.counts + 2 * w + 1), (unsigned long long)hi);
+}
+
+// The previous launch's pending counter rows (RowCombine, rx_common.h): every calling wave takes blocks by ticket until
+// they run out (exactly one ticket past the last block per wave, which the host's next base counts on).
+__device__ __forceinline__ void combine_pending(const RxParams& P, uint32_t lane) {
+    const RowCombine& Q = P.comb;
+    if (!Q.rows) return;
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(Q.ticket, 1u);
+        t = (uint32_t)__builtin_amdgcn_readlane((int)t, 0) - Q.base;
+        if (t >= Q.nblk) break;
+        comb_block(Q, t, lane);
+    }
 }
 
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
@@ -1183,6 +1253,7 @@ void dk_rx_kernel(RxParams P) {
     }
 
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
+    combine_pending(P, lane);  // a previous launch's deferred counter rows, in this wave's tail
     __syncthreads();
     flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
 }
@@ -1571,6 +1642,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         }
     }
 #endif
+    combine_pending(P, lane);  // a previous launch's deferred counter rows, in this wave's tail
 #ifdef DK_DIAG_STAMPS
     DK_STAMP_T(14, __builtin_amdgcn_s_memtime());
 #endif
@@ -1671,6 +1743,9 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
     const Blob B(P.frames, P.frames_bytes);
+    // a previous launch's deferred counter rows: the finish waves have nothing to do until their stream wave's first
+    // chunk has landed
+    if (finisher) combine_pending(P, lane);
     Rec stg[kStg];
     uint32_t nstg = 0, klast = 0;
     uint32_t c, lim;
@@ -2068,7 +2143,7 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
 #ifdef DK_ABL_NOFLUSH
     if (false) {
 #else
-    if (p.row_words) {
+    if (p.row_words && !p.defer_rows) {
 #endif
         const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
                       (grid + dk::kReduceRows - 1) / dk::kReduceRows);
@@ -2077,6 +2152,19 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
         if (hipGetLastError() != hipSuccess) return 5;
     }
     return 0;
+}
+
+int dk_launch_reduce(const dk::RowCombine& q, void* stream) {
+    if (!q.rows || !q.nrows || !q.row_words) return 0;
+    const dim3 g2((q.row_words + dk::kReduceCols - 1) / dk::kReduceCols, (q.nrows + dk::kReduceRows - 1) / dk::kReduceRows);
+    hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, (hipStream_t)stream, q.rows, q.nrows,
+                       q.row_words, q.row_stride, q.flow_words, q.nflows, q.counts, q.verdicts);
+    return hipGetLastError() == hipSuccess ? 0 : 5;
+}
+
+uint32_t dk_rx_comb_waves(uint32_t family) {
+    // the split kernel's finish waves (one per stream wave), every wave of the other families
+    return family == dk::kFamilySmall ? dk::kSmallWaves : (uint32_t)dk::kWaves;
 }
 
 int dk_tx_resident_blocks() {

@@ -210,14 +210,28 @@ class RxEngine:
         return RxResults(n, self.nflows, device=torch.device("cuda", self.device), tcp_fields=tcp_fields,
                          counts=counts, dst_ip=dst_ip, tcp_opts=tcp_opts)
 
-    def receive_batch(self, batch: FrameBatch, results: RxResults, stream=None) -> None:
-        """Asynchronous on `stream` (a torch.cuda.Stream; default: the current stream)."""
+    def receive_batch(self, batch: FrameBatch, results: RxResults, stream=None, defer_counts: bool = False) -> None:
+        """Asynchronous on `stream` (a torch.cuda.Stream; default: the current stream). defer_counts: the
+        DK_RX_BATCH_DEFER_COUNTS flag — this batch's counter increments land with the next receive_batch on the same
+        stream (inside its kernel) or flush_counts()."""
         import torch
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         b, r = batch.c_struct(), results.c_struct()
+        if defer_counts:
+            b.flags |= N.DK_RX_BATCH_DEFER_COUNTS
         _check(self.lib.dk_rx_process(self._ctx, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(s.cuda_stream)),
                "dk_rx_process")
+
+    def flush_counts(self, stream=None) -> None:
+        """dk_rx_counts_flush: the counters of a deferred batch on `stream` become current (one small launch)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(self.lib.dk_rx_counts_flush(self._ctx, ctypes.c_void_p(s.cuda_stream)), "dk_rx_counts_flush")
+
+    def build_id(self) -> str:
+        return self.lib.dk_rx_build_id().decode()
 
     def forget_stream(self, stream) -> None:
         """dk_rx_stream_forget: release this context's scratch of `stream` (a torch.cuda.Stream or a raw hipStream_t
@@ -254,7 +268,7 @@ class RxEngine:
         bad = set(knobs) - set(N.DK_DIAG_RX_KNOBS)
         assert not bad, bad
         arr = (ctypes.c_int32 * len(N.DK_DIAG_RX_KNOBS))(*[int(knobs.get(k, -1)) for k in N.DK_DIAG_RX_KNOBS])
-        _check(self.lib.dk_diag_rx_set_tuning(self._ctx, arr), "dk_diag_rx_set_tuning")
+        _check(self.lib.dk_diag_rx_set_tuning(self._ctx, arr, len(N.DK_DIAG_RX_KNOBS)), "dk_diag_rx_set_tuning")
 
     def counts_allreduce(self, results: RxResults, comm: int, stream=None) -> None:
         """dk_rx_flow_counts_allreduce: sum this batch's device counters over every rank of `comm` (an RCCL

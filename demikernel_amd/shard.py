@@ -8,8 +8,8 @@ their GPU; frame bytes never cross xGMI.
 
 `ShardedReceiver` is the per-rank driver bench.py --gpus N runs (one process per GPU under torchrun): it bootstraps
 the RCCL communicator (rank 0's id handed out over the launcher's process group), receives the rank's shard into
-accumulating counters and all-reduces them out of place on a side stream, so the reduction of batch k overlaps the
-kernel of batch k + 1 and no step zeroes anything. The CPU rehearsal (tests/test_multiproc.py, gloo, world size 2)
+accumulating counters (each batch's counter rows completed inside the next batch's kernel) and all-reduces them out of
+place on a side stream, overlapping the following kernels; no step zeroes anything. The CPU rehearsal (tests/test_multiproc.py, gloo, world size 2)
 drives the same sharding and bootstrap code with torch's all_reduce standing in for the RCCL call; on the GPU the
 RCCL call runs through a 1-rank communicator test, and bench.py --gpus 2 runs as two child ranks on one GPU
 (tests/test_gpu_multiproc.py, gloo counts: RCCL refuses two ranks on one device).
@@ -77,18 +77,21 @@ class TorchCountsAllreduce:
 
 class ShardedReceiver:
     """One rank of a packet-sharded receive: its engine, its RCCL communicator, and `nbuf` sets of accumulating
-    counters. The kernel adds every step's counts to the set of slot k % nbuf (never zeroed: no memset kernels on the
-    launch stream); after the kernel, dk_rx_flow_counts_allreduce_to sums that set over the ranks into the slot's
-    node-wide totals on a side stream, overlapping the next step's kernel, which adds to the other set. A set is reused
-    only after its previous all-reduce has read it (one event wait). The node-wide counts of every step so far are the
-    sum of the slots' totals (`counts()`). With comm=None (one GPU) there is one set and no collective."""
+    counters. Step k's kernel adds its counts to the set of slot k % nbuf (never zeroed: no memset kernels on the
+    launch stream). With `defer` (the default) the kernel leaves its counter rows pending (DK_RX_BATCH_DEFER_COUNTS) and
+    step k + 1's kernel adds them to step k's set inside its own launch, so no step pays a dependent second launch for
+    its counters; after that kernel, dk_rx_flow_counts_allreduce_to sums step k's set over the ranks into the slot's
+    node-wide totals on a side stream, overlapping the following kernels. A set is changed again only after its
+    previous all-reduce has read it (one event wait). flush() completes the last step (one small launch, then its
+    all-reduce). The node-wide counts of every step so far are the sum of the slots' totals (`counts()`). With
+    comm=None (one GPU) there is one set and no collective."""
 
-    def __init__(self, engine, results, comm, stream, nbuf: int = 2):
+    def __init__(self, engine, results, comm, stream, nbuf: int = 2, defer: bool = True):
         import torch
 
         from .rx import RxResults
 
-        self.eng, self.comm, self.stream = engine, comm, stream
+        self.eng, self.comm, self.stream, self.defer = engine, comm, stream, defer
         if comm is None:
             nbuf = 1
         self.side = torch.cuda.Stream(device=stream.device) if comm is not None else None
@@ -104,6 +107,7 @@ class ShardedReceiver:
             if comm is not None else None
         self.done = [None] * nbuf
         self.k = 0
+        self.pending = None  # the slot whose counters wait for the next launch (deferred rows)
 
     def reduce(self, slot: int, stream) -> None:
         """The slot's node-wide totals from every rank's accumulated set (on `stream`)."""
@@ -113,25 +117,49 @@ class ShardedReceiver:
         else:
             self.eng.counts_allreduce_to(r, fo, vo, self.comm.handle, stream=stream)
 
-    def step(self, batch) -> None:
+    def _allreduce_after(self, slot: int) -> None:
+        """All-reduce `slot`'s set on the side stream once the launch stream has completed its counts."""
         import torch
 
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self.side.wait_event(ev)
+        self.reduce(slot, self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        self.done[slot] = done
+
+    def step(self, batch) -> None:
         slot = self.k % len(self.res)
-        r = self.res[slot]
-        if self.done[slot] is not None:  # the set's previous all-reduce has read it before the kernel adds to it
-            self.stream.wait_event(self.done[slot])
-        self.eng.receive_batch(batch, r, stream=self.stream)
+        prev = self.pending
+        # the set this launch changes: deferred, only the pending one it completes (its own rows stay pending);
+        # otherwise its own
+        changed = prev if self.defer else slot
+        if changed is not None and self.done[changed] is not None:
+            self.stream.wait_event(self.done[changed])  # the set's previous all-reduce has read it first
+        self.eng.receive_batch(batch, self.res[slot], stream=self.stream, defer_counts=self.defer)
         if self.comm is not None:
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-            self.side.wait_event(ev)
-            self.reduce(slot, self.side)
-            done = torch.cuda.Event()
-            done.record(self.side)
-            self.done[slot] = done
+            if self.defer and prev is not None:
+                self._allreduce_after(prev)
+            elif not self.defer:
+                self._allreduce_after(slot)
+        self.pending = slot if self.defer else None
         self.k += 1
 
+    def flush(self) -> None:
+        """Complete the last deferred step's counters (and, with a communicator, issue their all-reduce)."""
+        if self.pending is None:
+            return
+        s = self.pending
+        if self.done[s] is not None:
+            self.stream.wait_event(self.done[s])
+        self.eng.flush_counts(self.stream)
+        if self.comm is not None:
+            self._allreduce_after(s)
+        self.pending = None
+
     def drain(self) -> None:
+        self.flush()
         if self.side is not None:
             self.side.synchronize()
         self.stream.synchronize()

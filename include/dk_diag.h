@@ -35,7 +35,9 @@ int dk_diag_path_stats_read(struct dk_rx_ctx* ctx, uint64_t out[4]); /* synchron
  * grid / grid_per_cu fix the persistent grid, debug > 0 prints each launch's choice to stderr, lds_table 0 keeps Active
  * lookups on the global socket table (no LDS copy). */
 #define DK_DIAG_RX_KNOBS 8
-int dk_diag_rx_set_tuning(struct dk_rx_ctx* ctx, const int32_t knobs[DK_DIAG_RX_KNOBS]); /* 0 or EINVAL */
+/* knobs[0 .. nknobs): the caller says how many it passes (knobs past nknobs are -1, the rule), so a caller built
+ * against an older, shorter list never has its array read past its end. 0 or EINVAL. */
+int dk_diag_rx_set_tuning(struct dk_rx_ctx* ctx, const int32_t* knobs, uint32_t nknobs);
 /* The same for dk_tx_checksum (process-wide; first read from DK_TX_SPLIT, DK_RX_SCHED, DK_RX_GRID_PER_CU). */
 int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu); /* 0 */
 

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DK_RX_ABI_VERSION 3u
+#define DK_RX_ABI_VERSION 4u
 
 /* Frames at an address that is a multiple of this take the vectorised path (16-byte aligned frames directly, other
  * even addresses — e.g. NIC buffers with the Ethernet header at 2 mod 16 — through a realigned header window); any
@@ -58,6 +58,14 @@ extern "C" {
 #define DK_RX_BATCH_ALIGNED16 1u /* hint: frames are (mostly) at 16-byte aligned addresses; the engine launches its
                                     instantiation without the realignment path (other frames then take the byte path,
                                     still bit-exact) */
+
+#define DK_RX_BATCH_DEFER_COUNTS 2u /* leave this batch's flow / verdict counter contributions pending on `stream`
+                                       (per-workgroup partial rows in the context's scratch): the next dk_rx_process on
+                                       the same context and stream adds them to THIS batch's counters inside its own
+                                       kernel, or dk_rx_counts_flush does. Saves the dependent second launch
+                                       (dk_flow_reduce_kernel) per batch when batches follow each other; the counters
+                                       are current once a later launch on the stream, or a flush, has run. Ignored by
+                                       dk_rx_process_host (synchronous, counters current at return). */
 
 /* Largest frame blob of one batch (bytes): offsets are u32 and the engine keeps 256 bytes of the 32-bit range for its
  * out-of-range loads. */
@@ -190,7 +198,8 @@ typedef struct dk_tcp_opts {
  *           address; payload = 14 | (len - 14) << 16 (the buffer ArpPeer::receive takes). The sender / target
  *           hardware addresses are frame bytes [22, 28) and [32, 38).
  * For every other verdict the fields are 0 (flow_id DK_FLOW_NONE).
- * flow_counts[flow_id] and verdict_counts[verdict] are incremented (they accumulate across calls). */
+ * flow_counts[flow_id] and verdict_counts[verdict] are incremented (they accumulate across calls); with
+ * DK_RX_BATCH_DEFER_COUNTS the increments land one launch later (see the flag). */
 typedef struct dk_rx_results {
     uint32_t* meta;
     uint32_t* src_ip;
@@ -229,8 +238,15 @@ uint32_t dk_rx_flow_table_size(const dk_rx_ctx* ctx);
  * Returns 0, EINVAL (null required pointer, frames_bytes > DK_RX_MAX_BLOB) or EIO (launch failure). */
 int dk_rx_process(dk_rx_ctx* ctx, const dk_rx_batch* batch, const dk_rx_results* res, void* stream);
 
-/* Release the context's launch scratch of `stream` before the caller destroys that stream: waits for the stream's
- * work, then frees the slot for another stream. Returns 0 (also when the context never saw the stream) or EIO. */
+/* Add the counter contributions a DK_RX_BATCH_DEFER_COUNTS launch left pending on `stream` to that launch's
+ * flow_counts / verdict_counts: one small launch on `stream` (nothing when nothing is pending). Asynchronous; the counters
+ * are current for work ordered after it on `stream`. Also done implicitly by the next dk_rx_process on the stream (in its
+ * kernel), dk_rx_stream_forget and dk_rx_ctx_destroy. Returns 0 or EIO. */
+int dk_rx_counts_flush(dk_rx_ctx* ctx, void* stream);
+
+/* Release the context's launch scratch of `stream` before the caller destroys that stream: flushes pending counters,
+ * waits for the stream's work, then frees the slot for another stream. Returns 0 (also when the context never saw the
+ * stream) or EIO. */
 int dk_rx_stream_forget(dk_rx_ctx* ctx, void* stream);
 
 /* Process a batch that lives in host memory (a NIC ring / raw-socket buffer / DPDK mempool): the kernel, with
@@ -267,6 +283,9 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
 const char* dk_rx_verdict_name(int verdict);
 int dk_rx_verdict_errno(int verdict); /* errno the reference returns for this verdict; 0 for deliver/divert/drop */
 uint32_t dk_rx_abi_version(void);
+/* Content hash of the sources, headers and compiler flags this library was built from (hex; "unversioned" for a build
+ * outside __graft_entry__.build()), so a test run can prove which build it loaded. */
+const char* dk_rx_build_id(void);
 int dk_rx_device_count(void);
 
 #ifdef __cplusplus

@@ -14,7 +14,17 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session", autouse=True)
 def _built():
-    """Build libdk_rx.so (gfx950) and the oracle once per session (no-op when up to date)."""
+    """The library under test is the checked-out tree's build. Without a GPU (this container): build libdk_rx.so
+    (gfx950) and the oracle once per session (no-op when the library's build id matches the tree). On a GPU box nothing
+    is built: the session stops unless the library's id equals the tree's content hash (__graft_entry__.tree_build_id),
+    and the GPU tests print the id they ran."""
     import __graft_entry__
+    import torch
 
-    __graft_entry__.build()
+    if not torch.cuda.is_available():
+        __graft_entry__.build()
+        return
+    got, want = __graft_entry__.lib_build_id(), __graft_entry__.tree_build_id()
+    if got != want:
+        pytest.exit(f"libdk_rx.so build id {got} != tree {want}: build on the CPU side first", returncode=3)
+    print(f"\nlibdk_rx.so build id {__graft_entry__.check_loaded_build()} (= tree)")

@@ -87,7 +87,10 @@ def test_tcp_header_constants():
 
 def test_verdict_tables():
     lib = N.load_library()
-    assert lib.dk_rx_abi_version() == 3
+    assert lib.dk_rx_abi_version() == 4
+    bid = lib.dk_rx_build_id().decode()
+    import __graft_entry__
+    assert bid == __graft_entry__.tree_build_id(), (bid, "the loaded library is not this tree's build")
     for i, name in enumerate(N.VERDICTS):
         assert lib.dk_rx_verdict_name(i).decode() == name
     assert lib.dk_rx_verdict_name(N.DK_V_COUNT).decode() == "UNKNOWN"

@@ -63,6 +63,14 @@ def _worker(rank, world, port, out_dir):
                 ok, msg = False, f"step {step}: reduced flow counts differ"
             if not np.array_equal(vc, (step + 1) * whole["verdict_counts"][: len(vc)]):
                 ok, msg = False, f"step {step}: reduced verdict counts differ"
+        for step in range(4):  # back-to-back steps: each kernel completes the previous step's deferred counters
+            sr.step(batch)
+        sr.drain()
+        fc, vc = sr.counts()
+        if not np.array_equal(fc.cpu().numpy().view(np.uint64), 7 * whole["flow_counts"][: len(fc)]):
+            ok, msg = False, "7 steps: reduced flow counts differ"
+        if not np.array_equal(vc.cpu().numpy().view(np.uint64), 7 * whole["verdict_counts"][: len(vc)]):
+            ok, msg = False, "7 steps: reduced verdict counts differ"
         got = res.to_numpy()
         for k in ("meta", "src_ip", "ports", "payload", "flow_id"):
             if not np.array_equal(got[k], mine[k]):

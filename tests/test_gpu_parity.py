@@ -859,6 +859,77 @@ def test_counter_rows_accumulate(torch_cuda, monkeypatch, family):
         assert np.array_equal(got["meta"], exp["meta"]) and np.array_equal(got["flow_id"], exp["flow_id"]), ctx
 
 
+@pytest.mark.parametrize("family", ["staged", "split", "small", "unstaged"])
+def test_deferred_counts(torch_cuda, monkeypatch, family):
+    """DK_RX_BATCH_DEFER_COUNTS: a launch leaves its counter rows pending and the next launch on the stream adds them to
+    the deferred launch's counters inside its own kernel (ticketed blocks, RowCombine), or dk_rx_counts_flush does.
+    Per kernel family and grid (7 workgroups, the default, 1,500; > 32,768 flows: verdict rows only): two counter sets
+    alternated with deferral, a launch without counters completing the pending rows, grid growth with rows pending
+    (flush before the scratch grows), a flush, 12 streams with deferred rows (slot takeovers flush them), and a pending
+    launch at dk_rx_stream_forget and at context destruction — every set ends at exactly k x the oracle's counts and
+    every per-frame result is the oracle's."""
+    import torch
+
+    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
+    monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
+    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
+    for n, nflows, grid in [(20000, 700, None), (20000, 700, "7"), (150000, 700, "1500"), (9000, 40000, None)]:
+        if grid is None:
+            monkeypatch.delenv("DK_RX_GRID", raising=False)
+        else:
+            monkeypatch.setenv("DK_RX_GRID", grid)
+        flows = np.concatenate([synth.make_flows(nflows, passive=False), synth.make_flows(8, kind="udp")])
+        ip_len = 50 if family == "small" else synth.imix_ip_lengths(n, seed=n)
+        tr = synth.traffic(n, ip_len, flows, seed=nflows + 1)
+        blob, off, lens = synth.build_numpy(tr)
+        synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
+        exp = run_oracle(blob, off, lens, flows)
+        ctx = f"{family} n={n} flows={nflows} grid={grid}"
+        small = FrameBatch.from_numpy(blob[: int(off[99]) + int(lens[99])], off[:100], lens[:100])
+        exp_small = run_oracle(blob, off[:100], lens[:100], flows)
+
+        def check_counts(r, k, e=exp, what=""):
+            got = r.to_numpy()
+            assert np.array_equal(got["flow_counts"], k * e["flow_counts"][: len(got["flow_counts"])]), (ctx, what)
+            assert np.array_equal(got["verdict_counts"], k * e["verdict_counts"]), (ctx, what)
+
+        eng = RxEngine(Config(LOCAL), device=0)
+        eng.set_sockets(flows)
+        b = FrameBatch.from_numpy(blob, off, lens, device=0)
+        ra, rb = eng.results(n), eng.results(n)
+        rs = eng.results(100)
+        s = torch.cuda.current_stream()
+        for who in "ABAAB":  # alternating sets, every launch deferred
+            eng.receive_batch(b, ra if who == "A" else rb, stream=s, defer_counts=True)
+        scratch = eng.results(n, counts=False)
+        eng.receive_batch(b, scratch, stream=s)  # no counters of its own: completes B's pending rows
+        torch.cuda.synchronize()
+        check_counts(ra, 3, what="A after 5 deferred")
+        check_counts(rb, 2, what="B completed by a launch without counters")
+        got = ra.to_numpy()
+        for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id"):
+            assert np.array_equal(got[k], exp[k]), (ctx, k)
+        # a small grid's rows pending, then a launch that needs more rows (the scratch grows: pending flushed first)
+        eng.receive_batch(small, rs, stream=s, defer_counts=True)
+        eng.receive_batch(b, ra, stream=s, defer_counts=True)
+        eng.flush_counts(s)
+        eng.flush_counts(s)  # nothing pending: no-op
+        torch.cuda.synchronize()
+        check_counts(rs, 1, exp_small, "small batch completed before the scratch grew")
+        check_counts(ra, 4, what="A flushed")
+        # more streams than scratch slots, each with rows pending: a takeover flushes the victim's rows on its stream
+        streams = [torch.cuda.Stream() for _ in range(12)]
+        for st in streams:
+            eng.receive_batch(b, rb, stream=st, defer_counts=True)
+        for st in streams[:6]:
+            eng.forget_stream(st)  # flushes and waits
+        eng.receive_batch(small, rs, stream=streams[7], defer_counts=True)
+        eng.close()  # flushes whatever is still pending, waits, frees
+        torch.cuda.synchronize()
+        check_counts(rb, 2 + 12, what="12 streams, takeovers, forget, close")
+        check_counts(rs, 2, exp_small, "pending at close")
+
+
 @pytest.mark.parametrize("mix", ["tcp1500", "udp64", "imix"])
 def test_aligned_traffic_stays_on_vector_path(torch_cuda, mix):
     """Performance guard (dk_diag path counters): well-formed 64-byte-slot traffic never falls back to the byte-load
