@@ -1,0 +1,84 @@
+// lds_table.h — host builder of the LDS copy of the Active socket table (rx_common.h: minimal perfect hash). Host code
+// only (no HIP calls), so the ASan + UBSan harness (tests/host_asan) links it too.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+#include "rx_common.h"
+
+namespace dk {
+
+// From the built open-addressing slots (so duplicates resolve exactly as there), the Active connections with
+// local_ip == cfg_ip (the only ones a reference lookup can ask for). Buckets are placed largest first, each with the
+// smallest displacement that puts all its keys on free slots. Returns false (no LDS table: lookups probe the global
+// table) for no keys, more than kLtMaxKeys, keys whose 32-bit hashes collide (they can never be separated: checked up
+// front on the sorted hashes, so such a table costs no displacement search), or no displacement below 2^20 for a
+// bucket.
+inline bool build_lds_table(const std::vector<uint32_t>& slots, uint32_t cap, uint32_t cfg_ip,
+                            std::vector<uint32_t>& out, uint32_t& n_out, uint32_t& b_out) {
+    struct Key {
+        uint32_t h, rip, ports, fid;
+    };
+    std::vector<Key> keys;
+    if (slots.size() < (size_t)cap * 4) return false;
+    for (uint32_t i = 0; i < cap; i++) {
+        const uint32_t* sl = &slots[(size_t)i * 4];
+        if (sl[0] == 0 || (sl[0] >> 24) != DK_FLOW_TCP_ACTIVE || sl[1] != cfg_ip) continue;
+        if (keys.size() >= kLtMaxKeys) return false;
+        keys.push_back({flow_hash(DK_FLOW_TCP_ACTIVE, cfg_ip, sl[2], sl[3]), sl[2], sl[3], sl[0] & 0xFFFFFFu});
+    }
+    const uint32_t n = (uint32_t)keys.size();
+    if (n == 0) return false;
+    {
+        std::vector<uint32_t> hs(n);
+        for (uint32_t k = 0; k < n; k++) hs[k] = keys[k].h;
+        std::sort(hs.begin(), hs.end());
+        if (std::adjacent_find(hs.begin(), hs.end()) != hs.end()) return false;  // two keys, one hash
+    }
+    const uint32_t nb = (n + 3) / 4;
+    std::vector<std::vector<uint32_t>> bucket(nb);
+    for (uint32_t k = 0; k < n; k++) bucket[lt_bucket(keys[k].h, nb)].push_back(k);
+    std::vector<uint32_t> order(nb);
+    for (uint32_t b = 0; b < nb; b++) order[b] = b;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return bucket[a].size() > bucket[b].size(); });
+    std::vector<uint8_t> taken(n, 0);
+    std::vector<uint32_t> disp(nb, 0), slot_of(n, 0), at;
+    for (uint32_t b : order) {
+        if (bucket[b].empty()) break;
+        uint32_t d = 0;
+        for (;; d++) {
+            if (d >= (1u << 20)) return false;
+            at.clear();
+            bool ok = true;
+            for (uint32_t k : bucket[b]) {
+                const uint32_t sl = lt_slot(keys[k].h, d, n);
+                if (taken[sl] || std::find(at.begin(), at.end(), sl) != at.end()) {
+                    ok = false;
+                    break;
+                }
+                at.push_back(sl);
+            }
+            if (ok) break;
+        }
+        disp[b] = d;
+        for (size_t j = 0; j < at.size(); j++) {
+            taken[at[j]] = 1;
+            slot_of[bucket[b][j]] = at[j];
+        }
+    }
+    out.assign(lt_words(n, nb), 0u);
+    for (uint32_t k = 0; k < n; k++) {
+        out[slot_of[k]] = keys[k].rip;
+        out[n + slot_of[k]] = keys[k].ports;
+        out[2 * n + slot_of[k]] = keys[k].fid;
+    }
+    std::copy(disp.begin(), disp.end(), out.begin() + 3 * n);
+    n_out = n;
+    b_out = nb;
+    return true;
+}
+
+}  // namespace dk

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <vector>
 
+#include "lds_table.h"
 #include "rx_common.h"
 #include "rx_plan.h"
 
@@ -127,68 +128,6 @@ int32_t env_knob(const char* name) {
     return e ? (int32_t)atoi(e) : -1;
 }
 
-// The LDS Active table (rx_common.h): a minimal perfect hash of the Active connections with local_ip == cfg_ip, taken
-// from the built open-addressing slots (so duplicates resolve exactly as there). Buckets are placed largest first,
-// each with the smallest displacement that puts all its keys on free slots. Returns false (no LDS table: lookups probe
-// the global table) for no keys, too many, or keys whose 32-bit hashes collide (never separable).
-bool build_lds_table(const std::vector<uint32_t>& slots, uint32_t cap, uint32_t cfg_ip, std::vector<uint32_t>& out,
-                     uint32_t& n_out, uint32_t& b_out) {
-    struct Key {
-        uint32_t h, rip, ports, fid;
-    };
-    std::vector<Key> keys;
-    for (uint32_t i = 0; i < cap; i++) {
-        const uint32_t* sl = &slots[(size_t)i * 4];
-        if (sl[0] == 0 || (sl[0] >> 24) != DK_FLOW_TCP_ACTIVE || sl[1] != cfg_ip) continue;
-        if (keys.size() >= dk::kLtMaxKeys) return false;
-        keys.push_back({dk::flow_hash(DK_FLOW_TCP_ACTIVE, cfg_ip, sl[2], sl[3]), sl[2], sl[3], sl[0] & 0xFFFFFFu});
-    }
-    const uint32_t n = (uint32_t)keys.size();
-    if (n == 0) return false;
-    const uint32_t nb = (n + 3) / 4;
-    std::vector<std::vector<uint32_t>> bucket(nb);
-    for (uint32_t k = 0; k < n; k++) bucket[dk::lt_bucket(keys[k].h, nb)].push_back(k);
-    std::vector<uint32_t> order(nb);
-    for (uint32_t b = 0; b < nb; b++) order[b] = b;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t a, uint32_t b) { return bucket[a].size() > bucket[b].size(); });
-    std::vector<uint8_t> taken(n, 0);
-    std::vector<uint32_t> disp(nb, 0), slot_of(n, 0), at;
-    for (uint32_t b : order) {
-        if (bucket[b].empty()) break;
-        uint32_t d = 0;
-        for (;; d++) {
-            if (d >= (1u << 20)) return false;
-            at.clear();
-            bool ok = true;
-            for (uint32_t k : bucket[b]) {
-                const uint32_t sl = dk::lt_slot(keys[k].h, d, n);
-                if (taken[sl] || std::find(at.begin(), at.end(), sl) != at.end()) {
-                    ok = false;
-                    break;
-                }
-                at.push_back(sl);
-            }
-            if (ok) break;
-        }
-        disp[b] = d;
-        for (size_t j = 0; j < at.size(); j++) {
-            taken[at[j]] = 1;
-            slot_of[bucket[b][j]] = at[j];
-        }
-    }
-    out.assign(dk::lt_words(n, nb), 0u);
-    for (uint32_t k = 0; k < n; k++) {
-        out[slot_of[k]] = keys[k].rip;
-        out[n + slot_of[k]] = keys[k].ports;
-        out[2 * n + slot_of[k]] = keys[k].fid;
-    }
-    std::copy(disp.begin(), disp.end(), out.begin() + 3 * n);
-    n_out = n;
-    b_out = nb;
-    return true;
-}
-
 int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask) {
     uint32_t* d = nullptr;
     if (hipMalloc(&d, slots.size() * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
@@ -196,6 +135,8 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
         (void)hipFree(d);
         return EIO;
     }
+    // Launches still in flight may read the old table (any stream, including ones that take no scratch slot): this
+    // relies on hipFree synchronizing the device before it releases memory (HIP runtime semantics).
     if (c->table) (void)hipFree(c->table);
     c->table = d;
     c->table_mask = mask;
@@ -570,8 +511,10 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
 void dk_rx_ctx_destroy(dk_rx_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->cfg.device);
-    // Deferred counter rows reach their counters first; then wait for this context's launches only: each slot's
-    // stream (or its last recorded event) and the pipeline's own streams; then free the scratch.
+    // Deferred counter rows reach their counters first; then wait for the launches that use slot scratch (each slot's
+    // stream, or its last recorded event) and the pipeline's own streams, and free the scratch. A launch that took no
+    // slot (no counters, not the small-frame kernel) may still be reading the socket table: freeing the table relies on
+    // hipFree synchronizing the device first (HIP runtime semantics), as upload_table does.
     for (StreamSlot& s : c->slots) (void)flush_pending(s);
     for (StreamSlot& s : c->slots) wait_slot(s);
     for (Stage& s : c->stages)
@@ -632,7 +575,7 @@ int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
     uint32_t lt_n = 0, lt_b = 0, lt_w = 0;
     {
         std::vector<uint32_t> lt;
-        if (build_lds_table(slots, cap, cfg_ip, lt, lt_n, lt_b)) {
+        if (dk::build_lds_table(slots, cap, cfg_ip, lt, lt_n, lt_b)) {
             lt_w = (uint32_t)lt.size();
             slots.insert(slots.end(), lt.begin(), lt.end());
         }

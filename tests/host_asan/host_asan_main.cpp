@@ -17,6 +17,9 @@
 //   host_asan plan    in out   in:  u32 n | u64 frames_bytes | u32 chunk_n | u32 zc | u64 max_bytes | off u32[n] |
 //                                   len u16[n]
 //                              out: u64 max_span | u32 nchunks | per chunk: u32 a, u32 e, u64 lo, u64 hi
+//   host_asan ltable  in out   in:  u32 cap | u32 cfg_ip | slots u32[4 cap] (the Active table's open-addressing slots)
+//                              out: i32 built | u32 n | u32 nbuckets | u32 nwords | words u32[nwords]
+//                              (the LDS Active table builder of lds_table.h)
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -24,6 +27,7 @@
 #include <cstring>
 #include <vector>
 
+#include "../../demikernel_amd/csrc/lds_table.h"
 #include "../../demikernel_amd/csrc/rx_plan.h"
 #include "../../include/dk_demi.h"
 #include "../../include/dk_ring.h"
@@ -167,11 +171,26 @@ int do_plan() {
     }
     return 0;
 }
+
+int do_ltable() {
+    const uint32_t cap = rd1<uint32_t>(), cfg_ip = rd1<uint32_t>();
+    std::vector<uint32_t> slots((size_t)cap * 4);
+    rd(slots.data(), slots.size());
+    std::vector<uint32_t> words;
+    uint32_t n = 0, nb = 0;
+    const bool ok = dk::build_lds_table(slots, cap, cfg_ip, words, n, nb);
+    wr1<int32_t>(ok ? 1 : 0);
+    wr1<uint32_t>(ok ? n : 0);
+    wr1<uint32_t>(ok ? nb : 0);
+    wr1<uint32_t>(ok ? (uint32_t)words.size() : 0);
+    if (ok) wr(words.data(), words.size());
+    return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
     if (argc != 4) {
-        fprintf(stderr, "usage: %s ring|release|udp|tcp|plan in out\n", argv[0]);
+        fprintf(stderr, "usage: %s ring|release|udp|tcp|plan|ltable in out\n", argv[0]);
         return 2;
     }
     g_in = fopen(argv[2], "rb");
@@ -179,7 +198,7 @@ int main(int argc, char** argv) {
     if (!g_in || !g_out) return 2;
     const char* m = argv[1];
     int rc = !strcmp(m, "ring") ? do_ring(false) : !strcmp(m, "release") ? do_ring(true) : !strcmp(m, "udp") ? do_udp()
-             : !strcmp(m, "tcp") ? do_tcp() : !strcmp(m, "plan") ? do_plan() : 2;
+             : !strcmp(m, "tcp") ? do_tcp() : !strcmp(m, "plan") ? do_plan() : !strcmp(m, "ltable") ? do_ltable() : 2;
     fclose(g_out);
     fclose(g_in);
     return rc;

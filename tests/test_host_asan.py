@@ -277,3 +277,102 @@ def test_host_chunk_planner(driver, tmp_path):
         assert got == exp
         assert span == max([h - lo for _, _, lo, h in exp], default=0)
         assert sum(e - a for a, e, _, _ in got) == n  # every frame in exactly one chunk, in order
+
+
+# --- the LDS Active table builder (lds_table.h) -------------------------------------------------------------------
+M32 = 0xFFFFFFFF
+ACTIVE = N.DK_FLOW_TCP_ACTIVE
+
+
+def _flow_hash(kind, lip, rip, ports):  # rx_common.h flow_hash
+    h = (kind * 0x9E3779B1) & M32
+    h ^= lip
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h ^= rip
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    h ^= ports
+    h = (h * 0x27D4EB2F) & M32
+    h ^= h >> 15
+    return h
+
+
+def _h2(kind, lip, rip):  # flow_hash's state just before `ports` is mixed in (the rest is a bijection of h2 ^ ports)
+    h = (kind * 0x9E3779B1) & M32
+    h ^= lip
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h ^= rip
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    return h
+
+
+def _fmix(h):
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    return h
+
+
+def _mulhi(a, b):
+    return (int(a) * int(b)) >> 32
+
+
+def _lt_lookup(words, n, nb, lip, rip, ports):  # rx_kernels.hip lt_lookup, on the host
+    h = _flow_hash(ACTIVE, lip, rip, ports)
+    d = int(words[3 * n + _mulhi(h, nb)])
+    sl = _mulhi(_fmix(h ^ ((d * 0x9E3779B1 + 0x7F4A7C15) & M32)), n)
+    return int(words[2 * n + sl]) if int(words[sl]) == rip and int(words[n + sl]) == ports else None
+
+
+def _ltable(driver, tmp_path, keys, cfg_ip, other=()):
+    """keys: [(rip, ports, fid)] Active on cfg_ip; other: Active keys on another local address. Slots at random
+    distinct positions of a power-of-two table (the builder scans slots, it does not re-probe)."""
+    allk = [(cfg_ip, r, p, f) for r, p, f in keys] + list(other)
+    cap = 16
+    while cap < 2 * max(len(allk), 1):
+        cap *= 2
+    slots = np.zeros((cap, 4), np.uint32)
+    pos = np.random.default_rng(len(allk)).permutation(cap)[: len(allk)]
+    for (lip, r, p, f), at in zip(allk, pos):
+        slots[at] = (ACTIVE << 24 | f, lip, r, p)
+    out = run(driver, "ltable", np.array([cap, cfg_ip], np.uint32).tobytes() + slots.tobytes(), tmp_path)
+    ok, n, nb, nw = np.frombuffer(out[:16], np.int32)
+    return int(ok), int(n), int(nb), np.frombuffer(out[16:16 + 4 * nw], np.uint32)
+
+
+def test_lds_table_builder(driver, tmp_path):
+    """Random tables of 1..4096 keys: every key is found at its flow id, keys of another local address and keys not in
+    the table are not; 4097 keys, two keys with one 32-bit hash, and a duplicated key are refused up front (the
+    collision check runs before the displacement search, so a refusal is quick)."""
+    import time
+
+    rng = np.random.default_rng(5)
+    cfg = 0x0201A8C0
+    for nk in (1, 2, 3, 7, 64, 1000, 4096):
+        rips = rng.integers(1, 2**32, nk, dtype=np.uint64).astype(np.uint32)
+        ports = rng.integers(0, 2**32, nk, dtype=np.uint64).astype(np.uint32)
+        keys = [(int(r), int(p), k) for k, (r, p) in enumerate(zip(rips, ports))]
+        other = [(0x0A0A0A0A, int(rips[0]), int(ports[0]), nk + 5)]
+        ok, n, nb, words = _ltable(driver, tmp_path, keys, cfg, other)
+        assert ok and n == nk and nb == (nk + 3) // 4, (nk, ok, n, nb)
+        for r, p, f in keys:
+            assert _lt_lookup(words, n, nb, cfg, r, p) == f, (nk, r, p)
+        for _ in range(200):
+            assert _lt_lookup(words, n, nb, cfg, int(rng.integers(1, 2**32)), int(rng.integers(0, 2**32))) is None
+    keys = [(k + 1, k, k) for k in range(4097)]
+    assert _ltable(driver, tmp_path, keys, cfg)[0] == 0
+    # two distinct keys with one flow_hash: same h2 ^ ports
+    r1, p1, r2 = 0x01020304, 0x00500050, 0x0A0B0C0D
+    p2 = _h2(ACTIVE, cfg, r1) ^ p1 ^ _h2(ACTIVE, cfg, r2)
+    assert _flow_hash(ACTIVE, cfg, r1, p1) == _flow_hash(ACTIVE, cfg, r2, p2) and (r1, p1) != (r2, p2)
+    for base in (0, 5, 900):
+        extra = [(int(rng.integers(1, 2**32)), int(rng.integers(0, 2**32)), 10 + k) for k in range(base)]
+        t = time.perf_counter()
+        ok, *_ = _ltable(driver, tmp_path, extra + [(r1, p1, 1), (r2, p2, 2)], cfg)
+        assert ok == 0 and time.perf_counter() - t < 20
+    assert _ltable(driver, tmp_path, [(r1, p1, 1), (r1, p1, 2)], cfg)[0] == 0  # duplicated key

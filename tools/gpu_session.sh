@@ -16,12 +16,25 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# C1 (tcp-echo shape): kernel family and grid, counters on / off
-step c1_fam 240 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 "" "split=0" "split=0,stage=0" \
-  "split=0,grid_per_cu=2" "split=0,stage=0,grid_per_cu=2" "split=0,stage=0,grid_per_cu=8"
-step c1_nocount 240 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 --no-counts "" "split=0" \
-  "split=0,stage=0"
-# rocprofv3 kernel stats and HBM traffic of C1 at the host rule
+# 1. parity: the changed paths first, then the whole GPU suite
+PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+step t_defer 400 $PYT tests/test_gpu_parity.py -k "deferred_counts or counter_rows or flow_counter or two_streams or streams_destroyed"
+step t_multi 300 $PYT tests/test_gpu_multiproc.py
+step t_all 900 $PYT -m gpu tests
+step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
+# 2. deferred counters and the family choice on C1, and deferral on the other configs
+step c1_fam 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 "" "defer=1" "split=0" "split=0,defer=1" \
+  "split=0,stage=0" "split=0,stage=0,defer=1" "split=0,stage=0,grid_per_cu=8,defer=1"
+for wl in c2_tcp1500 c4_imix c5_tcp1500_10k; do
+  step ${wl}_defer 300 python3 tools/tune_ab.py --workload $wl --reps 7 --iters 10 "" "defer=1"
+done
+step c3_defer 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 16 "" "defer=1"
+# 3. flow-count aggregation A/B (variant without it)
+for wl in c1_tcp1078 c2_tcp1500 c5_tcp1500_10k; do
+  step ${wl}_agg 300 python3 tools/tune_ab.py --workload $wl --rotate 3 --reps 7 --iters 10 --lib demikernel_amd/libdk_rx.so \
+    --lib build/variants/aggoff.so "defer=1"
+done
+# 4. rocprofv3 kernel stats and HBM traffic of C1 at the host rule
 cd /tmp
 step c1_stats 200 rocprofv3 --kernel-trace --stats -T -d $O/c1_stats -o run --output-format csv -- \
   python3 $R/tools/kbench.py --workload c1_tcp1078 --rotate 3 --iters 20
