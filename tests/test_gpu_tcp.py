@@ -106,6 +106,21 @@ SCENARIOS = {
     "long_runs": (S.conns(rn=1), [(0, 1 + 10 * k, 1, S.ACK, 10) for k in range(150)] +
                   [(0, 3001, 1, S.ACK, 10), (0, 1, 1, S.ACK, 10)] +
                   [(0, 1501 + 10 * k, 1, S.ACK, 10) for k in range(149)] + [(0, 2991, 1, S.ACK, 20)]),
+    # segments the key pass classifies without a walk (past the window end: OUT_OF_WINDOW; ending before the table's
+    # RCV.NXT: DUPLICATE) queued behind a FIN / an RST that closes the connection become UNPROCESSED
+    # (dk_tcp_fix_kernel); before the close they keep their class
+    "fin_then_classified": (S.conns(rn=1001, bufsz=1000), [(0, 1001, 1, S.ACK, 10), (0, 1011, 1, S.FIN | S.ACK, 0),
+                                                           (0, 5000, 1, S.ACK, 10), (0, 1, 1, S.ACK, 10)]),
+    "rst_then_classified": (S.conns(rn=1001, bufsz=1000), [(0, 1001, 1, S.ACK, 10), (0, 1011, 1, S.RST, 0),
+                                                           (0, 5000, 1, S.ACK, 10), (0, 1, 1, S.ACK, 10)]),
+    "classified_then_close": (S.conns(rn=1001, bufsz=1000), [(0, 5000, 1, S.ACK, 10), (0, 1, 1, S.ACK, 10),
+                                                             (0, 1001, 1, S.ACK, 10), (0, 1011, 1, S.FIN | S.ACK, 0),
+                                                             (0, 6000, 1, S.ACK, 10)]),
+}
+EXPECT = {  # what the oracle says these scenarios must exercise (guards the scenarios themselves)
+    "fin_then_classified": ["DELIVERED", "FIN", "UNPROCESSED", "UNPROCESSED"],
+    "rst_then_classified": ["DELIVERED", "RST", "UNPROCESSED", "UNPROCESSED"],
+    "classified_then_close": ["OUT_OF_WINDOW", "DUPLICATE", "DELIVERED", "FIN", "UNPROCESSED"],
 }
 
 
@@ -119,6 +134,8 @@ def test_branch_scenarios(tcp, name):
                                      ("meta", "flow_id", "tcp_seq", "tcp_ack", "payload")}
     exp_t = table.copy()
     exp = O.tcp_process(exp_t, rx)
+    if name in EXPECT:
+        assert S.acts(exp) == EXPECT[name], S.acts(exp)
     got_t, got = gpu_process(tcp, table.copy(), rx_device(rx))
     assert_same(got_t, got, exp_t, exp, name)
 
@@ -192,3 +209,22 @@ def test_rejects_missing_tcp_fields(tcp):
     assert e.value.errno == 22
     h = ctypes.c_void_p()
     assert tcp.lib.dk_tcp_ctx_create(-1, ctypes.byref(h)) == 22
+
+
+def test_rejects_misaligned_conns(tcp):
+    """The connection table must be 16-byte aligned (dk_tcp_key_kernel reads a connection's head with one 16-byte
+    load): a table 4 bytes off is refused with EINVAL before any launch."""
+    import ctypes
+
+    import torch
+
+    rx = S.batch([(0, 1, 1, S.ACK, 10)])
+    r = rx_device(rx)
+    buf = torch.zeros(2 * N.CONN_DTYPE.itemsize + 16, dtype=torch.uint8, device="cuda")
+    out = TcpOut(1, 1)
+    rs, o = r.c_struct(), out.c_struct()
+    for shift in (4, 8, 12):
+        rc = tcp.lib.dk_tcp_rx_process(tcp._ctx, ctypes.byref(rs), 1, ctypes.c_void_p(buf.data_ptr() + shift), 1,
+                                       ctypes.byref(o), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 22, (shift, rc)
+    torch.cuda.synchronize()

@@ -93,3 +93,42 @@ def test_live_loopback_ring_through_engine():
         eng.close()
     finally:
         pr.close()
+
+
+@pytest.mark.gpu
+def test_captured_live_ring_through_engine():
+    """The kernel-filled ring captured on a host with CAP_NET_RAW (tests/golden/live_ring_lo.npz, made by
+    tests/golden/make_ring_fixture.py: Linux's own block descriptors and tpacket3 headers) replayed through
+    dk_rx_process_tpacket3 on the GPU — page-locked in place, block scan, H2D of the blocks' byte ranges, kernel, D2H —
+    bit-exact against the oracle over the same ring bytes, for every frame in the ring (ours and any other traffic on
+    `lo` at capture time). The GPU boxes lack CAP_NET_RAW, so this is how the live ring reaches the engine there."""
+    import torch
+
+    from demikernel_amd._native import FLOW_DTYPE
+    from test_ring import load_live_fixture
+
+    assert torch.cuda.is_available()
+    g, ring = load_live_fixture()
+    bs, nb = int(g["block_size"]), int(g["nblocks"])
+    flows = g["flows"].view(FLOW_DTYPE)
+    eng = RxEngine(Config(synth.BOB_IPV4))
+    eng.set_sockets(flows)
+    r = RG.TpacketRing(ring, bs)  # page-locked in place (dk_ring_register)
+    try:
+        n = len(g["scan_off"])
+        res = RxResults(n, len(flows), tcp_fields=True, host=True)
+        nf, used = r.receive(eng, 0, nb, res)
+        assert (nf, used) == (n, nb)
+        peer = OraclePeer(synth.ipv4(synth.BOB_IPV4))
+        peer.set_flows(flows)
+        exp = peer.process(ring, g["scan_off"], g["scan_len"])
+        got = res.to_numpy()
+        for k in ("meta", "src_ip", "dst_ip", "ports", "payload", "flow_id", "tcp_seq", "tcp_ack", "tcp_win",
+                  "flow_counts", "verdict_counts"):
+            e = exp[k][: len(got[k])]
+            assert np.array_equal(got[k], e), k
+            assert np.array_equal(got[k], g["res_" + k][: len(got[k])]), k
+        assert (got["meta"] & 0xFF <= 1).mean() > 0.8
+    finally:
+        r.close()
+        eng.close()

@@ -111,3 +111,37 @@ def test_malformed_later_block_returns_good_prefix_then_is_consumed():
     r.release(1, 1)
     o3, _, nb3 = r.scan(2, used - 2, len(off))
     assert nb3 == used - 2 and np.array_equal(o3, eoff[eoff // bs >= 2])
+
+
+def load_live_fixture():
+    """The ring a live AF_PACKET socket on `lo` filled (tests/golden/make_ring_fixture.py), in page-aligned memory."""
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "live_ring_lo.npz"),
+                allow_pickle=False)
+    ring = RG.page_aligned_empty(g["ring"].nbytes)
+    ring[:] = g["ring"]
+    return g, ring
+
+
+def test_live_ring_fixture_scan_and_oracle():
+    """The captured kernel-written ring (block descriptors and tpacket3 headers exactly as Linux wrote them): the scan
+    finds the descriptors it found at capture time, every injected frame in order at 2 mod 16, and the oracle's
+    results over those descriptors are the ones recorded then (the GPU replay compares with the same oracle)."""
+    from demikernel_amd._native import FLOW_DTYPE
+    from oracle.oracle import OraclePeer
+
+    g, ring = load_live_fixture()
+    bs, nb = int(g["block_size"]), int(g["nblocks"])
+    off, ln, used = RG.TpacketRing(ring, bs, register=False).scan(0, nb, 1 << 16)
+    assert used == nb and np.array_equal(off, g["scan_off"]) and np.array_equal(ln, g["scan_len"])
+    frames, flen = g["frames"], g["frame_len"]
+    starts = np.concatenate([[0], np.cumsum(flen.astype(np.int64))[:-1]])
+    for j, k in enumerate(g["mine"]):
+        assert ring[off[k]:off[k] + ln[k]].tobytes() == frames[starts[j]:starts[j] + flen[j]].tobytes(), j
+    assert {int(off[k]) % 16 for k in g["mine"]} <= {2, 10}
+    peer = OraclePeer(synth.ipv4(synth.BOB_IPV4))
+    peer.set_flows(g["flows"].view(FLOW_DTYPE))
+    exp = peer.process(ring, off, ln)
+    for k, v in exp.items():
+        assert np.array_equal(v, g["res_" + k]), k
