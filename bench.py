@@ -482,9 +482,11 @@ def load_traffic_profile(workload):
         return None
 
 
-def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True):
+def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True, tcp_fields=False):
     """Device-resident kernel rate of another BASELINE config on this GPU (its own engine and batches; `rotate`
-    distinct batches when one would sit in the 256 MB MALL), with its roofline fields."""
+    distinct batches when one would sit in the 256 MB MALL), with its roofline fields. tcp_fields: the record a LibOS
+    binding consumes — tcp_seq / tcp_ack / tcp_win (12 more bytes per frame) and the tcp_opts records
+    (written for option-bearing segments only: none in these batches)."""
     from demikernel_amd import Config, RxEngine, synth
 
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
@@ -492,10 +494,10 @@ def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True):
     batches = [m[0] for m in made]
     _, flows, tr = made[0]
     n = batches[0].n
-    res = eng.results(n, dst_ip=dst_ip)
+    res = eng.results(n, dst_ip=dst_ip, tcp_fields=tcp_fields, tcp_opts=tcp_fields)
     wall, kern, _, _ = time_kernel(eng, batches, res, steps, warmup, stream)
     fb = int(tr.frame_len.astype(np.int64).sum())
-    rb = RESULT_BYTES if dst_ip else RESULT_BYTES - 4
+    rb = (RESULT_BYTES if dst_ip else RESULT_BYTES - 4) + (12 if tcp_fields else 0)
     algo = fb + n * (DESC_BYTES + rb)
     out = {"workload": WORKLOADS[name][0], "frames": n, "flows": len(flows), "batches_rotated": rotate,
            "gbps": round(fb * steps / wall / 1e9, 2), "mpkt_s": round(n * steps / wall / 1e6, 1),
@@ -503,7 +505,7 @@ def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True):
            "result_bytes_per_frame": rb,
            "roofline": {"bound": "hbm", "achieved": round(algo / kern / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo,
-                        "traffic": load_traffic_profile(name)}}
+                        "traffic": load_traffic_profile(name + ("_libos" if tcp_fields else ""))}}
     return out, eng, batches[0], flows
 
 
@@ -681,6 +683,11 @@ def main():
             del e
         except Exception as exc:  # noqa: BLE001 — an extra field must not cost the headline line; the error is reported
             out["c1_tcp1078"] = {"error": repr(exc)}
+        # the record the Rust LibOS binding consumes (deliver() needs seq / ack / window, and the
+        # option list on SYNs): C2 with tcp_fields and tcp_opts, 36 B of results per frame
+        out["c2_libos_record"], e, _, _ = rx_extra("c2_tcp1500", dev, stream, tcp_fields=True)
+        out["c2_libos_record"]["workload"] += " (LibOS record: + tcp_seq/ack/win, tcp_opts)"
+        del e
         out["c4_imix"], e, _, _ = rx_extra("c4_imix", dev, stream)
         del e
         out["c5_device"], e5, b5, f5 = rx_extra("c5_tcp1500_10k", dev, stream)

@@ -1125,16 +1125,33 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
 // tree of arrival tickets (write-through rows, drained, the last arriver of each group summing its group) was slower on
 // every workload (C2 +0.8 %, IMIX +2.3 %, C5 +3.3 %, C3 +23 %) and on small batches too, and replica rows filled by
 // memory-side atomics tied with the second launch; the kernels hold no inter-workgroup hand-off at all.
+// The kernels' by-value RxParams sits at the start of the kernel-argument segment. Fields used only at a kernel's end
+// (counter rows, the pending-rows combine) are read from there at the point of use: read through the by-value
+// parameter, the compiler loads them at the entry and keeps them in SGPRs across the chunk loop, where they spill to
+// VGPR lanes and cost v_readlane in the loop (DK_KARGS=0 restores that form for A/B).
+#ifndef DK_KARGS
+#define DK_KARGS 1
+#endif
+__device__ __forceinline__ const RxParams& kargs(const RxParams& P) {
+#if DK_KARGS
+    (void)P;
+    return *reinterpret_cast<const RxParams*>(__builtin_amdgcn_kernarg_segment_ptr());
+#else
+    return P;
+#endif
+}
 __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
                                                const uint32_t* s_flow, const uint32_t* s_vh) {
-    if (!P.row_words) return;
+    const RxParams& K = kargs(P);
+    if (!K.row_words) return;
 #ifdef DK_ABL_NOFLUSH  // ablation (tuning only): counters never leave LDS
     return;
 #endif
-    uint32_t* row = P.flow_scratch + (size_t)blockIdx.x * P.row_stride;
+    uint32_t* row = K.flow_scratch + (size_t)blockIdx.x * K.row_stride;
+    const uint32_t fw = K.flow_words;
     if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += nthreads) row[k] = s_flow[k];
-    if (P.res.verdict_counts && tid < kVerdictWords) row[P.flow_words + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
+        for (uint32_t k = tid; k < fw; k += nthreads) row[k] = s_flow[k];
+    if (K.res.verdict_counts && tid < kVerdictWords) row[fw + tid] = tid < DK_V_COUNT ? s_vh[tid] : 0u;
 }
 
 // Sum of one 64-column x rpb-row block of counter rows into the destination counters (the column sums of the
@@ -1175,7 +1192,7 @@ __device__ __forceinline__ void comb_block(const RowCombine& Q, uint32_t t, uint
 // The previous launch's pending counter rows (RowCombine, rx_common.h): every calling wave takes blocks by ticket until
 // they run out (exactly one ticket past the last block per wave, which the host's next base counts on).
 __device__ __forceinline__ void combine_pending(const RxParams& P, uint32_t lane) {
-    const RowCombine& Q = P.comb;
+    const RowCombine& Q = kargs(P).comb;
     if (!Q.rows) return;
     for (;;) {
         uint32_t t = 0;

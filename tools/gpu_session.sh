@@ -34,6 +34,12 @@ for wl in c1_tcp1078 c2_tcp1500 c5_tcp1500_10k; do
   step ${wl}_agg 300 python3 tools/tune_ab.py --workload $wl --rotate 3 --reps 7 --iters 10 --lib demikernel_amd/libdk_rx.so \
     --lib build/variants/aggoff.so "defer=1"
 done
+# 3b. end-only kernel arguments read at their use (DK_KARGS, default 1) vs through the by-value parameter
+for wl in c3_udp64 c4_imix c2_tcp1500; do
+  R8=1; [ $wl = c3_udp64 ] && R8=8
+  step ${wl}_kargs 300 python3 tools/tune_ab.py --workload $wl --rotate $R8 --reps 7 --iters 10 \
+    --lib demikernel_amd/libdk_rx.so --lib build/variants/kargs0.so "" "defer=1"
+done
 # 4. rocprofv3 kernel stats and HBM traffic of C1 at the host rule
 cd /tmp
 step c1_stats 200 rocprofv3 --kernel-trace --stats -T -d $O/c1_stats -o run --output-format csv -- \
