@@ -1135,7 +1135,7 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
 __device__ __forceinline__ const RxParams& kargs(const RxParams& P) {
 #if DK_KARGS
     (void)P;
-    return *reinterpret_cast<const RxParams*>(__builtin_amdgcn_kernarg_segment_ptr());
+    return *(const RxParams*)__builtin_amdgcn_kernarg_segment_ptr();  // (a C cast: it leaves the constant space)
 #else
     return P;
 #endif
