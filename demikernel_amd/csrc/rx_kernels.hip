@@ -1572,7 +1572,14 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
     const Blob B(P.frames, P.frames_bytes);
     SmallLds& W = s_wave[wv];
-    // Pipeline: chunk k is parsed while chunk k + 1's frame registers and chunk k + 2's descriptors load.
+    // Pipeline: descriptors are loaded two chunks ahead. With DK_SMALL_LATE (default) chunk k + 2's descriptor loads
+    // are issued before chunk k's window DMA, so the window's wait covers them, and chunk k's deferral mask is stored
+    // after its result stores and only when the chunk left frames (`had`), so it sits behind the next window's wait.
+    // Issued after the window (DK_SMALL_LATE=0, rounds 2-3), the descriptor loads and the mask store were caught by the
+    // compiler's wait for the window registers of the per-lane-load path: one more memory round trip per chunk.
+#ifndef DK_SMALL_LATE
+#define DK_SMALL_LATE 1
+#endif
     uint32_t c, lim, c1 = 0, lim1 = 0, c2 = 0, lim2 = 0;
     bool have = r.chunk(0, c, lim);
     bool have1 = have && r.chunk(1, c1, lim1);
@@ -1589,21 +1596,31 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
     const uint32_t nw = gridDim.x * kSmallWaves, gw = blockIdx.x * kSmallWaves + wv;  // deferral mask index k nw + gw
     bool deferred = false;  // wave-uniform: a chunk left frames to the general pass
+    // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
+    uint64_t had = DK_SMALL_LATE ? 0ull : ~0ull;
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
         const bool have2 = have1 && r.chunk(k + 2, c2, lim2);
+        uint32_t off2 = 0, len2 = 0;
+#if DK_SMALL_LATE
+        if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead, before this chunk's window DMA
+            off2 = P.off[c2 + r.lane_off];
+            len2 = P.len[c2 + r.lane_off];
+        }
+#endif
         const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + r.lane_off < lim1, off1, len1);
         uint32_t v, fid;
         Rec rec;
         rec.meta = kNoRec;
         if (k == 0) DK_STAMP(1);
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
-        uint32_t off2 = 0, len2 = 0;
+#if !DK_SMALL_LATE
         if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead (after the window wait)
             off2 = P.off[c2 + r.lane_off];
             len2 = P.len[c2 + r.lane_off];
         }
+#endif
         DK_STAMP(2 + 3 * k);
 #if DK_SMALL_DEFER
         if (kShift && __ballot(live && F.vec && !F.big && F.sh != 0)) {  // realign the windows of shifted frames
@@ -1612,11 +1629,19 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         }
         const bool take = live && small_fast_eligible(F, len, C.R);
         const uint64_t dm = __ballot(live && !take);
+#if !DK_SMALL_LATE
         if (lane == 0) P.defer[k * nw + gw] = dm;  // every chunk's mask, read back by this wave after the loop
+#endif
         deferred = deferred || dm != 0;
         small_fast<kOpt>(P, i, take, lane, C.R, len, v, fid);
         DK_STAMP(3 + 3 * k);
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
+#if DK_SMALL_LATE
+        if (dm != 0 || k >= 64) {  // read back by this wave after the loop
+            if (lane == 0) P.defer[k * nw + gw] = dm;
+            if (k < 64) had |= 1ull << k;
+        }
+#endif
 #else
         small_big_frames(F, lane, off, B, W, C);
         rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,
@@ -1643,6 +1668,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
         uint32_t cd, limd;
         for (uint32_t k = 0; r.chunk(k, cd, limd); k++) {
+            if (k < 64 && !((had >> k) & 1u)) continue;  // chunk k left no frame (no mask stored)
             const uint64_t m = P.defer[k * nw + gw];  // wave-uniform
             if (!m) continue;
             const uint32_t i = cd + r.lane_off;
@@ -1767,12 +1793,35 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     uint32_t nstg = 0, klast = 0;
     uint32_t c, lim;
     const uint32_t p0 = finisher ? fin : 0u, dp = finisher ? (uint32_t)kFin : 1u;
-    for (uint32_t p = p0; r.chunk(p, c, lim); p += dp) {
+    // Descriptors one chunk ahead (DK_SPLIT_PREFETCH, round 4): loaded at the top of chunk p, a stream wave would
+    // otherwise open every chunk with a dependent descriptor round trip before its first frame load (nothing of its
+    // own in flight meanwhile) — one in 16 chunks at C2, one in 2 at C1.
+#ifndef DK_SPLIT_PREFETCH
+#define DK_SPLIT_PREFETCH 1
+#endif
+    bool have = r.chunk(p0, c, lim);
+    uint32_t noff = 0, nlen = 0;
+    if (DK_SPLIT_PREFETCH && have && c + r.lane_off < lim) {
+        noff = P.off[c + r.lane_off];
+        nlen = P.len[c + r.lane_off];
+    }
+    for (uint32_t p = p0; have; p += dp) {
         const uint32_t b = p % kBufs;
         WaveLds& W = s_buf[b][sw];
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
+#if DK_SPLIT_PREFETCH
+        const uint32_t off = noff, len = nlen;
+        uint32_t nc, nlim;
+        const bool nhave = r.chunk(p + dp, nc, nlim);
+        noff = nlen = 0;
+        if (nhave && nc + r.lane_off < nlim) {
+            noff = P.off[nc + r.lane_off];
+            nlen = P.len[nc + r.lane_off];
+        }
+#else
         const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
+#endif
         const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
         if (!finisher) {
             // frames of <= 64 bytes: their granules ride along with the big frames' stream and reach the finisher
@@ -1816,6 +1865,13 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
             }
             count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         }
+#if DK_SPLIT_PREFETCH
+        c = nc;
+        lim = nlim;
+        have = nhave;
+#else
+        have = r.chunk(p + dp, c, lim);
+#endif
     }
     __syncthreads();
     if (finisher && nstg) flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);

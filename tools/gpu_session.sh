@@ -18,36 +18,25 @@ export TMPDIR=/tmp
 
 # 1. parity: the changed paths first, then the whole GPU suite
 PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step t_defer 400 $PYT tests/test_gpu_parity.py -k "deferred_counts or counter_rows or flow_counter or two_streams or streams_destroyed"
+step t_defer 400 $PYT tests/test_gpu_parity.py -k "deferred_counts or counter_rows or flow_counter or two_streams or streams_destroyed or full_size_c1 or full_size_c3"
 step t_multi 300 $PYT tests/test_gpu_multiproc.py
 step t_all 900 $PYT -m gpu tests
 step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
-# 2. deferred counters and the family choice on C1, and deferral on the other configs
-step c1_fam 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 "" "defer=1" "split=0" "split=0,defer=1" \
-  "split=0,stage=0" "split=0,stage=0,defer=1" "split=0,stage=0,grid_per_cu=8,defer=1"
-for wl in c2_tcp1500 c4_imix c5_tcp1500_10k; do
-  step ${wl}_defer 300 python3 tools/tune_ab.py --workload $wl --reps 7 --iters 10 "" "defer=1"
-done
-step c3_defer 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 16 "" "defer=1"
-# 3. flow-count aggregation A/B (variant without it)
-for wl in c1_tcp1078 c2_tcp1500 c5_tcp1500_10k; do
-  step ${wl}_agg 300 python3 tools/tune_ab.py --workload $wl --rotate 3 --reps 7 --iters 10 --lib demikernel_amd/libdk_rx.so \
-    --lib build/variants/aggoff.so "defer=1"
-done
-# 3b. end-only kernel arguments read at their use (DK_KARGS, default 1) vs through the by-value parameter
-for wl in c3_udp64 c4_imix c2_tcp1500; do
-  R8=1; [ $wl = c3_udp64 ] && R8=8
-  step ${wl}_kargs 300 python3 tools/tune_ab.py --workload $wl --rotate $R8 --reps 7 --iters 10 \
-    --lib demikernel_amd/libdk_rx.so --lib build/variants/kargs0.so "" "defer=1"
-done
-# 4. rocprofv3 kernel stats and HBM traffic of C1 at the host rule
+# 2. A/B: deferred counters (defer=1) x builds (head = every round-4 change; each variant turns one of them off)
+V=build/variants
+H=demikernel_amd/libdk_rx.so
+step ab_c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 7 --iters 20 --lib $H --lib $V/pref0.so \
+  --lib $V/aggoff.so "" "defer=1" "split=0,defer=1" "split=0,stage=0,defer=1"
+step ab_c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 16 --lib $H --lib $V/late0.so \
+  --lib $V/kargs0.so "" "defer=1"
+step ab_c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --iters 10 --lib $H --lib $V/pref0.so \
+  --lib $V/aggoff.so --lib $V/kargs0.so "" "defer=1"
+step ab_c4 300 python3 tools/tune_ab.py --workload c4_imix --reps 7 --iters 10 --lib $H --lib $V/kargs0.so "" "defer=1"
+step ab_c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --iters 8 --lib $H --lib $V/pref0.so \
+  --lib $V/aggoff.so "" "defer=1"
+# 3. rocprofv3 kernel stats of C1 (deferred counters, as the bench runs)
 cd /tmp
 step c1_stats 200 rocprofv3 --kernel-trace --stats -T -d $O/c1_stats -o run --output-format csv -- \
-  python3 $R/tools/kbench.py --workload c1_tcp1078 --rotate 3 --iters 20
-step c1_fetch 200 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "dk_rx_split_kernel|read_probe" -T \
-  -d $O/fetch_c1_tcp1078 -o run --output-format csv -- python3 $R/tools/kbench.py --workload c1_tcp1078 --iters 5 --probe-one
-step c1_write 200 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "dk_rx_split_kernel|read_probe" -T \
-  -d $O/write_c1_tcp1078 -o run --output-format csv -- python3 $R/tools/kbench.py --workload c1_tcp1078 --iters 5 --probe-one
+  python3 $R/tools/kbench.py --workload c1_tcp1078 --rotate 3 --iters 20 --defer
 cd $R
-step c1_sq 300 bash tools/pmc_kernel.sh c1_tcp1078 ${TAG}_c1 --rotate 3
 echo done

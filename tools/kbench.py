@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--grids", default="256,512,768,1024")
     ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
     ap.add_argument("--lib", default=None, help="a variant libdk_rx.so (tools/variants.sh) instead of the in-tree one")
+    ap.add_argument("--tcp-fields", action="store_true", help="the LibOS record: + tcp_seq/ack/win and tcp_opts")
+    ap.add_argument("--defer", action="store_true", help="deferred counters (DK_RX_BATCH_DEFER_COUNTS), as bench.py runs")
     args = ap.parse_args()
 
     import torch
@@ -57,7 +59,7 @@ def main():
     eng = RxEngine(Config(synth.BOB_IPV4), lib_path=os.path.abspath(args.lib) if args.lib else None)
     batch, flows, tr = bench.make_batch(eng, args.workload, 0, synth.SEED, 1)
     rot = [batch] + [bench.make_batch(eng, args.workload, 0, synth.SEED + 1000 * k, 1)[0] for k in range(1, args.rotate)]
-    res = eng.results(batch.n, counts=not args.no_counts)
+    res = eng.results(batch.n, counts=not args.no_counts, tcp_fields=args.tcp_fields, tcp_opts=args.tcp_fields)
     it = [0]
 
     def next_batch():
@@ -65,8 +67,9 @@ def main():
         return rot[it[0] % len(rot)]
     fb = int(tr.frame_len.astype(np.int64).sum())
     if not args.no_rx:
-        t = time_events(lambda: eng.receive_batch(next_batch(), res), args.iters)
-        algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES)
+        t = time_events(lambda: eng.receive_batch(next_batch(), res, defer_counts=args.defer), args.iters)
+        eng.flush_counts()
+        algo = fb + batch.n * (bench.DESC_BYTES + bench.RESULT_BYTES + (12 if args.tcp_fields else 0))
         print(json.dumps({"kernel": "dk_rx", "workload": args.workload, "counts": not args.no_counts,
                           "frames": batch.n, "frame_bytes": fb, "algo_bytes": algo, "blob_bytes": batch.blob.numel(),
                           "ms": round(t * 1e3, 4),

@@ -53,7 +53,7 @@ def main():
     stats = os.path.join(src, "bench", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
-    for sub in ("c3", "tx"):
+    for sub in ("c3", "tx", "c1"):
         st = os.path.join(src, sub, "run_kernel_stats.csv")
         if os.path.exists(st):
             shutil.copy(st, os.path.join(dst, f"{tag}_{sub}_kernel_stats.csv"))
@@ -66,7 +66,8 @@ def main():
     traffic = {}
     rows = [["workload", "kernel", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "calib_factor", "hbm_read_bytes",
              "hbm_write_bytes", "algo_bytes", "traffic_over_algo"]]
-    for wl in ("c2_tcp1500", "c3_udp64", "c4_imix", "c5_tcp1500_10k"):
+    for wl in ("c2_tcp1500", "c3_udp64", "c4_imix", "c5_tcp1500_10k", "c1_tcp1078", "c3_udp64_random_ports",
+               "c2_tcp1500_libos"):
         fdir, wdir = os.path.join(src, f"fetch_{wl}"), os.path.join(src, f"write_{wl}")
         if not os.path.exists(os.path.join(fdir, "run_counter_collection.csv")):
             continue
