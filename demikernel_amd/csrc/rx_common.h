@@ -82,12 +82,13 @@ constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a p
 constexpr uint32_t kRowAlignWords = 32;  // counter rows padded to whole 128-byte lines
 
 // Counter rows a previous launch on the same stream left pending (DK_RX_BATCH_DEFER_COUNTS), added to that launch's
-// counters inside this launch: waves with nothing else to do (the split kernel's finish waves before their first chunk,
-// every other kernel's waves after their last one) take blocks of the rows by tickets from a
-// monotonically increasing device word. Every wave that runs the loop ends it with exactly one ticket past the last
-// block, so the word advances by nblk + waves per launch and the host knows the next launch's base without reading it.
-// Blocks are 64 columns x rpb rows (a multiple of kCombRows, the loads per lane in flight together): 16 rows for
-// narrow rows (many blocks for many waves), 64 for wide ones (C5's 10k flows: 4x fewer u64 atomics).
+// counters inside this launch by waves with nothing else to do: the split kernel's finish waves before their first
+// chunk (their stream waves are filling the pipeline), every other kernel's waves with the fewest chunks after their
+// last one (round-robin chunks leave the highest-numbered waves one chunk short). Blocks of 64 columns x rpb rows are
+// assigned statically, block j to the j-th of those waves (mod their count): no atomics on a shared word (a ticket word
+// taken by every wave measured 3x slower at C3: ~6,000 same-address atomics per launch serialise at the memory side).
+// rpb: 16 rows for narrow rows (many small blocks for many waves), 64 for wide ones (C5's 10k flows: 4x fewer u64
+// atomics). kCombRows = the loads per lane in flight together.
 constexpr uint32_t kCombRows = 16;
 constexpr uint32_t kCombCols = 64;
 struct RowCombine {
@@ -95,8 +96,6 @@ struct RowCombine {
     uint32_t nrows, row_words, row_stride, flow_words, nflows;
     uint64_t* counts;      // the pending launch's flow_counts / verdict_counts (either may be nullptr)
     uint64_t* verdicts;
-    uint32_t* ticket;      // device word (per stream slot)
-    uint32_t base;         // its value when this launch starts
     uint32_t rpb;          // rows per block
     uint32_t ncolblk, nblk;
 };
@@ -161,6 +160,5 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
 // dk_flow_reduce_kernel over rows left pending by a deferred launch (dk_rx_counts_flush and the scratch paths).
 int dk_launch_reduce(const dk::RowCombine& q, void* stream);
 uint32_t dk_rx_small_block_waves();  // waves per workgroup of the small-frame kernel
-uint32_t dk_rx_comb_waves(uint32_t family);  // waves per workgroup that run the pending-rows combine loop
 int dk_tx_resident_blocks();  // occupancy of dk_tx_kernel per CU (0 on error)
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream);

@@ -38,8 +38,6 @@ struct CountScratch {
     uint32_t half = 0;       // the half the next launch writes
     uint64_t* defer = nullptr;  // the small-frame kernel's per-chunk deferral masks
     size_t ndefer = 0;
-    uint32_t* ticket = nullptr;  // the combine's ticket word (device)
-    uint32_t ticket_base = 0;    // its value once every launch issued so far has run
     bool pending = false;
     dk::RowCombine pend{};       // rows, nrows, row_words, row_stride, flow_words, nflows, counts, verdicts
 };
@@ -148,7 +146,6 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
 void free_slot(StreamSlot& s) {  // the caller has flushed and waited for the slot's launches
     if (s.cs.rows) (void)hipFree(s.cs.rows);
     if (s.cs.defer) (void)hipFree(s.cs.defer);
-    if (s.cs.ticket) (void)hipFree(s.cs.ticket);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
 }
@@ -218,18 +215,10 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
     return 0;
 }
 
-// Rows for `grid` workgroups (two halves) and `ndefer` deferral masks, and the combine's ticket word. Growing flushes
-// the slot's pending rows and waits for its launches before freeing.
+// Rows for `grid` workgroups (two halves) and `ndefer` deferral masks. Growing flushes the slot's pending rows and
+// waits for its launches before freeing.
 int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, size_t ndefer) {
     CountScratch& cs = s.cs;
-    if (!cs.ticket) {
-        if (hipMalloc(&cs.ticket, sizeof(uint32_t)) != hipSuccess) {
-            cs.ticket = nullptr;
-            return ENOMEM;
-        }
-        if (hipMemsetAsync(cs.ticket, 0, sizeof(uint32_t), s.stream) != hipSuccess) return EIO;
-        cs.ticket_base = 0;
-    }
     const size_t words = (size_t)grid * row_stride;
     if (cs.rows_words >= words && cs.ndefer >= ndefer) return 0;
     if (flush_pending(s)) return EIO;
@@ -348,8 +337,6 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.comb = dk::RowCombine{};
     if (cs && cs->pending) {  // the previous deferred launch's rows (in the other half) are added inside this launch
         p.comb = cs->pend;
-        p.comb.ticket = cs->ticket;
-        p.comb.base = cs->ticket_base;
         p.comb.rpb = p.comb.row_words > 16 * dk::kCombCols ? 4 * dk::kCombRows : dk::kCombRows;
         p.comb.ncolblk = (p.comb.row_words + dk::kCombCols - 1) / dk::kCombCols;
         p.comb.nblk = p.comb.ncolblk * ((p.comb.nrows + p.comb.rpb - 1) / p.comb.rpb);
@@ -362,10 +349,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
                 p.small, p.lt_words ? p.lt_n : 0u, p.defer_rows, p.comb.nblk);
     rc = dk_launch_rx(p, grid, stream);
     if (rc == 0 && cs) {
-        if (p.comb.rows) {  // every wave of the grid that runs the combine loop ends it with one ticket past the blocks
-            cs->ticket_base += p.comb.nblk + grid * dk_rx_comb_waves(family);
-            cs->pending = false;
-        }
+        if (p.comb.rows) cs->pending = false;
         if (p.row_words) {
             if (p.defer_rows) {
                 cs->pend = dk::RowCombine{};

@@ -659,14 +659,14 @@ __device__ __forceinline__ void coop_finish(uint32_t k0, uint32_t k1, uint32_t m
     }
 }
 
-// Phase B of one chunk: the medium frames' steps, then the large frames' steps.
-template <bool kShift, bool kHdrT = false, uint32_t kR = kRoundsPerStep>
+// Phase B of one chunk: the medium frames' steps (kMR rounds each), then the large frames' steps (kR rounds each).
+template <bool kShift, bool kHdrT = false, uint32_t kR = kRoundsPerStep, uint32_t kMR = kMedR>
 __device__ __forceinline__ void coop_stream(const CoopPlan& pl, uint32_t lane, WaveLds& W, const Blob& B) {
 #if DK_COOP_MED_U > 0
-    for (uint32_t r = 0; r * 4 < pl.nmed; r += kMedR) {
-        CoopStep<kMedU, kMedR> S;
-        coop_issue<kMedU, kMedR, kHdrT>(0, pl.nmed, r, lane, W, B, S, 0);
-        coop_finish<kShift, kMedU, kMedR, kHdrT>(0, pl.nmed, 1, r, lane, W, B, S);
+    for (uint32_t r = 0; r * 4 < pl.nmed; r += kMR) {
+        CoopStep<kMedU, kMR> S;
+        coop_issue<kMedU, kMR, kHdrT>(0, pl.nmed, r, lane, W, B, S, 0);
+        coop_finish<kShift, kMedU, kMR, kHdrT>(0, pl.nmed, 1, r, lane, W, B, S);
     }
 #endif
     for (uint32_t r = 0; r * 4 < pl.ncoop - pl.nmed; r += kR) {
@@ -1189,18 +1189,18 @@ __device__ __forceinline__ void comb_block(const RowCombine& Q, uint32_t t, uint
         atomicAdd(reinterpret_cast<unsigned long long*>(Q.counts + 2 * w + 1), (unsigned long long)hi);
 }
 
-// The previous launch's pending counter rows (RowCombine, rx_common.h): every calling wave takes blocks by ticket until
-// they run out (exactly one ticket past the last block per wave, which the host's next base counts on).
-__device__ __forceinline__ void combine_pending(const RxParams& P, uint32_t lane) {
+// The previous launch's pending counter rows (RowCombine, rx_common.h): the calling wave, the w-th of nw combining
+// waves, adds blocks w, w + nw, ... (wave-uniform).
+__device__ __forceinline__ void combine_pending(const RxParams& P, uint32_t lane, uint32_t w, uint32_t nw) {
     const RowCombine& Q = kargs(P).comb;
     if (!Q.rows) return;
-    for (;;) {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(Q.ticket, 1u);
-        t = (uint32_t)__builtin_amdgcn_readlane((int)t, 0) - Q.base;
-        if (t >= Q.nblk) break;
-        comb_block(Q, t, lane);
-    }
+    for (uint32_t t = w; t < Q.nblk; t += nw) comb_block(Q, t, lane);
+}
+// Tail form: the waves of a round-robin grid with the fewest chunks are the highest-numbered ones, so block j goes to
+// wave nwaves - 1 - j (mod nwaves).
+__device__ __forceinline__ void combine_pending_tail(const RxParams& P, uint32_t lane, uint32_t waves_per_group) {
+    const uint32_t nw = gridDim.x * waves_per_group, gw = blockIdx.x * waves_per_group + (threadIdx.x >> 6);
+    combine_pending(P, lane, nw - 1 - gw, nw);
 }
 
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
@@ -1270,7 +1270,7 @@ void dk_rx_kernel(RxParams P) {
     }
 
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
-    combine_pending(P, lane);  // a previous launch's deferred counter rows, in this wave's tail
+    combine_pending_tail(P, lane, kWaves);  // a previous launch's deferred counter rows, in this wave's tail
     __syncthreads();
     flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
 }
@@ -1685,7 +1685,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         }
     }
 #endif
-    combine_pending(P, lane);  // a previous launch's deferred counter rows, in this wave's tail
+    combine_pending_tail(P, lane, kSmallWaves);  // a previous launch's deferred counter rows, in this wave's tail
 #ifdef DK_DIAG_STAMPS
     DK_STAMP_T(14, __builtin_amdgcn_s_memtime());
 #endif
@@ -1696,6 +1696,29 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     DK_STAMP_T(13, __builtin_amdgcn_s_memrealtime());
 #endif
 }
+
+// A wave's chunks with their descriptors loaded one chunk ahead: D.off / D.len belong to chunk D.c (0 outside the
+// batch); next() starts the loads of the following chunk.
+struct DescAhead {
+    uint32_t c, lim, off, len;
+    bool have;
+    __device__ __forceinline__ DescAhead(const RxParams& P, const WaveRange& r, uint32_t p0) {
+        have = r.chunk(p0, c, lim);
+        off = len = 0;
+        if (have && c + r.lane_off < lim) {
+            off = P.off[c + r.lane_off];
+            len = P.len[c + r.lane_off];
+        }
+    }
+    __device__ __forceinline__ void next(const RxParams& P, const WaveRange& r, uint32_t p) {
+        have = r.chunk(p, c, lim);
+        off = len = 0;
+        if (have && c + r.lane_off < lim) {
+            off = P.off[c + r.lane_off];
+            len = P.len[c + r.lane_off];
+        }
+    }
+};
 
 // LDS flag words between the waves of a workgroup (the split kernels' hand-off): acquire spin, release publish.
 typedef __attribute__((address_space(3))) uint32_t lu32;
@@ -1735,6 +1758,15 @@ struct SplitShape {
     static constexpr int kStg = DK_SPLIT_STG;    // chunks of results a finish wave stages
 };
 constexpr int kSplitBlock = SplitShape<1>::kThreads;  // the TX split kernel's shape
+// Rounds of 4 frames a split-kernel stream wave keeps in flight per step (large frames; medium frames: as many 5-load
+// rounds as fit the same load registers). A stream wave's chunks are a chain of dependent steps, so a batch with few
+// chunks per stream wave (C1: 2) is bound by the chain length, not by bandwidth; the finish waves' register budget
+// (256 VGPRs) leaves the stream role room for deeper steps.
+#ifndef DK_SPLIT_ROUNDS
+#define DK_SPLIT_ROUNDS 2
+#endif
+constexpr uint32_t kSplitRounds = DK_SPLIT_ROUNDS;
+constexpr uint32_t kSplitMedRounds = (kSplitRounds * kCoopU) / kMedU;
 template <int kStgK>
 __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[kStgK], uint32_t nst,
                                             const WaveRange& r, uint32_t k_last, uint32_t stride) {
@@ -1786,57 +1818,46 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
     const Blob B(P.frames, P.frames_bytes);
-    // a previous launch's deferred counter rows: the finish waves have nothing to do until their stream wave's first
-    // chunk has landed
-    if (finisher) combine_pending(P, lane);
-    Rec stg[kStg];
-    uint32_t nstg = 0, klast = 0;
-    uint32_t c, lim;
-    const uint32_t p0 = finisher ? fin : 0u, dp = finisher ? (uint32_t)kFin : 1u;
-    // Descriptors one chunk ahead (DK_SPLIT_PREFETCH, round 4): loaded at the top of chunk p, a stream wave would
-    // otherwise open every chunk with a dependent descriptor round trip before its first frame load (nothing of its
-    // own in flight meanwhile) — one in 16 chunks at C2, one in 2 at C1.
-#ifndef DK_SPLIT_PREFETCH
-#define DK_SPLIT_PREFETCH 1
-#endif
-    bool have = r.chunk(p0, c, lim);
-    uint32_t noff = 0, nlen = 0;
-    if (DK_SPLIT_PREFETCH && have && c + r.lane_off < lim) {
-        noff = P.off[c + r.lane_off];
-        nlen = P.len[c + r.lane_off];
-    }
-    for (uint32_t p = p0; have; p += dp) {
-        const uint32_t b = p % kBufs;
-        WaveLds& W = s_buf[b][sw];
-        const uint32_t i = c + r.lane_off;
-        const bool live = i < lim;
-#if DK_SPLIT_PREFETCH
-        const uint32_t off = noff, len = nlen;
-        uint32_t nc, nlim;
-        const bool nhave = r.chunk(p + dp, nc, nlim);
-        noff = nlen = 0;
-        if (nhave && nc + r.lane_off < nlim) {
-            noff = P.off[nc + r.lane_off];
-            nlen = P.len[nc + r.lane_off];
-        }
-#else
-        const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
-#endif
-        const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
-        if (!finisher) {
+    // The two roles run separate loops, so neither carries the other's registers (the finish waves' 16 staged chunks
+    // are not live in the stream loop, which may then keep deeper steps in flight: DK_SPLIT_ROUNDS). Both read their
+    // descriptors one chunk ahead (round 4: loaded at the top of chunk p, a stream wave opened every chunk with a
+    // dependent descriptor round trip before its first frame load; C5 -1.3 %).
+    DescAhead D(P, r, finisher ? fin : 0u);
+    if (!finisher) {
+        for (uint32_t p = 0; D.have; p++) {
+            const uint32_t b = p % kBufs;
+            WaveLds& W = s_buf[b][sw];
+            const bool live = D.c + r.lane_off < D.lim;
+            const uint32_t off = D.off, len = D.len;
+            D.next(P, r, p + 1);
+            const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
             // frames of <= 64 bytes: their granules ride along with the big frames' stream and reach the finisher
             // through the LDS header slot too, so the finish wave never waits on frame memory (IMIX: 7 of 12 frames)
             RegAcc Rs;
             small_load(F, B, off, Rs);
             if (p >= (uint32_t)kBufs) lds_wait_eq(&s_free[sw][b], p - kBufs + 1);  // buffer read out
             const CoopPlan pl = coop_plan(F, lane, off, W);
-            coop_stream<kShift>(pl, lane, W, B);
+            coop_stream<kShift, false, kSplitRounds, kSplitMedRounds>(pl, lane, W, B);
             if (F.vec && !F.big)
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     W.hdr[lane][k] = make_uint4(Rs.w[4 * k], Rs.w[4 * k + 1], Rs.w[4 * k + 2], Rs.w[4 * k + 3]);
             if (lane == 0) lds_publish(&s_ready[sw][b], p + 1);
-        } else {
+        }
+    } else {
+        // a previous launch's deferred counter rows: the finish waves have nothing to do until their stream wave's
+        // first chunk has landed
+        combine_pending(P, lane, blockIdx.x * kWaves + sw, gridDim.x * kWaves);
+        Rec stg[kStg];
+        uint32_t nstg = 0, klast = 0;
+        for (uint32_t p = fin; D.have; p += (uint32_t)kFin) {
+            const uint32_t b = p % kBufs;
+            WaveLds& W = s_buf[b][sw];
+            const uint32_t i = D.c + r.lane_off;
+            const bool live = i < D.lim;
+            const uint32_t off = D.off, len = D.len;
+            D.next(P, r, p + (uint32_t)kFin);
+            const FrameDesc<kShift> F(P.frames, P.frames_bytes, live, off, len);
             Chunk C;
             lds_wait_eq(&s_ready[sw][b], p + 1);
             if (F.vec && !F.big)
@@ -1865,16 +1886,9 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
             }
             count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         }
-#if DK_SPLIT_PREFETCH
-        c = nc;
-        lim = nlim;
-        have = nhave;
-#else
-        have = r.chunk(p + dp, c, lim);
-#endif
+        if (nstg) flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
     }
     __syncthreads();
-    if (finisher && nstg) flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
     flush_counters(P, tid, S::kThreads, lds_flows, s_flow, s_vh);
 }
 
@@ -2233,11 +2247,6 @@ int dk_launch_reduce(const dk::RowCombine& q, void* stream) {
     hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, (hipStream_t)stream, q.rows, q.nrows,
                        q.row_words, q.row_stride, q.flow_words, q.nflows, q.counts, q.verdicts);
     return hipGetLastError() == hipSuccess ? 0 : 5;
-}
-
-uint32_t dk_rx_comb_waves(uint32_t family) {
-    // the split kernel's finish waves (one per stream wave), every wave of the other families
-    return family == dk::kFamilySmall ? dk::kSmallWaves : (uint32_t)dk::kWaves;
 }
 
 int dk_tx_resident_blocks() {

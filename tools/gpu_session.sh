@@ -18,25 +18,19 @@ export TMPDIR=/tmp
 
 # 1. parity: the changed paths first, then the whole GPU suite
 PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step t_defer 400 $PYT tests/test_gpu_parity.py -k "deferred_counts or counter_rows or flow_counter or two_streams or streams_destroyed or full_size_c1 or full_size_c3"
+step t_defer 400 $PYT tests/test_gpu_parity.py -k "deferred_counts or counter_rows or kernel_variants or full_size_c1 or full_size_c2"
 step t_multi 300 $PYT tests/test_gpu_multiproc.py
 step t_all 900 $PYT -m gpu tests
 step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
-# 2. A/B: deferred counters (defer=1) x builds (head = every round-4 change; each variant turns one of them off)
+# 2. A/B: deferred counters (defer=1, static block assignment) x builds (sr3/sr4: 3/4 rounds per split-kernel step)
 V=build/variants
 H=demikernel_amd/libdk_rx.so
-step ab_c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 7 --iters 20 --lib $H --lib $V/pref0.so \
-  --lib $V/aggoff.so "" "defer=1" "split=0,defer=1" "split=0,stage=0,defer=1"
-step ab_c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 16 --lib $H --lib $V/late0.so \
-  --lib $V/kargs0.so "" "defer=1"
-step ab_c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --iters 10 --lib $H --lib $V/pref0.so \
-  --lib $V/aggoff.so --lib $V/kargs0.so "" "defer=1"
+step ab_c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 7 --iters 20 --lib $H --lib $V/sr3.so \
+  --lib $V/sr4.so "" "defer=1"
+step ab_c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 16 --lib $H --lib $V/kargs0.so "" "defer=1"
+step ab_c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --iters 10 --lib $H --lib $V/sr3.so --lib $V/sr4.so \
+  "" "defer=1"
 step ab_c4 300 python3 tools/tune_ab.py --workload c4_imix --reps 7 --iters 10 --lib $H --lib $V/kargs0.so "" "defer=1"
-step ab_c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --iters 8 --lib $H --lib $V/pref0.so \
-  --lib $V/aggoff.so "" "defer=1"
-# 3. rocprofv3 kernel stats of C1 (deferred counters, as the bench runs)
-cd /tmp
-step c1_stats 200 rocprofv3 --kernel-trace --stats -T -d $O/c1_stats -o run --output-format csv -- \
-  python3 $R/tools/kbench.py --workload c1_tcp1078 --rotate 3 --iters 20 --defer
-cd $R
+step ab_c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --iters 8 --lib $H --lib $V/sr3.so --lib $V/sr4.so \
+  "" "defer=1"
 echo done
