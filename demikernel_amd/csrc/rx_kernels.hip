@@ -1257,6 +1257,12 @@ void dk_rx_kernel(RxParams P) {
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
+        // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
+        // at the top of the next chunk, after a staged flush, their wait also waited for every store's write ack.
+#ifndef DK_EARLY_DESC
+#define DK_EARLY_DESC 1
+#endif
+        if (DK_EARLY_DESC) asm volatile("" ::"v"(noff), "v"(nlen));
         if (kStage) {  // shift register of the last kStageK chunks' results; stored when full and at exit
 #pragma unroll
             for (int q = kStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
@@ -1702,7 +1708,8 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 struct DescAhead {
     uint32_t c, lim, off, len;
     bool have;
-    __device__ __forceinline__ DescAhead(const RxParams& P, const WaveRange& r, uint32_t p0) {
+    template <class PT>  // RxParams or TxParams: off, len
+    __device__ __forceinline__ DescAhead(const PT& P, const WaveRange& r, uint32_t p0) {
         have = r.chunk(p0, c, lim);
         off = len = 0;
         if (have && c + r.lane_off < lim) {
@@ -1710,7 +1717,8 @@ struct DescAhead {
             len = P.len[c + r.lane_off];
         }
     }
-    __device__ __forceinline__ void next(const RxParams& P, const WaveRange& r, uint32_t p) {
+    template <class PT>
+    __device__ __forceinline__ void next(const PT& P, const WaveRange& r, uint32_t p) {
         have = r.chunk(p, c, lim);
         off = len = 0;
         if (have && c + r.lane_off < lim) {
@@ -1875,6 +1883,7 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
             Rec rec;
             rec.meta = kNoRec;
             rx_finish<kShift, true>(P, i, live, lane, W, off, len, C, v, fid, rec);
+            if (DK_EARLY_DESC) asm volatile("" ::"v"(D.off), "v"(D.len));  // waited for before the stores (as dk_rx_kernel)
             if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
 #pragma unroll
             for (int q = kStg - 1; q > 0; q--) stg[q] = stg[q - 1];
@@ -2128,20 +2137,29 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
     __syncthreads();
     const WaveRange r = wave_range(0, P.n, sw, lane);
     const Blob B(P.frames, P.frames_bytes);
-    uint32_t c, lim;
-    for (uint32_t p = 0; r.chunk(p, c, lim); p++) {
-        const uint32_t b = p % kBufs;
-        WaveLds& W = s_buf[b][sw];
-        const uint32_t i = c + r.lane_off;
-        const bool live = i < lim;
-        const uint32_t off = live ? P.off[i] : 0u, len = live ? P.len[i] : 0u;
-        const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
-        if (!finisher) {
+    // separate role loops, descriptors one chunk ahead (as dk_rx_split_kernel)
+    DescAhead D(P, r, 0);
+    if (!finisher) {
+        for (uint32_t p = 0; D.have; p++) {
+            const uint32_t b = p % kBufs;
+            WaveLds& W = s_buf[b][sw];
+            const bool live = D.c + r.lane_off < D.lim;
+            const uint32_t off = D.off, len = D.len;
+            D.next(P, r, p + 1);
+            const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
             if (p >= (uint32_t)kBufs) lds_wait_eq(&s_free[sw][b], p - kBufs + 1);  // buffer read out
             const CoopPlan pl = coop_plan(F, lane, off, W);
             coop_stream<true, true>(pl, lane, W, B);
             if (lane == 0) lds_publish(&s_ready[sw][b], p + 1);
-        } else {
+        }
+    } else {
+        for (uint32_t p = 0; D.have; p++) {
+            const uint32_t b = p % kBufs;
+            WaveLds& W = s_buf[b][sw];
+            const bool live = D.c + r.lane_off < D.lim;
+            const uint32_t off = D.off, len = D.len;
+            D.next(P, r, p + 1);
+            const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
             Chunk C;
             small_load(F, B, off, C.R);
             lds_wait_eq(&s_ready[sw][b], p + 1);
@@ -2149,6 +2167,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
             coop_gather(F, pl, lane, W, C);
             TxWin win;
             tx_finish<false>(P, lane, W, off, len, C, win);
+            asm volatile("" ::"v"(D.off), "v"(D.len));  // the next descriptors waited for before this chunk's writes
             if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
         }
     }
