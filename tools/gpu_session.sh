@@ -16,26 +16,11 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# 1. parity
-PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step t_part 400 $PYT tests/test_gpu_parity.py -k "deferred_counts or kernel_variants or full_size_c4 or tx"
-step t_all 900 $PYT -m gpu tests
-step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
-# 2. A/B with deferred counters (what bench.py runs); early0: next descriptors waited for at the top of the chunk
-V=build/variants
-H=demikernel_amd/libdk_rx.so
-step ab_c4 300 python3 tools/tune_ab.py --workload c4_imix --reps 9 --iters 10 --lib $H --lib $V/early0.so --lib $V/kargs0.so \
-  --lib $V/prev.so "defer=1"
-step ab_c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 11 --iters 16 --lib $H --lib $V/kargs0.so \
-  --lib $V/prev.so "defer=1"
-step ab_c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --iters 10 --lib $H --lib $V/early0.so --lib $V/prev.so "defer=1"
-step ab_c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --iters 8 --lib $H --lib $V/early0.so --lib $V/prev.so "defer=1"
-step ab_c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 7 --iters 20 --lib $H --lib $V/early0.so \
-  --lib $V/kargs0.so --lib $V/prev.so "defer=1"
-# 3. TX split kernel: separate role loops + descriptors ahead (head) vs before (prev)
-step ab_tx 300 python3 tools/abtest.py --workload c2_tcp1500 --grids 0 --tx --reps 7 $H $V/prev.so
-# 4. C1 shape at 1x, 2x, 4x, 8x the frames: the per-launch fixed cost (intercept) vs the per-byte rate
-for F in 131072 262144 524288 1048576; do
-  step c1_n$F 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 5 --iters 10 --frames $F "defer=1"
-done
+# 1. the bench line exactly as the driver runs it, then the collective-overlap check (1-rank RCCL communicator)
+step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+step overlap 300 python3 tools/overlap_collective.py --out $O/r04_overlap.json
+# 2. SQ counter passes (3 runs each, <= 8 SQ counters per run) of the C1 / C3 / C4 kernels, deferred counters
+step sq_c1 300 bash tools/pmc_kernel.sh c1_tcp1078 ${TAG}_c1 --rotate 3 --defer
+step sq_c3 300 bash tools/pmc_kernel.sh c3_udp64 ${TAG}_c3 --rotate 8 --defer
+step sq_c4 300 bash tools/pmc_kernel.sh c4_imix ${TAG}_c4 --defer
 echo done
