@@ -112,6 +112,9 @@ def preheat(eng, batch, stream, seconds):
     del scratch
 
 
+GATHER_EVERY = 8  # batches per all-reduce of the counters at N > 1 (bench --gather-every)
+
+
 def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
     """Run the untimed preheat, then warmup + timed steps. A step = the receive pass over one batch, whose counter
     rows the next step's kernel completes (DK_RX_BATCH_DEFER_COUNTS; the last step's by one flush launch inside the
@@ -123,7 +126,7 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
 
     from demikernel_amd.shard import ShardedReceiver
 
-    sr = ShardedReceiver(eng, res, comm, stream)
+    sr = ShardedReceiver(eng, res, comm, stream, gather_every=GATHER_EVERY)
     preheat(eng, batches[0], stream, PREHEAT_S)
     for k in range(warmup):
         sr.step(batches[k % len(batches)])
@@ -510,6 +513,7 @@ def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True, tcp_f
 
 
 def main():
+    global GATHER_EVERY
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -525,6 +529,9 @@ def main():
     ap.add_argument("--backend", default="gloo", choices=["nccl", "gloo"],
                     help="N > 1: process group for the barrier and the max-over-ranks timing only (the counters are "
                          "reduced by dk_rx_flow_counts_allreduce_to over RCCL)")
+    ap.add_argument("--gather-every", type=int, default=GATHER_EVERY,
+                    help="N > 1: batches per all-reduce of the node-wide counters (exact at every gather and at the "
+                         "end; RCCL's kernel does not run beside the receive kernels, DESIGN.md §7)")
     ap.add_argument("--frames-per-gpu", type=int, default=0,
                     help="override the workload's frames per GPU (tests only; the line's config records it)")
     ap.add_argument("--counts-via-torch-gloo-test", action="store_true",
@@ -534,6 +541,7 @@ def main():
                     help="write the node-wide flow / verdict counters after the timed steps to this .npz (rank 0)")
     args = ap.parse_args()
     set_preheat(args.preheat_seconds)
+    GATHER_EVERY = max(args.gather_every, 1)
 
     import torch
 
@@ -568,8 +576,9 @@ def main():
             print(f"bench: rank {rank}: dk_comm_init_rank failed ({e}); the packet-sharded path needs the RCCL "
                   f"communicator of include/dk_comm.h", file=sys.stderr, flush=True)
             sys.exit(3)
-        collective = ("dk_rx_flow_counts_allreduce_to (RCCL all-reduce of accumulating u64 flow + verdict counters) "
-                      "per step on a side stream, double-buffered (overlaps the next step's kernel)")
+        collective = (f"dk_rx_flow_counts_allreduce_to (RCCL all-reduce of accumulating u64 flow + verdict counters) "
+                      f"every {GATHER_EVERY} batches and after the last, on a side stream, double-buffered counter "
+                      f"sets (node-wide counts exact at every gather)")
 
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
     stream = torch.cuda.current_stream(dev)

@@ -793,6 +793,25 @@ __device__ __forceinline__ void st_res(uint32_t* p, uint32_t v) {
 // The six required result words of one frame (dk_rx.h), held in registers when the kernel stages its stores.
 struct Rec {
     uint32_t meta, src, dst, ports, pay, fid;
+    uint32_t seq, ack, win;  // the optional TCP fields (staged only by the split kernel's kTcp instantiation)
+};
+// What a staging slot holds: the six required words, or (kTcp) nine.
+template <bool kTcp>
+struct StgRec {
+    uint32_t meta, src, dst, ports, pay, fid;
+    __device__ __forceinline__ StgRec& operator=(const Rec& r) {
+        meta = r.meta; src = r.src; dst = r.dst; ports = r.ports; pay = r.pay; fid = r.fid;
+        return *this;
+    }
+};
+template <>
+struct StgRec<true> {
+    uint32_t meta, src, dst, ports, pay, fid, seq, ack, win;
+    __device__ __forceinline__ StgRec& operator=(const Rec& r) {
+        meta = r.meta; src = r.src; dst = r.dst; ports = r.ports; pay = r.pay; fid = r.fid;
+        seq = r.seq; ack = r.ack; win = r.win;
+        return *this;
+    }
 };
 // Result staging: result stores interleaved with the frame stream cost ~11 % at C2 (every wave's
 // 6 x 256 B of results per chunk reach HBM as scattered write bursts between the reads; ablation: storing them in an
@@ -887,7 +906,7 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     DK_SUB_STAMP(1);
 }
 
-template <bool kStage, bool kOpt = true, bool kNtRes = false>
+template <bool kStage, bool kOpt = true, bool kNtRes = false, bool kTcpStaged = false>
 __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live, uint32_t lane, uint32_t off,
                                         FinState& St, uint32_t& v_out, uint32_t& fid_out, Rec& rec,
                                         uint32_t stamp_base = ~0u) {
@@ -961,7 +980,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
             pay = poff | ((L.E - poff) << 16);
             if (is_tcp) { seq = L.seq; ack = L.ack; win = L.winurg; }
         }
-        rec = Rec{meta, src, dst, ports, pay, fid};
+        rec = Rec{meta, src, dst, ports, pay, fid, seq, ack, win};
         if (!kStage) {
         st_res<kNtRes>(P.res.meta + i, meta);
 #ifdef DK_ABL_NOSTORE  // ablation (tuning only): one result array
@@ -975,7 +994,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
         st_res<kNtRes>(P.res.flow_id + i, fid);
         }
         }
-        if (kOpt) {  // optional outputs (kOpt = false: the caller asked for none; fewer live SGPRs)
+        if (kOpt && !kTcpStaged) {  // optional outputs (kOpt = false: the caller asked for none; fewer live SGPRs)
             if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
             if (P.res.tcp_ack) P.res.tcp_ack[i] = ack;
             if (P.res.tcp_win) P.res.tcp_win[i] = win;
@@ -996,7 +1015,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
     fid_out = fid;
 }
 
-template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false>
+template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false, bool kTcpStaged = false>
 __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
                                           uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
@@ -1013,7 +1032,7 @@ __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool li
 #endif
     FinState St;
     rx_front<kShift>(P, live, lane, W, off, len, C, St, stamp_base);
-    rx_back<kStage, kOpt, kNtRes>(P, i, live, lane, off, St, v_out, fid_out, rec, stamp_base);
+    rx_back<kStage, kOpt, kNtRes, kTcpStaged>(P, i, live, lane, off, St, v_out, fid_out, rec, stamp_base);
 }
 
 // Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). Chunk k of a wave holds the
@@ -1049,9 +1068,17 @@ __device__ __forceinline__ WaveRange wave_range(uint32_t sched, uint32_t n, uint
     return r;
 }
 
+// The staged results are a shift register: stg[q] holds chunk k_last - q (a fixed slot per chunk of a burst, selected
+// by the burst position, made the compiler index the array dynamically: scratch memory).
+template <class T, int kN>
+__device__ __forceinline__ void stage_put(T (&stg)[kN], const Rec& rec) {
+#pragma unroll
+    for (int q = kN - 1; q > 0; q--) stg[q] = stg[q - 1];
+    stg[0] = rec;
+}
 // Store the nst most recent staged chunks: stg[q] holds the results of chunk k_last - q (kNoRec marks idle lanes).
 constexpr uint32_t kNoRec = 0xFFFFFFFFu;  // never a meta word (verdicts < 64)
-__device__ __forceinline__ void flush_staged(const RxParams& P, const Rec (&stg)[kStageK], uint32_t nst,
+__device__ __forceinline__ void flush_staged(const RxParams& P, const StgRec<false> (&stg)[kStageK], uint32_t nst,
                                              const WaveRange& r, uint32_t k_last) {
 #pragma unroll
     for (int q = kStageK - 1; q >= 0; q--) {
@@ -1229,7 +1256,7 @@ void dk_rx_kernel(RxParams P) {
     __syncthreads();
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
-    Rec stg[kStage ? kStageK : 1];
+    StgRec<false> stg[kStage ? kStageK : 1];
     uint32_t nstg = 0;  // wave-uniform
     uint32_t c, lim, nc, nlim;
     bool have = r.chunk(0, c, lim);
@@ -1263,19 +1290,17 @@ void dk_rx_kernel(RxParams P) {
 #define DK_EARLY_DESC 1
 #endif
         if (DK_EARLY_DESC) asm volatile("" ::"v"(noff), "v"(nlen));
-        if (kStage) {  // shift register of the last kStageK chunks' results; stored when full and at exit
-#pragma unroll
-            for (int q = kStageK - 1; q > 0; q--) stg[q] = stg[q - 1];
-            stg[0] = rec;
+        if (kStage) {  // the last kStageK chunks' results; stored when full and at exit
+            stage_put(stg, rec);
             if (++nstg == kStageK) {
-                flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, k);
+                flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, k);
                 nstg = 0;
             }
         }
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
     }
 
-    if (kStage && nstg) flush_staged(P, reinterpret_cast<const Rec(&)[kStageK]>(stg), nstg, r, nchunks - 1);
+    if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     combine_pending_tail(P, lane, kWaves);  // a previous launch's deferred counter rows, in this wave's tail
     __syncthreads();
     flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
@@ -1764,6 +1789,10 @@ struct SplitShape {
 #endif
     static constexpr int kBufs = DK_SPLIT_BUFS;  // LDS buffers per stream wave
     static constexpr int kStg = DK_SPLIT_STG;    // chunks of results a finish wave stages
+#ifndef DK_SPLIT_STG_TCP
+#define DK_SPLIT_STG_TCP 10
+#endif
+    static constexpr int kStgTcp = DK_SPLIT_STG_TCP;  // ... with the TCP fields (9 words a frame)
 };
 constexpr int kSplitBlock = SplitShape<1>::kThreads;  // the TX split kernel's shape
 // Rounds of 4 frames a split-kernel stream wave keeps in flight per step (large frames; medium frames: as many 5-load
@@ -1776,7 +1805,15 @@ constexpr int kSplitBlock = SplitShape<1>::kThreads;  // the TX split kernel's s
 constexpr uint32_t kSplitRounds = DK_SPLIT_ROUNDS;
 constexpr uint32_t kSplitMedRounds = (kSplitRounds * kCoopU) / kMedU;
 template <int kStgK>
-__device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[kStgK], uint32_t nst,
+__device__ __forceinline__ void store_tcp_fields(const RxParams& P, const StgRec<false>&, uint32_t) {}
+template <int kStgK>
+__device__ __forceinline__ void store_tcp_fields(const RxParams& P, const StgRec<true>& x, uint32_t i) {
+    if (P.res.tcp_seq) st_res<DK_SPLIT_NT_RES>(P.res.tcp_seq + i, x.seq);
+    if (P.res.tcp_ack) st_res<DK_SPLIT_NT_RES>(P.res.tcp_ack + i, x.ack);
+    if (P.res.tcp_win) st_res<DK_SPLIT_NT_RES>(P.res.tcp_win + i, x.win);
+}
+template <int kStgK, bool kTcp>
+__device__ __forceinline__ void flush_split(const RxParams& P, const StgRec<kTcp> (&stg)[kStgK], uint32_t nst,
                                             const WaveRange& r, uint32_t k_last, uint32_t stride) {
 #pragma unroll
     for (int q = kStgK - 1; q >= 0; q--) {
@@ -1791,6 +1828,7 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
         st_res<DK_SPLIT_NT_RES>(P.res.ports + i, stg[q].ports);
         st_res<DK_SPLIT_NT_RES>(P.res.payload + i, stg[q].pay);
         st_res<DK_SPLIT_NT_RES>(P.res.flow_id + i, stg[q].fid);
+        store_tcp_fields<kStgK>(P, stg[q], i);
     }
 }
 
@@ -1798,11 +1836,13 @@ __device__ __forceinline__ void flush_split(const RxParams& P, const Rec (&stg)[
 // written, set by the stream wave) and a free word (p + 1: read out, set by the finish wave that took p). A stream wave
 // runs up to kBufs - 1 chunks ahead of the slowest finisher and no wave waits at a workgroup barrier.
 
-template <bool kShift, int kFin>
+// kTcp: the LibOS record (tcp_seq / tcp_ack / tcp_win requested) — the finish waves stage those too (9 words per
+// frame, 16 chunks in 256 VGPRs) instead of storing them between the frame reads.
+template <bool kShift, int kFin, bool kTcp = false>
 __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_kernel(RxParams P) {
     using S = SplitShape<kFin>;
     constexpr int kBufs = S::kBufs;
-    constexpr int kStg = S::kStg;
+    constexpr int kStg = kTcp ? S::kStgTcp : S::kStg;
     __shared__ WaveLds s_buf[kBufs][kWaves];  // [chunk % kBufs][stream wave]
     __shared__ uint32_t s_ready[kWaves][kBufs], s_free[kWaves][kBufs];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
@@ -1856,7 +1896,7 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
         // a previous launch's deferred counter rows: the finish waves have nothing to do until their stream wave's
         // first chunk has landed
         combine_pending(P, lane, blockIdx.x * kWaves + sw, gridDim.x * kWaves);
-        Rec stg[kStg];
+        StgRec<kTcp> stg[kStg];
         uint32_t nstg = 0, klast = 0;
         for (uint32_t p = fin; D.have; p += (uint32_t)kFin) {
             const uint32_t b = p % kBufs;
@@ -1882,20 +1922,18 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
             uint32_t v, fid;
             Rec rec;
             rec.meta = kNoRec;
-            rx_finish<kShift, true>(P, i, live, lane, W, off, len, C, v, fid, rec);
+            rx_finish<kShift, true, WaveLds, true, false, kTcp>(P, i, live, lane, W, off, len, C, v, fid, rec);
             if (DK_EARLY_DESC) asm volatile("" ::"v"(D.off), "v"(D.len));  // waited for before the stores (as dk_rx_kernel)
             if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
-#pragma unroll
-            for (int q = kStg - 1; q > 0; q--) stg[q] = stg[q - 1];
-            stg[0] = rec;
+            stage_put(stg, rec);
             klast = p;
             if (++nstg == (uint32_t)kStg) {
-                flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
+                flush_split<kStg, kTcp>(P, stg, nstg, r, klast, (uint32_t)kFin);
                 nstg = 0;
             }
             count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         }
-        if (nstg) flush_split(P, stg, nstg, r, klast, (uint32_t)kFin);
+        if (nstg) flush_split<kStg, kTcp>(P, stg, nstg, r, klast, (uint32_t)kFin);
     }
     __syncthreads();
     flush_counters(P, tid, S::kThreads, lds_flows, s_flow, s_vh);
@@ -2225,6 +2263,7 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
                        : p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
+    const bool tcp = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win;  // the split kernel stages the TCP fields
     if (p.small && p.aligned16 && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small && p.aligned16)
@@ -2233,6 +2272,10 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.split && p.aligned16 && tcp)
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 1, true>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
+    else if (p.split && tcp)
+        hipLaunchKernelGGL((dk::dk_rx_split_kernel<true, 1, true>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 1>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split)

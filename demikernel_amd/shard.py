@@ -77,21 +77,27 @@ class TorchCountsAllreduce:
 
 class ShardedReceiver:
     """One rank of a packet-sharded receive: its engine, its RCCL communicator, and `nbuf` sets of accumulating
-    counters. Step k's kernel adds its counts to the set of slot k % nbuf (never zeroed: no memset kernels on the
-    launch stream). With `defer` (the default) the kernel leaves its counter rows pending (DK_RX_BATCH_DEFER_COUNTS) and
-    step k + 1's kernel adds them to step k's set inside its own launch, so no step pays a dependent second launch for
-    its counters; after that kernel, dk_rx_flow_counts_allreduce_to sums step k's set over the ranks into the slot's
+    counters. Steps are grouped in gather periods of `gather_every` steps; the steps of period j add their counts to
+    the set of slot j % nbuf (never zeroed: no memset kernels on the launch stream). With `defer` (the default) each
+    kernel leaves its counter rows pending (DK_RX_BATCH_DEFER_COUNTS) and the next step's kernel adds them inside its
+    own launch, so no step pays a dependent second launch for its counters. Once a period's counts are complete (after
+    the first kernel of the next period), dk_rx_flow_counts_allreduce_to sums that set over the ranks into the slot's
     node-wide totals on a side stream, overlapping the following kernels. A set is changed again only after its
-    previous all-reduce has read it (one event wait). flush() completes the last step (one small launch, then its
-    all-reduce). The node-wide counts of every step so far are the sum of the slots' totals (`counts()`). With
-    comm=None (one GPU) there is one set and no collective."""
+    previous all-reduce has read it (one event wait). flush() completes the last step and gathers it. The node-wide
+    counts of every step so far are the sum of the slots' totals (`counts()`), exact at every gather.
 
-    def __init__(self, engine, results, comm, stream, nbuf: int = 2, defer: bool = True):
+    gather_every = 1 gathers after every batch; tools/overlap_collective.py measured that RCCL's kernel does not run
+    beside the receive kernels (they hold every CU), so each gather costs the step ~its own time (~10 us); gathering
+    every K batches keeps the totals exact at each gather and divides that cost by K.
+    With comm=None (one GPU) there is one set and no collective."""
+
+    def __init__(self, engine, results, comm, stream, nbuf: int = 2, defer: bool = True, gather_every: int = 1):
         import torch
 
         from .rx import RxResults
 
         self.eng, self.comm, self.stream, self.defer = engine, comm, stream, defer
+        self.every = max(int(gather_every), 1)
         if comm is None:
             nbuf = 1
         self.side = torch.cuda.Stream(device=stream.device) if comm is not None else None
@@ -105,9 +111,10 @@ class ShardedReceiver:
             self.res.append(r)
         self.tot = [(torch.zeros_like(r.t["flow_counts"]), torch.zeros_like(r.t["verdict_counts"])) for r in self.res] \
             if comm is not None else None
-        self.done = [None] * nbuf
+        self.done = [None] * nbuf     # the event after each set's latest all-reduce
+        self.waited = [True] * nbuf   # the launch stream already waits for that event
         self.k = 0
-        self.pending = None  # the slot whose counters wait for the next launch (deferred rows)
+        self.pending = None  # the set whose counts wait for the next launch (deferred rows)
 
     def reduce(self, slot: int, stream) -> None:
         """The slot's node-wide totals from every rank's accumulated set (on `stream`)."""
@@ -128,35 +135,41 @@ class ShardedReceiver:
         done = torch.cuda.Event()
         done.record(self.side)
         self.done[slot] = done
+        self.waited[slot] = False
+
+    def _before_change(self, slot) -> None:
+        """The launch stream is about to add to set `slot`: its previous all-reduce must have read it."""
+        if slot is not None and not self.waited[slot]:
+            self.stream.wait_event(self.done[slot])
+            self.waited[slot] = True
 
     def step(self, batch) -> None:
-        slot = self.k % len(self.res)
-        prev = self.pending
-        # the set this launch changes: deferred, only the pending one it completes (its own rows stay pending);
+        slot = (self.k // self.every) % len(self.res)
+        prev, prev_k = self.pending, self.k - 1
+        # the sets this launch changes: deferred, only the pending one it completes (its own rows stay pending);
         # otherwise its own
-        changed = prev if self.defer else slot
-        if changed is not None and self.done[changed] is not None:
-            self.stream.wait_event(self.done[changed])  # the set's previous all-reduce has read it first
+        self._before_change(prev if self.defer else slot)
         self.eng.receive_batch(batch, self.res[slot], stream=self.stream, defer_counts=self.defer)
         if self.comm is not None:
-            if self.defer and prev is not None:
-                self._allreduce_after(prev)
-            elif not self.defer:
+            if self.defer:
+                if prev is not None and (prev_k + 1) % self.every == 0:  # step prev_k ended a gather period
+                    self._allreduce_after(prev)
+            elif (self.k + 1) % self.every == 0:
                 self._allreduce_after(slot)
         self.pending = slot if self.defer else None
         self.k += 1
 
     def flush(self) -> None:
-        """Complete the last deferred step's counters (and, with a communicator, issue their all-reduce)."""
-        if self.pending is None:
-            return
-        s = self.pending
-        if self.done[s] is not None:
-            self.stream.wait_event(self.done[s])
-        self.eng.flush_counts(self.stream)
-        if self.comm is not None:
-            self._allreduce_after(s)
-        self.pending = None
+        """Complete the last deferred step's counters and gather whatever has not been gathered yet."""
+        if self.pending is not None:
+            s = self.pending
+            self._before_change(s)
+            self.eng.flush_counts(self.stream)
+            self.pending = None
+            if self.comm is not None:  # the last step's set, whether or not it ended a period
+                self._allreduce_after(s)
+        elif self.comm is not None and not self.defer and self.k % self.every != 0:
+            self._allreduce_after(((self.k - 1) // self.every) % len(self.res))
 
     def drain(self) -> None:
         self.flush()

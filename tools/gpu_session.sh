@@ -16,11 +16,19 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# 1. the bench line exactly as the driver runs it, then the collective-overlap check (1-rank RCCL communicator)
-step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
-step overlap 300 python3 tools/overlap_collective.py --out $O/r04_overlap.json
-# 2. SQ counter passes (3 runs each, <= 8 SQ counters per run) of the C1 / C3 / C4 kernels, deferred counters
-step sq_c1 300 bash tools/pmc_kernel.sh c1_tcp1078 ${TAG}_c1 --rotate 3 --defer
-step sq_c3 300 bash tools/pmc_kernel.sh c3_udp64 ${TAG}_c3 --rotate 8 --defer
-step sq_c4 300 bash tools/pmc_kernel.sh c4_imix ${TAG}_c4 --defer
+# 1. parity
+PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+step t_part 400 $PYT tests/test_gpu_parity.py -k "full_size_c2 or deferred_counts or kernel_variants or tcp_fields or options"
+step t_multi 300 $PYT tests/test_gpu_multiproc.py
+step t_all 900 $PYT -m gpu tests
+step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
+# 2. A/B: the LibOS record staged by the split kernel (head) vs stored between the frame reads (prev)
+V=build/variants
+H=demikernel_amd/libdk_rx.so
+step ab_libos 300 python3 tools/tune_ab.py --workload c2_tcp1500 --tcp-fields --reps 7 --iters 10 --lib $H --lib $V/prev.so "defer=1"
+step ab_c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --iters 10 --lib $H --lib $V/prev.so "defer=1"
+step ab_c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --iters 8 --lib $H --lib $V/prev.so "defer=1"
+step ab_c4 300 python3 tools/tune_ab.py --workload c4_imix --reps 7 --iters 10 --lib $H --lib $V/prev.so "defer=1"
+# 3. the collective beside the kernels: every step, every 8 steps, 8 CUs left free
+step overlap 400 python3 tools/overlap_collective.py --out $O/r04_overlap.json
 echo done

@@ -3,10 +3,10 @@
 
     python tools/overlap_collective.py [--out profiles/r04_overlap.json]
 On one GPU, with a 1-rank RCCL communicator (dk_comm_init_all over device 0), ShardedReceiver steps at C2 and the C4
-IMIX shard are timed three ways in one process, interleaved: no collective (comm=None, what N = 1 runs), the product
-form (deferred counter rows, dk_rx_flow_counts_allreduce_to on a side stream after each step's counts complete), and
-the product collective without deferral (a reduce launch per step). If the persistent one-workgroup-per-CU kernels
-kept RCCL's kernel from running beside them, the step would grow by the collective's own time (measured alone too).
+IMIX shard are timed in one process, interleaved: no collective (comm=None, what N = 1 runs), the all-reduce after
+every step (deferred counter rows, and without deferral), after every 8 steps, and after every step with 8 CUs left
+free of the receive kernel. If the persistent kernels keep RCCL's kernel from running beside them, a step grows by
+the collective's own time (measured alone too).
 """
 import argparse
 import json
@@ -40,12 +40,18 @@ def main():
         eng = RxEngine(Config(synth.BOB_IPV4))
         batch, flows, tr = bench.make_batch(eng, wl, 0, synth.SEED)
         res = eng.results(batch.n)
-        modes = {"no_collective": (None, True), "rccl_deferred": (comm, True), "rccl_reduce_per_step": (comm, False)}
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        per_cu = 1 if wl == "c2_tcp1500" else 3  # split kernel / staged kernel (rx_host.cpp launch_batch)
+        # mode: (communicator, deferred counters, gather every K steps, CUs left free for RCCL's kernel)
+        modes = {"no_collective": (None, True, 1, 0), "rccl_every_step": (comm, True, 1, 0),
+                 "rccl_every_step_no_defer": (comm, False, 1, 0), "rccl_every_8": (comm, True, 8, 0),
+                 "rccl_every_step_8_cus_free": (comm, True, 1, 8)}
         t = {m: [] for m in modes}
         bench.preheat(eng, batch, stream, 0.25)
         for _ in range(args.reps):
-            for m, (cm, defer) in modes.items():
-                sr = ShardedReceiver(eng, res, cm, stream, defer=defer)
+            for m, (cm, defer, every, free) in modes.items():
+                eng.set_tuning(grid=(cus - free) * per_cu if free else -1)
+                sr = ShardedReceiver(eng, res, cm, stream, defer=defer, gather_every=every)
                 for _ in range(3):
                     sr.step(batch)
                 sr.drain()
@@ -59,6 +65,7 @@ def main():
                 if cm is not None:
                     fo, vo = sr.counts()
                     assert int(vo.sum()) == (args.steps + 3) * batch.n, (m, int(vo.sum()))
+        eng.set_tuning()
         sr = ShardedReceiver(eng, res, comm, stream)
         coll = []
         for _ in range(10):
