@@ -91,7 +91,9 @@ class ShardedReceiver:
     every K batches keeps the totals exact at each gather and divides that cost by K.
     With comm=None (one GPU) there is one set and no collective."""
 
-    def __init__(self, engine, results, comm, stream, nbuf: int = 2, defer: bool = True, gather_every: int = 1):
+    def __init__(self, engine, results, comm, stream, nbuf: int = 2, defer: bool = True, gather_every: int = 1,
+                 side_stream: bool = True):
+        """side_stream=False issues the all-reduce on the launch stream itself (serialised between two kernels)."""
         import torch
 
         from .rx import RxResults
@@ -100,7 +102,7 @@ class ShardedReceiver:
         self.every = max(int(gather_every), 1)
         if comm is None:
             nbuf = 1
-        self.side = torch.cuda.Stream(device=stream.device) if comm is not None else None
+        self.side = (torch.cuda.Stream(device=stream.device) if side_stream else stream) if comm is not None else None
         results.zero_counts()
         self.res = [results]
         for _ in range(nbuf - 1):  # same per-frame arrays, own counters

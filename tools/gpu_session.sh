@@ -16,19 +16,18 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# 1. parity
-PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step t_part 400 $PYT tests/test_gpu_parity.py -k "full_size_c2 or deferred_counts or kernel_variants or tcp_fields or options"
-step t_multi 300 $PYT tests/test_gpu_multiproc.py
-step t_all 900 $PYT -m gpu tests
-step smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()"
-# 2. A/B: the LibOS record staged by the split kernel (head) vs stored between the frame reads (prev)
-V=build/variants
-H=demikernel_amd/libdk_rx.so
-step ab_libos 300 python3 tools/tune_ab.py --workload c2_tcp1500 --tcp-fields --reps 7 --iters 10 --lib $H --lib $V/prev.so "defer=1"
-step ab_c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --iters 10 --lib $H --lib $V/prev.so "defer=1"
-step ab_c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --iters 8 --lib $H --lib $V/prev.so "defer=1"
-step ab_c4 300 python3 tools/tune_ab.py --workload c4_imix --reps 7 --iters 10 --lib $H --lib $V/prev.so "defer=1"
-# 3. the collective beside the kernels: every step, every 8 steps, 8 CUs left free
-step overlap 400 python3 tools/overlap_collective.py --out $O/r04_overlap.json
+# 1. rocprofv3 evidence: kernel stats of the bench, FETCH/WRITE traffic per workload, C1/C3/TX/TCP kernel stats
+step profile 1000 bash tools/profile_bench.sh $TAG
+# 2. the collective beside the kernels (side stream / same stream, every 1 / 8 / 16 steps)
+step overlap 300 python3 tools/overlap_collective.py --out $O/r04_overlap.json
+# 3. IMIX LDS bank conflicts by structure: as run / socket table probed in global memory (no LDS table) / no counters
+cd /tmp
+SQ="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_LDS_ATOMIC SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+step lds_asis 120 rocprofv3 --pmc $SQ --kernel-include-regex "dk_rx_kernel" -T -d $O/lds_asis -o run --output-format csv -- \
+  python3 $R/tools/kbench.py --workload c4_imix --iters 8 --defer
+DK_RX_LDS_TABLE=0 step lds_notable 120 rocprofv3 --pmc $SQ --kernel-include-regex "dk_rx_kernel" -T -d $O/lds_notable -o run \
+  --output-format csv -- python3 $R/tools/kbench.py --workload c4_imix --iters 8 --defer
+step lds_nocount 120 rocprofv3 --pmc $SQ --kernel-include-regex "dk_rx_kernel" -T -d $O/lds_nocount -o run --output-format csv \
+  -- python3 $R/tools/kbench.py --workload c4_imix --iters 8 --no-counts
+cd $R
 echo done

@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="")
     args = ap.parse_args()
@@ -43,15 +43,20 @@ def main():
         cus = torch.cuda.get_device_properties(0).multi_processor_count
         per_cu = 1 if wl == "c2_tcp1500" else 3  # split kernel / staged kernel (rx_host.cpp launch_batch)
         # mode: (communicator, deferred counters, gather every K steps, CUs left free for RCCL's kernel)
-        modes = {"no_collective": (None, True, 1, 0), "rccl_every_step": (comm, True, 1, 0),
-                 "rccl_every_step_no_defer": (comm, False, 1, 0), "rccl_every_8": (comm, True, 8, 0),
-                 "rccl_every_step_8_cus_free": (comm, True, 1, 8)}
+        # mode: (communicator, deferred counters, gather every K steps, CUs left free, collective on a side stream)
+        modes = {"no_collective": (None, True, 1, 0, True), "rccl_every_step": (comm, True, 1, 0, True),
+                 "rccl_every_step_no_defer": (comm, False, 1, 0, True), "rccl_every_8": (comm, True, 8, 0, True),
+                 "rccl_every_8_same_stream": (comm, True, 8, 0, False),
+                 "rccl_every_16": (comm, True, 16, 0, True),
+                 "rccl_every_16_same_stream": (comm, True, 16, 0, False),
+                 "rccl_every_step_same_stream": (comm, True, 1, 0, False),
+                 "rccl_every_step_8_cus_free": (comm, True, 1, 8, True)}
         t = {m: [] for m in modes}
         bench.preheat(eng, batch, stream, 0.25)
         for _ in range(args.reps):
-            for m, (cm, defer, every, free) in modes.items():
+            for m, (cm, defer, every, free, side) in modes.items():
                 eng.set_tuning(grid=(cus - free) * per_cu if free else -1)
-                sr = ShardedReceiver(eng, res, cm, stream, defer=defer, gather_every=every)
+                sr = ShardedReceiver(eng, res, cm, stream, defer=defer, gather_every=every, side_stream=side)
                 for _ in range(3):
                     sr.step(batch)
                 sr.drain()
