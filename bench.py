@@ -126,7 +126,7 @@ def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
 
     from demikernel_amd.shard import ShardedReceiver
 
-    sr = ShardedReceiver(eng, res, comm, stream, gather_every=GATHER_EVERY)
+    sr = ShardedReceiver(eng, res, comm, stream, gather_every=GATHER_EVERY, side_stream=False)
     preheat(eng, batches[0], stream, PREHEAT_S)
     for k in range(warmup):
         sr.step(batches[k % len(batches)])
@@ -577,8 +577,9 @@ def main():
                   f"communicator of include/dk_comm.h", file=sys.stderr, flush=True)
             sys.exit(3)
         collective = (f"dk_rx_flow_counts_allreduce_to (RCCL all-reduce of accumulating u64 flow + verdict counters) "
-                      f"every {GATHER_EVERY} batches and after the last, on a side stream, double-buffered counter "
-                      f"sets (node-wide counts exact at every gather)")
+                      f"every {GATHER_EVERY} batches and after the last, on the launch stream (RCCL's kernel does not "
+                      f"run beside the receive kernels: profiles/r04_overlap.json), double-buffered counter sets "
+                      f"(node-wide counts exact at every gather)")
 
     eng = RxEngine(Config(synth.BOB_IPV4), device=dev)
     stream = torch.cuda.current_stream(dev)
