@@ -9,7 +9,8 @@ their GPU; frame bytes never cross xGMI.
 `ShardedReceiver` is the per-rank driver bench.py --gpus N runs (one process per GPU under torchrun): it bootstraps
 the RCCL communicator (rank 0's id handed out over the launcher's process group), receives the rank's shard into
 accumulating counters (each batch's counter rows completed inside the next batch's kernel) and all-reduces them out of
-place on a side stream, overlapping the following kernels; no step zeroes anything. The CPU rehearsal (tests/test_multiproc.py, gloo, world size 2)
+place every K batches (bench.py: K = 8, on the launch stream, since RCCL's kernel does not run beside the persistent
+receive kernels); no step zeroes anything. The CPU rehearsal (tests/test_multiproc.py, gloo, world size 2)
 drives the same sharding and bootstrap code with torch's all_reduce standing in for the RCCL call; on the GPU the
 RCCL call runs through a 1-rank communicator test, and bench.py --gpus 2 runs as two child ranks on one GPU
 (tests/test_gpu_multiproc.py, gloo counts: RCCL refuses two ranks on one device).
@@ -82,7 +83,7 @@ class ShardedReceiver:
     kernel leaves its counter rows pending (DK_RX_BATCH_DEFER_COUNTS) and the next step's kernel adds them inside its
     own launch, so no step pays a dependent second launch for its counters. Once a period's counts are complete (after
     the first kernel of the next period), dk_rx_flow_counts_allreduce_to sums that set over the ranks into the slot's
-    node-wide totals on a side stream, overlapping the following kernels. A set is changed again only after its
+    node-wide totals, on a side stream (side_stream=True) or between two kernels on the launch stream. A set is changed again only after its
     previous all-reduce has read it (one event wait). flush() completes the last step and gathers it. The node-wide
     counts of every step so far are the sum of the slots' totals (`counts()`), exact at every gather.
 
