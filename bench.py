@@ -6,7 +6,8 @@
 A step = one dk_rx_process pass over one HBM-resident batch of the workload (default: BASELINE config 2,
 1,048,576 x 1500 B IPv4/TCP frames over 1,024 flows, 1 % corrupted tail), plus, for N > 1, the RCCL all-reduce of the
 per-flow packet counts (dk_rx_flow_counts_allreduce over a dk_comm.h communicator: the only collective on this path,
-on a side stream, overlapping the next step's kernel). Weak scaling: every rank owns one batch (its packet shard).
+every --gather-every batches on the launch stream). Weak scaling: every rank owns one batch (its packet
+shard).
 `value` = sum of frame bytes processed by all ranks / max-over-ranks time.  Rank 0 prints one JSON line.
 At N = 1 the line also carries the other BASELINE configs as extras (C3 64 B UDP, C4 IMIX shard, C5 10k-flow shard
 kernel-only and end to end from pinned host memory, C1-shaped CPU baseline), each with its own roofline fields.
@@ -118,8 +119,8 @@ GATHER_EVERY = 8  # batches per all-reduce of the counters at N > 1 (bench --gat
 def time_kernel(eng, batches, res, steps, warmup, stream, dist=None, comm=None):
     """Run the untimed preheat, then warmup + timed steps. A step = the receive pass over one batch, whose counter
     rows the next step's kernel completes (DK_RX_BATCH_DEFER_COUNTS; the last step's by one flush launch inside the
-    timed region), + for N > 1 the all-reduce of each step's counters over RCCL (ShardedReceiver: double-buffered
-    counters, the collective on a side stream overlapping the following kernels). Returns (wall seconds for `steps`,
+    timed region), + for N > 1 the all-reduce of the counters over RCCL every GATHER_EVERY steps and after the last
+    (ShardedReceiver: double-buffered accumulating counters, the collective on the launch stream). Returns (wall seconds for `steps`,
     per-step seconds on the launch stream from HIP events around the timed region incl. the flush, per-step collective
     seconds measured unoverlapped)."""
     import torch
@@ -415,7 +416,7 @@ def rx_kernel_name(frame_bytes, n):
     """The receive kernel family the host picks for a batch (rx_host.cpp launch_batch: mean blob bytes per frame; the
     blob holds 64-byte-aligned slots, so its size is rounded up per frame)."""
     per = frame_bytes // max(n, 1)
-    return ("dk_rx_small_kernel" if per <= 96 else "dk_rx_split_kernel" if per >= 1024 else
+    return ("dk_rx_small_kernel" if per <= 96 else "dk_rx_split_kernel" if per >= 1280 else
             "dk_rx_kernel (staged)" if per >= 128 else "dk_rx_kernel")
 
 

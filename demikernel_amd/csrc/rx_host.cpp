@@ -265,7 +265,10 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
         }
     }
     // Kernel instantiation, schedule and resident workgroups per CU (measured, DESIGN.md §8 "Tuning log"):
-    //  - >= 1 KiB of blob per frame: the split kernel (stream waves + finish waves, one 512-thread workgroup per CU);
+    //  - >= 1,280 bytes of blob per frame (the frames a stream wave streams with 6 loads per lane): the split kernel
+    //    (stream waves + finish waves, one 512-thread workgroup per CU). Below, the staged kernel's 12 waves per CU
+    //    keep more medium frames in flight (round 4, C1's 1078-byte frames: staged 27.9 vs split 30.2 us at 131,072
+    //    frames, 177.9 vs 186.8 at 1M; 1500-byte frames: split ahead from 131,072 frames up, C5 -5.5 %);
     //  - >= 128 bytes: the result-staging kernel (stores leave in one burst per 6 chunks instead of between the frame
     //    reads; -11 % at C2 before the split kernel, -4 % IMIX);
     //  - <= 96 bytes: the small-frame kernel (issue/latency-bound, wants occupancy);
@@ -273,7 +276,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     // Never more workgroups per CU than the occupancy admits (large socket tables take LDS).
     const uint64_t bytes_per_frame = size_hint / p.n;
     p.stage = bytes_per_frame >= 128 ? 1u : 0u;
-    p.split = bytes_per_frame >= 1024 ? 1u : 0u;
+    p.split = bytes_per_frame >= 1280 ? 1u : 0u;
     p.small = bytes_per_frame <= 96 ? 1u : 0u;
     if (T.stage >= 0) p.stage = T.stage ? 1u : 0u;
     if (T.split >= 0) p.split = T.split ? 1u : 0u;
@@ -311,6 +314,17 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
     const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
     uint32_t grid = std::min((ntiles + tiles_per_wg - 1) / tiles_per_wg, per_cu * c->cu_count);
+#ifndef DK_FEW_TILES_SCHED1
+#define DK_FEW_TILES_SCHED1 0
+#endif
+    // Fewer 256-frame tiles than resident workgroups (C1: 512 tiles, 768 staged workgroups): every wave of the full
+    // grid takes an even contiguous share of the frames (sched 1: one partial chunk per wave) instead of whole chunks
+    // for two thirds of the waves.
+    if (DK_FEW_TILES_SCHED1 && T.sched < 0 && T.grid <= 0 && !p.small && !p.split && ntiles < per_cu * c->cu_count &&
+        p.n >= 16u * 4u * per_cu * c->cu_count) {
+        p.sched = 1;
+        grid = per_cu * c->cu_count;
+    }
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);

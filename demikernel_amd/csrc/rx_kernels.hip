@@ -1256,6 +1256,16 @@ void dk_rx_kernel(RxParams P) {
     __syncthreads();
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
+#ifndef DK_STAGED_PRIO
+#define DK_STAGED_PRIO 0
+#endif
+#if DK_STAGED_PRIO  // experiment (as the small kernel): waves with one chunk more than the rest issue first
+    {
+        uint32_t cc, ll;
+        const uint32_t kmin = ((P.n + 63) / 64) / (gridDim.x * kWaves);
+        if (r.chunk(kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_STAGED_PRIO);
+    }
+#endif
     StgRec<false> stg[kStage ? kStageK : 1];
     uint32_t nstg = 0;  // wave-uniform
     uint32_t c, lim, nc, nlim;
@@ -1469,6 +1479,9 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
 #ifndef DK_SMALL_DEFER
 #define DK_SMALL_DEFER 1
 #endif
+#ifndef DK_SMALL_PRIO
+#define DK_SMALL_PRIO 1
+#endif
 template <bool kShift>
 __device__ __forceinline__ bool small_fast_eligible(const FrameDesc<kShift>& F, uint32_t len, const RegAcc& R) {
     const bool ihl5 = ((R.w[3] >> 16) & 0x0Fu) == 5u;
@@ -1595,12 +1608,41 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 #endif
     DK_STAMP(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
+    const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
+#ifndef DK_SMALL_DESC_EARLY
+#define DK_SMALL_DESC_EARLY 1
+#endif
+    uint32_t c, lim, c1 = 0, lim1 = 0, c2 = 0, lim2 = 0;
+    bool have = r.chunk(0, c, lim);
+    bool have1 = have && r.chunk(1, c1, lim1);
+    uint32_t off = 0, len = 0, off1 = 0, len1 = 0;
+#if DK_SMALL_DESC_EARLY  // the first two chunks' descriptors in flight during the LDS init and the barrier
+    if (have && c + r.lane_off < lim) {
+        off = P.off[c + r.lane_off];
+        len = P.len[c + r.lane_off];
+    }
+    if (have1 && c1 + r.lane_off < lim1) {
+        off1 = P.off[c1 + r.lane_off];
+        len1 = P.len[c1 + r.lane_off];
+    }
+#endif
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
     __syncthreads();
-
-    const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
+#ifdef DK_DIAG_STAMPS
+    DK_STAMP_T(11, __builtin_amdgcn_s_memtime());
+#endif
+    // The grid is one generation of waves and the chunks do not divide evenly: the waves with one chunk more than the
+    // rest (the last round's) set the launch's length, so they issue first on their SIMD (s_setprio; round 4: C3
+    // -2.6 % with the first descriptors loaded before the barrier, DK_SMALL_DESC_EARLY).
+#if DK_SMALL_PRIO
+    {
+        uint32_t cc, ll;
+        const uint32_t kmin = ((P.n + 63) / 64) / (gridDim.x * kSmallWaves);
+        if (r.chunk(kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_SMALL_PRIO);
+    }
+#endif
     const Blob B(P.frames, P.frames_bytes);
     SmallLds& W = s_wave[wv];
     // Pipeline: descriptors are loaded two chunks ahead. With DK_SMALL_LATE (default) chunk k + 2's descriptor loads
@@ -1611,10 +1653,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 #ifndef DK_SMALL_LATE
 #define DK_SMALL_LATE 1
 #endif
-    uint32_t c, lim, c1 = 0, lim1 = 0, c2 = 0, lim2 = 0;
-    bool have = r.chunk(0, c, lim);
-    bool have1 = have && r.chunk(1, c1, lim1);
-    uint32_t off = 0, len = 0, off1 = 0, len1 = 0;
+#if !DK_SMALL_DESC_EARLY
     if (have && c + r.lane_off < lim) {
         off = P.off[c + r.lane_off];
         len = P.len[c + r.lane_off];
@@ -1623,6 +1662,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = P.off[c1 + r.lane_off];
         len1 = P.len[c1 + r.lane_off];
     }
+#endif
     Chunk C;
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
     const uint32_t nw = gridDim.x * kSmallWaves, gw = blockIdx.x * kSmallWaves + wv;  // deferral mask index k nw + gw

@@ -16,18 +16,14 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# 1. rocprofv3 evidence: kernel stats of the bench, FETCH/WRITE traffic per workload, C1/C3/TX/TCP kernel stats
-step profile 1000 bash tools/profile_bench.sh $TAG
-# 2. the collective beside the kernels (side stream / same stream, every 1 / 8 / 16 steps)
-step overlap 300 python3 tools/overlap_collective.py --out $O/r04_overlap.json
-# 3. IMIX LDS bank conflicts by structure: as run / socket table probed in global memory (no LDS table) / no counters
-cd /tmp
-SQ="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_LDS_ATOMIC SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE"
-step lds_asis 120 rocprofv3 --pmc $SQ --kernel-include-regex "dk_rx_kernel" -T -d $O/lds_asis -o run --output-format csv -- \
-  python3 $R/tools/kbench.py --workload c4_imix --iters 8 --defer
-DK_RX_LDS_TABLE=0 step lds_notable 120 rocprofv3 --pmc $SQ --kernel-include-regex "dk_rx_kernel" -T -d $O/lds_notable -o run \
-  --output-format csv -- python3 $R/tools/kbench.py --workload c4_imix --iters 8 --defer
-step lds_nocount 120 rocprofv3 --pmc $SQ --kernel-include-regex "dk_rx_kernel" -T -d $O/lds_nocount -o run --output-format csv \
-  -- python3 $R/tools/kbench.py --workload c4_imix --iters 8 --no-counts
-cd $R
+L=demikernel_amd/libdk_rx.so
+V=build/variants
+# 1. the GPU suite at this build
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+# 2. C3: priority / early descriptors, each on and off
+step c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 11 --lib $L --lib $V/noprio.so --lib $V/prio2.so --lib $V/noearly.so --lib $V/none.so "defer=1"
+# 3. C1 by the host rule (staged now) vs the split kernel
+step c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 4 --reps 9 --lib $L --lib $V/fewsched1.so "defer=1" "defer=1,split=1"
+# 4. IMIX: priority for the staged kernel's waves with one chunk more
+step imix 300 python3 tools/tune_ab.py --workload c4_imix --rotate 2 --reps 9 --lib $L --lib $V/stprio1.so "defer=1"
 echo done

@@ -2,7 +2,7 @@
 """Per-wave timeline of the small-frame kernel from a -DDK_DIAG_STAMPS build (tuning tool).
 
     python tools/stamps.py build/variants/stamps.so [--workload c3_udp64]
-Stamps per wave (s_memtime): 0 entry, 1 after setup, per chunk k < 3: 2+3k frames in registers, 3+3k parsed +
+Stamps per wave (s_memtime): 0 entry, 11 after the workgroup barrier, 1 after setup, per chunk k < 3: 2+3k frames in registers, 3+3k parsed +
 probed + results stored, 4+3k counted; 14 before the counter flush, 15 exit; 12/13 s_memrealtime at entry/exit;
 16+5k..19+5k: rx_finish sub-phases of chunk k (32 slots per wave). Prints quantiles of each
 phase (µs) and the wave start/end spread over the launch.
@@ -68,7 +68,7 @@ def timeline(args, e, lib, rot, r, nw):
         us = lambda x: x / mhz  # noqa: E731  (s_memtime: shader clock ticks -> µs)
         q = lambda a: [round(float(v), 2) for v in np.percentile(a, [0, 10, 50, 90, 100])]  # noqa: E731
         row = {"mhz": round(mhz, 1), "waves": int(used.sum()), "start": q(rt(st[:, 12] - t0)), "exit": q(rt(st[:, 13] - t0)),
-               "setup": q(us(st[:, 1] - st[:, 0])), "flush": q(us(st[:, 15] - st[:, 14]))}
+               "setup": q(us(st[:, 1] - st[:, 0])), "to_barrier": q(us(st[:, 11] - st[:, 0])), "flush": q(us(st[:, 15] - st[:, 14]))}
         for k in range(3):
             have = st[:, 2 + 3 * k] != 0
             if not have.any():
