@@ -314,17 +314,6 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
     const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
     uint32_t grid = std::min((ntiles + tiles_per_wg - 1) / tiles_per_wg, per_cu * c->cu_count);
-#ifndef DK_FEW_TILES_SCHED1
-#define DK_FEW_TILES_SCHED1 0
-#endif
-    // Fewer 256-frame tiles than resident workgroups (C1: 512 tiles, 768 staged workgroups): every wave of the full
-    // grid takes an even contiguous share of the frames (sched 1: one partial chunk per wave) instead of whole chunks
-    // for two thirds of the waves.
-    if (DK_FEW_TILES_SCHED1 && T.sched < 0 && T.grid <= 0 && !p.small && !p.split && ntiles < per_cu * c->cu_count &&
-        p.n >= 16u * 4u * per_cu * c->cu_count) {
-        p.sched = 1;
-        grid = per_cu * c->cu_count;
-    }
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);

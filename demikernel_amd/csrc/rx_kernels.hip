@@ -1256,16 +1256,6 @@ void dk_rx_kernel(RxParams P) {
     __syncthreads();
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
-#ifndef DK_STAGED_PRIO
-#define DK_STAGED_PRIO 0
-#endif
-#if DK_STAGED_PRIO  // experiment (as the small kernel): waves with one chunk more than the rest issue first
-    {
-        uint32_t cc, ll;
-        const uint32_t kmin = ((P.n + 63) / 64) / (gridDim.x * kWaves);
-        if (r.chunk(kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_STAGED_PRIO);
-    }
-#endif
     StgRec<false> stg[kStage ? kStageK : 1];
     uint32_t nstg = 0;  // wave-uniform
     uint32_t c, lim, nc, nlim;
@@ -1635,7 +1625,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 #endif
     // The grid is one generation of waves and the chunks do not divide evenly: the waves with one chunk more than the
     // rest (the last round's) set the launch's length, so they issue first on their SIMD (s_setprio; round 4: C3
-    // -2.6 % with the first descriptors loaded before the barrier, DK_SMALL_DESC_EARLY).
+    // -2.1 % together with the first descriptors loaded before the barrier, DK_SMALL_DESC_EARLY).
 #if DK_SMALL_PRIO
     {
         uint32_t cc, ll;
