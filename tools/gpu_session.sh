@@ -18,17 +18,10 @@ export TMPDIR=/tmp
 
 L=demikernel_amd/libdk_rx.so
 V=build/variants
-# 0. variants' results against the oracle (their timings count only if they are bit-exact)
-echo "== vparity"
-timeout -k 10 300 python3 tools/variant_parity.py --lib $V/tiny.so --lib $V/fewsched1.so --lib $V/stprio1.so > $O/vparity.log 2>&1
-rc=$?; grep -h '^{' $O/vparity.log | cut -c1-300
-if [ $rc -gt 1 ]; then echo "vparity rc=$rc"; tail -20 $O/vparity.log; exit 10; fi  # 1 = a mismatch: keep going
-# 1. the GPU suite at this build
-step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-# 2. C3: priority / early descriptors, each on and off
-step c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 11 --lib $L --lib $V/noprio.so --lib $V/prio2.so --lib $V/noearly.so --lib $V/none.so "defer=1"
-# 3. C1 by the host rule (staged now) vs the split kernel
-step c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 4 --reps 9 --lib $L --lib $V/fewsched1.so "defer=1" "defer=1,split=1"
-# 4. IMIX: priority for the staged kernel's waves with one chunk more
-step imix 300 python3 tools/tune_ab.py --workload c4_imix --rotate 2 --reps 9 --lib $L --lib $V/stprio1.so --lib $V/nosmall.so --lib $V/tiny.so "defer=1"
+# 1. MALL: one batch re-read every launch vs 2 / 3 rotating batches (the bench's C2 and IMIX lines use one)
+for w in c2_tcp1500 c4_imix c5_tcp1500_10k; do
+  for r in 1 2 3; do
+    step mall_${w}_r$r 300 python3 tools/tune_ab.py --workload $w --rotate $r --reps 7 "defer=1"
+  done
+done
 echo done
