@@ -16,12 +16,13 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-L=demikernel_amd/libdk_rx.so
-V=build/variants
-# 1. MALL: one batch re-read every launch vs 2 / 3 rotating batches (the bench's C2 and IMIX lines use one)
-for w in c2_tcp1500 c4_imix c5_tcp1500_10k; do
-  for r in 1 2 3; do
-    step mall_${w}_r$r 300 python3 tools/tune_ab.py --workload $w --rotate $r --reps 7 "defer=1"
-  done
-done
+# 1. the GPU suite, smoke() and the bench line at this build
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+# 2. rocprofv3 evidence: kernel stats of the bench, FETCH/WRITE traffic per workload, C1/C3/TX/TCP kernel stats
+step profile 1000 bash tools/profile_bench.sh $TAG
+# 3. SQ counters of the kernels changed this round: C1 (staged now), C3 (priority + early descriptors)
+step sq_c1 300 bash tools/pmc_kernel.sh c1_tcp1078 ${TAG}_c1 --defer --rotate 3
+step sq_c3 300 bash tools/pmc_kernel.sh c3_udp64 ${TAG}_c3 --defer --rotate 8
 echo done
