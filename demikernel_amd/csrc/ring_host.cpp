@@ -8,9 +8,12 @@
 #include <hip/hip_runtime.h>
 #include <linux/if_packet.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstddef>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "../../include/dk_ring.h"
 
@@ -36,6 +39,10 @@ int scan_block(const uint8_t* ring, uint64_t base, uint32_t block_size, uint32_t
         len[n + k] = (uint16_t)t.tp_snaplen;
         if (k + 1 < h.num_pkts) {
             if (t.tp_next_offset == 0) return EBADMSG;
+            // the chain is a dependent walk through the block (one cache miss per frame): fetch the header a few
+            // frames ahead, assuming the stride repeats (any address inside the block is harmless)
+            const uint64_t ahead = p + 4ull * t.tp_next_offset;
+            if (ahead < block_size) __builtin_prefetch(b + ahead, 0, 0);
             p += t.tp_next_offset;
         }
     }
@@ -74,6 +81,9 @@ struct PinnedDescs {
 };
 thread_local PinnedDescs t_descs;
 
+constexpr uint32_t kScanThreads = 8;          // host threads a long ring scan may use
+constexpr uint32_t kScanBlocksPerThread = 4;  // below 2 x this many ready blocks the scan stays on the calling thread
+
 uint32_t* status_word(uint8_t* ring, uint64_t base) {
     return reinterpret_cast<uint32_t*>(ring + base + offsetof(tpacket_block_desc, hdr.bh1.block_status));
 }
@@ -103,31 +113,71 @@ int dk_ring_scan_tpacket3(const void* ring, uint64_t ring_bytes, uint32_t block_
     const uint64_t nring = ring_bytes / block_size;
     if (first_block >= nring) return EINVAL;
     uint8_t* r = const_cast<uint8_t*>(static_cast<const uint8_t*>(ring));
+    // Pass 1, block descriptors only: the ready blocks that fit in cap and each one's first output slot. A block that
+    // would overflow cap ends the scan before it (ENOSPC when it is the first: nothing consumed).
+    std::vector<uint32_t> start;
     uint32_t n = 0, k = 0;
-    int rc = 0;
     for (; k < nblocks && k < nring; k++) {
         const uint64_t base = ((first_block + k) % nring) * block_size;
         uint32_t status;
         __atomic_load(status_word(r, base), &status, __ATOMIC_ACQUIRE);  // pairs with the kernel's block close
         if (!(status & TP_STATUS_USER)) break;                            // still the kernel's
-        rc = scan_block(r, base, block_size, off, len, cap, n);
-        if (rc && k > 0) {  // the blocks before it are complete: return them; the next call starts at this block
-            rc = 0;
+        tpacket_block_desc bd;
+        std::memcpy(&bd, r + base, sizeof(bd));
+        const uint32_t np = bd.hdr.bh1.num_pkts;
+        if ((uint64_t)n + np > cap) {
+            if (k == 0) return ENOSPC;
             break;
         }
-        if (rc == EBADMSG) {  // the first block is malformed: report it, consumed (the caller hands it back)
-            k++;
-            break;
-        }
-        if (rc) break;  // ENOSPC with the first block: it alone holds more than cap frames, nothing consumed
+        start.push_back(n);
+        n += np;
         if (n == cap) {  // full: the next block cannot fit
             k++;
             break;
         }
     }
+    const uint32_t nb = k;
+    // Pass 2: each block's header chain into its slots. The chains are independent, so a long scan walks blocks on
+    // several threads (the walk is one cache miss per frame; ~14 ns a frame on one core of the GPU box).
+    std::vector<int> brc(nb, 0);
+    auto walk = [&](uint32_t j0, uint32_t j1) {
+        for (uint32_t j = j0; j < j1; j++) {
+            uint32_t pos = start[j];
+            brc[j] = scan_block(r, ((first_block + j) % nring) * block_size, block_size, off, len, cap, pos);
+            if (brc[j]) break;  // later blocks of this range are not returned
+        }
+    };
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t nt = std::min({kScanThreads, hw, nb / kScanBlocksPerThread});
+    bool parallel = false;
+    if (nt > 1) {
+        std::vector<std::thread> th;
+        try {
+            for (uint32_t t = 1; t < nt; t++) th.emplace_back(walk, nb * t / nt, nb * (t + 1) / nt);
+            parallel = true;
+        } catch (...) {  // no threads: the calling thread walks everything
+        }
+        walk(0, parallel ? nb / nt : nb);
+        for (std::thread& t : th) t.join();
+    } else {
+        walk(0, nb);
+    }
+    // The first malformed block ends the scan: the blocks before it are returned; when it is the first, it is reported
+    // (EBADMSG) and counted as consumed so that the caller hands it back.
+    for (uint32_t j = 0; j < nb; j++) {
+        if (!brc[j]) continue;
+        if (j == 0) {
+            *n_frames = 0;
+            *n_blocks = 1;
+            return brc[j];
+        }
+        *n_frames = start[j];
+        *n_blocks = j;
+        return 0;
+    }
     *n_frames = n;
-    *n_blocks = k;
-    return rc;
+    *n_blocks = nb;
+    return 0;
 }
 
 int dk_ring_release_tpacket3(void* ring, uint64_t ring_bytes, uint32_t block_size, uint32_t first_block,

@@ -113,6 +113,33 @@ def test_malformed_later_block_returns_good_prefix_then_is_consumed():
     assert nb3 == used - 2 and np.array_equal(o3, eoff[eoff // bs >= 2])
 
 
+def test_long_scan_on_several_threads():
+    """A scan over many ready blocks walks them on several host threads (ring_host.cpp: 8 or more blocks); the result is
+    the sequential walk's: every frame in ring order, a capacity cut at a block boundary, a malformed block in a later
+    thread's range returning the good prefix, and that block reported (EBADMSG, consumed) when a scan starts at it."""
+    blob, off, lens = frames(12000, seed=9)
+    bs = 1 << 16
+    ring, used, eoff, elen = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+    assert used >= 40
+    r = RG.TpacketRing(ring, bs, register=False)
+    o, ln, nb = r.scan(0, used, len(off))
+    assert nb == used and np.array_equal(o, eoff) and np.array_equal(ln, elen)
+    per_block = np.bincount((eoff // bs).astype(np.int64), minlength=used)
+    cut = int(per_block[:29].sum()) + 3  # blocks 0..28 fit, block 29 does not
+    o, _, nb = r.scan(0, used, cut)
+    assert nb == 29 and np.array_equal(o, eoff[eoff // bs < 29])
+    bad = 31
+    first_pkt = bad * bs + RG.BLOCK_DESC_BYTES
+    ring[first_pkt:first_pkt + 4] = 0  # tp_next_offset 0 on a packet that is not the block's last
+    o, _, nb = r.scan(0, used, len(off))
+    assert nb == bad and np.array_equal(o, eoff[eoff // bs < bad])
+    with pytest.raises(Fail) as e:
+        r.scan(bad, used - bad, len(off))
+    assert e.value.errno == EBADMSG and e.value.blocks == 1
+    o, _, nb = r.scan(bad + 1, used - bad - 1, len(off))
+    assert nb == used - bad - 1 and np.array_equal(o, eoff[eoff // bs > bad])
+
+
 def load_live_fixture():
     """The ring a live AF_PACKET socket on `lo` filled (tests/golden/make_ring_fixture.py), in page-aligned memory."""
     import os
