@@ -343,17 +343,21 @@ def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=5):
     r = RG.TpacketRing(ring, block_size)
     res = RxResults(n, len(flows), host=True)
     nbytes = int(elen.astype(np.int64).sum())
-    rates = []
+    rates, scans = [], []
     try:
         for _ in range(reps):
             t = time.perf_counter()
             nf, nb = r.receive(eng, 0, used, res)
             rates.append(nbytes / (time.perf_counter() - t) / 1e9)
             assert nf == n and nb == used
+            t = time.perf_counter()  # the host's share: the block scan alone (dk_ring_scan_tpacket3)
+            r.scan(0, used, n)
+            scans.append(time.perf_counter() - t)
     finally:
         r.close()
     return {"gbps": round(float(np.median(rates)), 2), "gbps_max": round(max(rates), 2), "frames": n, "bytes": nbytes,
             "blocks": used, "block_size": block_size, "reps": reps, "stat": "median",
+            "host_scan_ms": round(float(np.median(scans)) * 1e3, 3),
             "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
 
 

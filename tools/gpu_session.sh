@@ -16,13 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-L=demikernel_amd/libdk_rx.so
-V=build/variants
-echo "== vparity"
-timeout -k 10 300 python3 tools/variant_parity.py --lib $V/pair.so > $O/vparity.log 2>&1
-rc=$?; grep -h '^{' $O/vparity.log | cut -c1-200
-if [ $rc -gt 1 ]; then echo "vparity rc=$rc"; tail -20 $O/vparity.log; exit 10; fi
-# small-frame kernel: two chunks per iteration (both windows and both table loads in flight), 4 waves/SIMD
-step c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 11 --lib $L --lib $V/pair.so "defer=1"
-step c3rp 300 python3 tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 7 --lib $L --lib $V/pair.so "defer=1"
+# the GPU suite, smoke() and the bench line at this build
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 echo done
