@@ -60,8 +60,9 @@ def assert_same(got, exp, ctx=""):
             raise AssertionError(f"{ctx}: '{k}' differs at {bad}: got {v[bad]} exp {e[bad]}{extra}")
 
 
-def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None, dst_ip=True):
-    got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes, aligned16=aligned16, dst_ip=dst_ip)
+def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None, dst_ip=True, tcp_fields=True):
+    got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes, aligned16=aligned16, dst_ip=dst_ip,
+                  tcp_fields=tcp_fields)
     exp = run_oracle(blob, off, lens, flows, cfg, frames_bytes=frames_bytes)
     assert_same(got, exp, ctx)
     return got
@@ -101,15 +102,17 @@ def test_random_batches(torch_cuda, mix, hint):
     assert (got["meta"] & 0xFF <= 1).mean() > 0.9
 
 
+@pytest.mark.parametrize("record", ["libos", "headline"])
 @pytest.mark.parametrize("grid", [None, "7"])
 @pytest.mark.parametrize("sched", ["0", "1"])
 @pytest.mark.parametrize("family", ["unstaged", "staged", "split", "small"])
-def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
+def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid, record):
     """Every shipped kernel family (results stored per chunk / staged in registers / split stream+finish waves /
     small-frame kernel, whose frames past the 64-byte window are summed wave-wide) under both wave schedules, with a
     grid small enough that each wave walks many chunks (staged results flushed mid-loop and at exit) and with the
     default grid. The split kernel always walks sched 0. Under sched 1 every family writes the 20-byte layout (no
-    dst_ip, ABI 3)."""
+    dst_ip, ABI 3). Both records: with the TCP fields (the LibOS record) and without (the 24-byte record bench.py
+    times), i.e. every instantiation of every family."""
     monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
     monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
     monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
@@ -122,8 +125,9 @@ def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid):
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.05, tr))
     perm = np.random.default_rng(8).permutation(n)
-    got = check(blob, off[perm], lens[perm], flows, ctx=f"{family} sched={sched} grid={grid}", dst_ip=sched != "1")
-    assert ("dst_ip" in got) == (sched != "1")
+    got = check(blob, off[perm], lens[perm], flows, ctx=f"{family} sched={sched} grid={grid} {record}",
+                dst_ip=sched != "1", tcp_fields=record == "libos")
+    assert ("dst_ip" in got) == (sched != "1") and ("tcp_seq" in got) == (record == "libos")
 
 
 @pytest.mark.parametrize("family", ["staged", "unstaged"])
@@ -520,7 +524,7 @@ def test_tpacket3_ring_path_matches_oracle(torch_cuda):
         eng.close()
 
 
-def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, host_checksums=False):
+def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, host_checksums=False, record="libos", defer=False):
     """A batch at a BASELINE config's full size with a `corrupt` tail (synth.corruption_plan), compared with the oracle
     on EVERY frame: all nine result arrays and both counter arrays of the whole batch, bit for bit (the oracle runs
     over the host's CPUs, OraclePeer.process_par). Plus the properties the workload is built for: every intact frame
@@ -531,6 +535,9 @@ def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, host_checksums=Fa
     device and checksummed by dk_tx_checksum, and the whole-batch oracle comparison catches any common-mode error of
     the two kernels (the oracle sums every segment itself). TCP/UDP checksum VALUES are pinned by no reference vector
     (SURVEY.md §4): they rest on the oracle's restatement plus the independent implementation.
+    record: "libos" = the 36-byte record with tcp_seq / ack / win (the kernels' TCP-field instantiations), "headline" =
+    the 24-byte record bench.py times (the other instantiations). defer: counters deferred and completed by
+    dk_rx_counts_flush, as the bench runs them.
     Returns (engine, batch, traffic, results as numpy, host copy of the blob)."""
     import torch
 
@@ -548,10 +555,13 @@ def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, host_checksums=Fa
         lens = np.asarray(batch.len.cpu().numpy().view(np.uint16))
         synth.corrupt_device(batch, off, plan)
         blob = batch.blob.cpu().numpy()
-    r = eng.results(n, tcp_fields=True)
-    eng.receive_batch(batch, r)
+    r = eng.results(n, tcp_fields=record == "libos")
+    eng.receive_batch(batch, r, defer_counts=defer)
+    if defer:
+        eng.flush_counts()
     torch.cuda.synchronize()
     got = r.to_numpy()
+    assert ("tcp_seq" in got) == (record == "libos")
     ref = OraclePeer(ipv4(LOCAL))
     ref.set_flows(flows)
     exp = ref.process_par(blob, off, lens)
@@ -587,8 +597,9 @@ def test_full_size_c2(torch_cuda):
 
 
 def test_full_size_c2_device_built(torch_cuda):
-    """The bench's own C2 batch (device-generated, checksummed by dk_tx_checksum): whole batch bit-exact."""
-    full_size(1 << 20, 1486, synth.make_flows(1024))
+    """The bench's own C2 launch: its batch (device-generated, checksummed by dk_tx_checksum), its 24-byte record (the
+    split kernel's instantiation without the TCP fields) and its deferred counters: whole batch bit-exact."""
+    full_size(1 << 20, 1486, synth.make_flows(1024), record="headline", defer=True)
 
 
 def test_full_size_c3(torch_cuda):
@@ -596,11 +607,17 @@ def test_full_size_c3(torch_cuda):
     full_size(1 << 20, 50, synth.make_flows(1024, kind="udp"), seed=synth.SEED + 1)
 
 
+def test_full_size_c3_headline_record(torch_cuda):
+    """C3 as bench.py times it: the 24-byte record (the small-frame kernel without the TCP fields) and deferred
+    counters; whole batch bit-exact."""
+    full_size(1 << 20, 50, synth.make_flows(1024, kind="udp"), seed=synth.SEED + 2, record="headline", defer=True)
+
+
 def test_full_size_c4_imix_shard(torch_cuda):
     """BASELINE config 4's per-GPU shard (2M IMIX frames, 40/576/1500 B at 7:4:1) with a 1 % corrupted tail; whole
     batch bit-exact."""
     n = 1 << 21
-    full_size(n, synth.imix_ip_lengths(n, seed=5), synth.make_flows(1024), seed=5)
+    full_size(n, synth.imix_ip_lengths(n, seed=5), synth.make_flows(1024), seed=5, record="headline", defer=True)
 
 
 def test_c5_host_pipeline_10k_flows(torch_cuda):

@@ -16,13 +16,6 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-L=demikernel_amd/libdk_rx.so
-V=build/variants
-echo "== vparity"
-timeout -k 10 300 python3 tools/variant_parity.py --lib $V/m1.so --lib $V/m1u4.so > $O/vparity.log 2>&1
-rc=$?; grep -h '^{' $O/vparity.log | cut -c1-200
-if [ $rc -gt 1 ]; then echo "vparity rc=$rc"; tail -20 $O/vparity.log; exit 10; fi
-# staged kernel: fewer medium frames per step (1 round of 4), and a 4-load medium span
-step c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 --lib $L --lib $V/m1.so --lib $V/m1u4.so --lib $V/u4.so "defer=1"
-step imix 300 python3 tools/tune_ab.py --workload c4_imix --reps 9 --lib $L --lib $V/m1.so --lib $V/m1u4.so --lib $V/u4.so "defer=1"
+# the GPU suite with the headline-record parity cases
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 echo done
