@@ -81,8 +81,9 @@ struct PinnedDescs {
 };
 thread_local PinnedDescs t_descs;
 
-constexpr uint32_t kScanThreads = 8;          // host threads a long ring scan may use
-constexpr uint32_t kScanBlocksPerThread = 4;  // below 2 x this many ready blocks the scan stays on the calling thread
+constexpr uint32_t kScanThreads = 8;              // host threads a long ring scan may use
+constexpr uint32_t kScanBlocksPerThread = 4;      // a thread walks at least this many blocks ...
+constexpr uint32_t kScanFramesPerThread = 16384;  // ... and this many frames (~0.2 ms of walk: more than a thread start)
 
 uint32_t* status_word(uint8_t* ring, uint64_t base) {
     return reinterpret_cast<uint32_t*>(ring + base + offsetof(tpacket_block_desc, hdr.bh1.block_status));
@@ -138,7 +139,7 @@ int dk_ring_scan_tpacket3(const void* ring, uint64_t ring_bytes, uint32_t block_
     }
     const uint32_t nb = k;
     // Pass 2: each block's header chain into its slots. The chains are independent, so a long scan walks blocks on
-    // several threads (the walk is one cache miss per frame; ~14 ns a frame on one core of the GPU box).
+    // several threads (the walk is one cache miss per frame: ~14 ns a frame on one core of the GPU box).
     std::vector<int> brc(nb, 0);
     auto walk = [&](uint32_t j0, uint32_t j1) {
         for (uint32_t j = j0; j < j1; j++) {
@@ -148,7 +149,7 @@ int dk_ring_scan_tpacket3(const void* ring, uint64_t ring_bytes, uint32_t block_
         }
     };
     const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const uint32_t nt = std::min({kScanThreads, hw, nb / kScanBlocksPerThread});
+    const uint32_t nt = std::min({kScanThreads, hw, nb / kScanBlocksPerThread, n / kScanFramesPerThread});
     bool parallel = false;
     if (nt > 1) {
         std::vector<std::thread> th;

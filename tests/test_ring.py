@@ -114,10 +114,11 @@ def test_malformed_later_block_returns_good_prefix_then_is_consumed():
 
 
 def test_long_scan_on_several_threads():
-    """A scan over many ready blocks walks them on several host threads (ring_host.cpp: 8 or more blocks); the result is
+    """A scan over many ready blocks walks them on several host threads (ring_host.cpp: >= 8 blocks and >= 32,768
+    frames); the result is
     the sequential walk's: every frame in ring order, a capacity cut at a block boundary, a malformed block in a later
     thread's range returning the good prefix, and that block reported (EBADMSG, consumed) when a scan starts at it."""
-    blob, off, lens = frames(12000, seed=9)
+    blob, off, lens = frames(40000, seed=9)
     bs = 1 << 16
     ring, used, eoff, elen = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
     assert used >= 40

@@ -16,6 +16,5 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# the GPU suite with the headline-record parity cases
-step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 echo done
