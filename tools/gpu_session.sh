@@ -16,5 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 echo done
