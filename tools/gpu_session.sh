@@ -16,7 +16,14 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+L=demikernel_amd/libdk_rx.so
+V=build/variants
+echo "== vparity"
+timeout -k 10 300 python3 tools/variant_parity.py --lib $V/aos.so --lib $V/stg8.so > $O/vparity.log 2>&1
+rc=$?; grep -h '^{' $O/vparity.log | cut -c1-200
+if [ $rc -gt 1 ]; then echo "vparity rc=$rc"; tail -20 $O/vparity.log; exit 10; fi
+# LDS Active table as 16-byte slots (one ds_read_b128 per lookup); staged kernel with 8 staged chunks
+step imix 300 python3 tools/tune_ab.py --workload c4_imix --reps 9 --lib $L --lib $V/aos.so --lib $V/stg8.so "defer=1"
+step c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --lib $L --lib $V/aos.so "defer=1"
+step c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --lib $L --lib $V/aos.so "defer=1"
 echo done
