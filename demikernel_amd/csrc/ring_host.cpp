@@ -150,15 +150,17 @@ int dk_ring_scan_tpacket3(const void* ring, uint64_t ring_bytes, uint32_t block_
     };
     const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
     const uint32_t nt = std::min({kScanThreads, hw, nb / kScanBlocksPerThread, n / kScanFramesPerThread});
-    bool parallel = false;
     if (nt > 1) {
+        // thread t walks blocks [nb t / nt, nb (t + 1) / nt); the calling thread takes range 0 and, when a thread
+        // could not be started, that range and every later one
         std::vector<std::thread> th;
+        uint32_t started = 1;
         try {
-            for (uint32_t t = 1; t < nt; t++) th.emplace_back(walk, nb * t / nt, nb * (t + 1) / nt);
-            parallel = true;
-        } catch (...) {  // no threads: the calling thread walks everything
+            for (; started < nt; started++) th.emplace_back(walk, nb * started / nt, nb * (started + 1) / nt);
+        } catch (...) {
         }
-        walk(0, parallel ? nb / nt : nb);
+        walk(0, nb / nt);
+        if (started < nt) walk(nb * started / nt, nb);
         for (std::thread& t : th) t.join();
     } else {
         walk(0, nb);

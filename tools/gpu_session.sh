@@ -16,14 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-L=demikernel_amd/libdk_rx.so
-V=build/variants
-echo "== vparity"
-timeout -k 10 300 python3 tools/variant_parity.py --lib $V/aos.so --lib $V/stg8.so > $O/vparity.log 2>&1
-rc=$?; grep -h '^{' $O/vparity.log | cut -c1-200
-if [ $rc -gt 1 ]; then echo "vparity rc=$rc"; tail -20 $O/vparity.log; exit 10; fi
-# LDS Active table as 16-byte slots (one ds_read_b128 per lookup); staged kernel with 8 staged chunks
-step imix 300 python3 tools/tune_ab.py --workload c4_imix --reps 9 --lib $L --lib $V/aos.so --lib $V/stg8.so "defer=1"
-step c2 300 python3 tools/tune_ab.py --workload c2_tcp1500 --reps 7 --lib $L --lib $V/aos.so "defer=1"
-step c5 300 python3 tools/tune_ab.py --workload c5_tcp1500_10k --reps 5 --lib $L --lib $V/aos.so "defer=1"
+# grid shape re-check after this round's changes (deferred counters, priorities)
+step imix 300 python3 tools/tune_ab.py --workload c4_imix --reps 7 "defer=1" "defer=1,grid_per_cu=2" "defer=1,sched=1"
+step c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 "defer=1" "defer=1,grid_per_cu=4"
+step c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 "defer=1" "defer=1,grid_per_cu=1" "defer=1,sched=1"
 echo done
