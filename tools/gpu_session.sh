@@ -16,8 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# grid shape re-check after this round's changes (deferred counters, priorities)
-step imix 300 python3 tools/tune_ab.py --workload c4_imix --reps 7 "defer=1" "defer=1,grid_per_cu=2" "defer=1,sched=1"
-step c3 300 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 "defer=1" "defer=1,grid_per_cu=4"
-step c1 300 python3 tools/tune_ab.py --workload c1_tcp1078 --rotate 3 --reps 9 "defer=1" "defer=1,grid_per_cu=1" "defer=1,sched=1"
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 echo done
