@@ -123,7 +123,8 @@ struct RxParams {
     uint32_t row_words;      // words per workgroup row of flow_scratch: flow_words + (verdict_counts ? kVerdictWords : 0)
     uint32_t row_stride;     // row_words rounded up to kRowAlignWords
     uint32_t* flow_scratch;  // [grid][row_stride]: the packed-u16 flow histogram (kFlowLds), then the u32 verdict
-                             // histogram; nullptr when row_words == 0. dk_flow_reduce_kernel adds the rows up.
+                             // histogram; nullptr when row_words == 0. dk_flow_reduce_kernel (or, deferred, the
+                             // stream's next launch) adds the rows up.
     uint64_t* defer;         // small-frame kernel: [ceil(n / 64)] masks of the frames each 64-frame chunk left to the
                              // general path after its main loop
     unsigned long long* path_stats;  // nullable: [4] frames per path (dk_diag.h)

@@ -1148,7 +1148,9 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
 
 // Workgroup exit: the LDS histograms (flow words in kFlowLds mode, then the verdict words) become this workgroup's row
 // of the launch scratch (plain stores), and dk_flow_reduce_kernel, a second launch on the same stream, adds the rows to
-// the caller's u64 counters. Round 3 measured every in-launch form against it on two boxes: a two-level
+// the caller's u64 counters — or, with DK_RX_BATCH_DEFER_COUNTS, the stream's next receive launch does inside its own
+// kernel (combine_pending). Round 3 measured every in-launch combine of a launch's OWN rows against the second launch on
+// two boxes: a two-level
 // tree of arrival tickets (write-through rows, drained, the last arriver of each group summing its group) was slower on
 // every workload (C2 +0.8 %, IMIX +2.3 %, C5 +3.3 %, C3 +23 %) and on small batches too, and replica rows filled by
 // memory-side atomics tied with the second launch; the kernels hold no inter-workgroup hand-off at all.

@@ -883,7 +883,7 @@ def test_counter_rows_accumulate(torch_cuda, monkeypatch, family):
 @pytest.mark.parametrize("family", ["staged", "split", "small", "unstaged"])
 def test_deferred_counts(torch_cuda, monkeypatch, family):
     """DK_RX_BATCH_DEFER_COUNTS: a launch leaves its counter rows pending and the next launch on the stream adds them to
-    the deferred launch's counters inside its own kernel (ticketed blocks, RowCombine), or dk_rx_counts_flush does.
+    the deferred launch's counters inside its own kernel (statically assigned row blocks, RowCombine), or dk_rx_counts_flush does.
     Per kernel family and grid (7 workgroups, the default, 1,500; > 32,768 flows: verdict rows only): two counter sets
     alternated with deferral, a launch without counters completing the pending rows, grid growth with rows pending
     (flush before the scratch grows), a flush, 12 streams with deferred rows (slot takeovers flush them), and a pending
