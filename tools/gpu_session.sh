@@ -18,5 +18,7 @@ export TMPDIR=/tmp
 
 step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+# ring scan: walker threads 8 / 12, prefetch 4 / 8 frames ahead
+V=build/variants
+step ring 400 python3 tools/ring_ab.py --lib $V/t8a4.so --lib $V/t12a4.so --lib $V/t8a8.so --lib $V/t12a8.so --reps 5
 echo done
