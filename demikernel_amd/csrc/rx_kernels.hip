@@ -1240,6 +1240,16 @@ __device__ __forceinline__ void combine_pending_tail(const RxParams& P, uint32_t
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
+#ifdef DK_DIAG_STAMPS  // diagnostic build: per-wave s_memtime stamps of dk_rx_kernel (tools/stamps_staged.py)
+#define DK_STAMPW(slot, t)                                                                                          \
+    do {                                                                                                            \
+        const uint64_t t_ = (t);                                                                                    \
+        if (P.path_stats && lane_id() == 0)                                                                         \
+            P.path_stats[4 + 32 * (blockIdx.x * kWaves + (threadIdx.x >> 6)) + (slot)] = t_;                        \
+    } while (0)
+#else
+#define DK_STAMPW(slot, t) do {} while (0)
+#endif
 template <bool kShift, bool kStage>
 __global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED)
 void dk_rx_kernel(RxParams P) {
@@ -1250,12 +1260,15 @@ void dk_rx_kernel(RxParams P) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6;
+    DK_STAMPW(12, __builtin_amdgcn_s_memrealtime());
+    DK_STAMPW(0, __builtin_amdgcn_s_memtime());
     const bool lds_flows = P.flow_mode == kFlowLds;
     for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     lt_load(P, tid, kBlock);
     __syncthreads();
+    DK_STAMPW(1, __builtin_amdgcn_s_memtime());
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     StgRec<false> stg[kStage ? kStageK : 1];
@@ -1283,9 +1296,12 @@ void dk_rx_kernel(RxParams P) {
         Rec rec;
         rec.meta = kNoRec;
         Chunk C;
+        if (k < 3) DK_STAMPW(2 + 3 * k, __builtin_amdgcn_s_memtime());
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
+        if (k < 3) DK_STAMPW(3 + 3 * k, __builtin_amdgcn_s_memtime());
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
+        if (k < 3) DK_STAMPW(4 + 3 * k, __builtin_amdgcn_s_memtime());
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
         // at the top of the next chunk, after a staged flush, their wait also waited for every store's write ack.
 #ifndef DK_EARLY_DESC
@@ -1302,10 +1318,14 @@ void dk_rx_kernel(RxParams P) {
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
     }
 
+    DK_STAMPW(11, __builtin_amdgcn_s_memtime());
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     combine_pending_tail(P, lane, kWaves);  // a previous launch's deferred counter rows, in this wave's tail
+    DK_STAMPW(14, __builtin_amdgcn_s_memtime());
     __syncthreads();
     flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
+    DK_STAMPW(15, __builtin_amdgcn_s_memtime());
+    DK_STAMPW(13, __builtin_amdgcn_s_memrealtime());
 }
 
 // Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
