@@ -16,14 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-L=demikernel_amd/libdk_rx.so
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 V=build/variants
-echo "== vparity"
-timeout -k 10 300 python3 tools/variant_parity.py --lib $V/dyn.so --frames 1048576 > $O/vparity.log 2>&1
-rc=$?; grep -h '^{' $O/vparity.log | cut -c1-200
-if [ $rc -gt 1 ]; then echo "vparity rc=$rc"; tail -20 $O/vparity.log; exit 10; fi
-# staged kernel: dynamic tail (the last rounds grabbed from 8 counters) vs static round-robin
-step imix 300 python3 tools/tune_ab.py --workload c4_imix --reps 9 --lib $L --lib $V/dyn.so --lib $V/nodyn.so "defer=1"
-step imix_r2 300 python3 tools/tune_ab.py --workload c4_imix --rotate 2 --reps 7 --lib $L --lib $V/dyn.so "defer=1"
-step c1x8 300 python3 tools/tune_ab.py --workload c1_tcp1078 --frames 1048576 --rotate 2 --reps 5 --lib $L --lib $V/dyn.so "defer=1"
+step st_c1 300 python3 tools/stamps_staged.py $V/stamps.so --workload c1_tcp1078 --rotate 3
 echo done
