@@ -141,6 +141,85 @@ def test_long_scan_on_several_threads():
     assert nb == used - bad - 1 and np.array_equal(o, eoff[eoff // bs > bad])
 
 
+def reference_scan(ring, bs, first, nblocks, cap):
+    """The walk's contract restated block by block in Python (dk_ring.h: stop at a kernel-owned block; a block that
+    overflows cap ends the scan before it, ENOSPC when it is the first; the first malformed block ends the scan after
+    the good ones, EBADMSG and consumed when it is the first; stop once cap is exactly full)."""
+    u32 = lambda a: int(np.frombuffer(ring[a:a + 4].tobytes(), np.uint32)[0])  # noqa: E731
+    u16 = lambda a: int(np.frombuffer(ring[a:a + 2].tobytes(), np.uint16)[0])  # noqa: E731
+    nring = ring.nbytes // bs
+    offs, lens, k = [], [], 0
+    while k < min(nblocks, nring):
+        base = ((first + k) % nring) * bs
+        if not (u32(base + 8) & RG.TP_STATUS_USER):
+            break
+        npk, p = u32(base + 12), u32(base + 16)
+        if npk and len(offs) + npk > cap:
+            return (ENOSPC, 0, 0, [], []) if k == 0 else (0, len(offs), k, offs, lens)
+        bo, bl, bad = [], [], False
+        for j in range(npk):
+            if p + RG.PKT_HDR_BYTES > bs:
+                bad = True
+                break
+            f, sn = p + u16(base + p + 24), u32(base + p + 12)
+            if sn > 0xFFFF or f + sn > bs:
+                bad = True
+                break
+            bo.append(base + f)
+            bl.append(sn)
+            if j + 1 < npk:
+                nxt = u32(base + p)
+                if nxt == 0:
+                    bad = True
+                    break
+                p += nxt
+        if bad:
+            return (EBADMSG, 0, 1, [], []) if k == 0 else (0, len(offs), k, offs, lens)
+        offs += bo
+        lens += bl
+        k += 1
+        if len(offs) == cap:
+            break
+    return 0, len(offs), k, offs, lens
+
+
+def test_scan_matches_reference_walk_under_corruption():
+    """The two-pass, multi-thread walk (ring_host.cpp) against reference_scan on rings of 48+ blocks with corrupted
+    headers, kernel-owned blocks, wrapped starts and caps that cut anywhere: return code, frames, blocks consumed and
+    every descriptor identical."""
+    blob, off, lens = frames(40000, seed=21)
+    bs = 1 << 16
+    ring0, used, _, _ = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+    rng = np.random.default_rng(22)
+    for case in range(12):
+        ring = ring0.copy()
+        for _ in range(int(rng.integers(0, 4))):
+            blk = int(rng.integers(0, used))
+            what = int(rng.integers(0, 4))
+            b = blk * bs
+            if what == 0:  # tp_next_offset of the block's first packet zeroed
+                ring[b + RG.BLOCK_DESC_BYTES:b + RG.BLOCK_DESC_BYTES + 4] = 0
+            elif what == 1:  # snaplen past the block
+                ring[b + RG.BLOCK_DESC_BYTES + 12:b + RG.BLOCK_DESC_BYTES + 16] = np.frombuffer(
+                    np.uint32(bs).tobytes(), np.uint8)
+            elif what == 2:  # handed back to the kernel
+                ring[b + 8:b + 12] = 0
+            else:  # num_pkts inflated: the chain runs off the block
+                ring[b + 12:b + 16] = np.frombuffer(np.uint32(100000).tobytes(), np.uint8)
+        first = int(rng.integers(0, used)) if case % 3 == 0 else 0
+        cap = int(rng.choice([len(off), int(rng.integers(1, len(off)))]))
+        exp = reference_scan(ring, bs, first, used, cap)
+        r = RG.TpacketRing(ring, bs, register=False)
+        try:
+            o, ln, nb = r.scan(first, used, cap)
+            got = (0, len(o), nb)
+        except Fail as e:
+            o, ln, got = [], [], (e.errno, 0, e.blocks)
+        assert got == exp[:3], (case, got, exp[:3])
+        if got[0] == 0:
+            assert np.array_equal(o, np.array(exp[3], np.uint32)) and np.array_equal(ln, np.array(exp[4], np.uint16))
+
+
 def load_live_fixture():
     """The ring a live AF_PACKET socket on `lo` filled (tests/golden/make_ring_fixture.py), in page-aligned memory."""
     import os
