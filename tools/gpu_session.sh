@@ -16,8 +16,6 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-V=build/variants
-step st_c1 300 python3 tools/stamps_staged.py $V/stamps.so --workload c1_tcp1078 --rotate 3
+# rocprofv3 evidence at the final build: bench kernel stats, FETCH/WRITE traffic per workload, C1/C3/TX/TCP stats
+step profile 1000 bash tools/profile_bench.sh $TAG
 echo done
