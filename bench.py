@@ -636,6 +636,8 @@ def main():
                    "global_frames": total_frames, "parallelism": f"packet-shard x{world}",
                    "collective": collective},
         "mpkt_s": round(total_frames * args.steps / wall / 1e6, 2),
+        # the content hash compiled into the loaded libdk_rx.so (__graft_entry__.tree_build_id of its sources)
+        "build_id": eng.build_id(),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms_avg": round(kern_avg * 1e3, 4),
