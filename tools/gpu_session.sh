@@ -16,6 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# rocprofv3 evidence at the final build: bench kernel stats, FETCH/WRITE traffic per workload, C1/C3/TX/TCP stats
-step profile 1000 bash tools/profile_bench.sh $TAG
+# round-end rehearsal at HEAD: the GPU tests, smoke() and the default bench line (as the driver runs them)
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
 echo done
