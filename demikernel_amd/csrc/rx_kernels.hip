@@ -253,7 +253,11 @@ __device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const Rx
 // each check is one compare + select, applied last-to-first so the first failing check in Appendix A order wins. The
 // early-return form made the compiler re-materialise every zeroed Lane field on each of its ~25 exits, i.e. ~12
 // v_mov per check per wave on the path every valid frame takes. I3/I4 (hs < 20, iplen < hs) cannot fire here.
-__device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const RxParams& P, Lane& L) {
+// kWaveCheck (small-frame kernel, DK_SMALL_WCHK): when no live lane of the wave fails any check, the verdict is the
+// protocol's pending value and the select chain is skipped (one wave-uniform branch).
+template <bool kWaveCheck = false>
+__device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const RxParams& P, Lane& L,
+                                           bool live = true) {
     const uint32_t et = a.be16(12);
     const uint32_t iplen = len - 14;
     const uint32_t b14 = a.b8(14);
@@ -269,29 +273,46 @@ __device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const 
     const uint32_t doff = (b12 >> 4) * 4;
     const bool tcp = proto == 6u;
     const uint32_t stored = tcp ? a.be16(50) : a.be16(40);
-
-    uint32_t v4 = tcp ? (seg < 20 ? (uint32_t)DK_V_TCP_SHORT                                  // T1
-                         : seg < doff ? (uint32_t)DK_V_TCP_DOFF_TRUNC                         // T2
-                         : doff < 20 ? (uint32_t)DK_V_TCP_DOFF_SMALL : kPendTcp)              // T3
-                      : (seg < 8 ? (uint32_t)DK_V_UDP_SHORT                                   // U1
-                         : a.be16(38) != seg ? (uint32_t)DK_V_UDP_LEN : kPendUdp);            // U2
     const bool icmp = proto == 1u;
-    uint32_t v = icmp ? (seg < 8 ? (uint32_t)DK_V_ICMP_SHORT : kPendIcmp) : v4;
-    v = (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) ? (uint32_t)DK_V_IP_SRC : v;   // F2
-    v = (dst != P.local_ip && dst != 0xFFFFFFFFu) ? (uint32_t)DK_V_IP_DST : v;                   // F1
-    v = csum_from_residue(be_residue(hsum)) != ipcs ? (uint32_t)DK_V_IP_CSUM : v;                // I13
-    v = ipcs == 0xFFFFu ? (uint32_t)DK_V_IP_CSUM_FFFF : v;                                       // I12
-    v = (proto != 1u && proto != 6u && proto != 17u) ? (uint32_t)DK_V_IP_PROTO : v;              // I11
-    v = a.b8(22) == 0 ? (uint32_t)DK_V_IP_TTL : v;                                               // I10
-    v = (frag & 0x1FFFu) ? (uint32_t)DK_V_IP_FRAGOFF : v;                                        // I9
-    v = (frag & 0x2000u) ? (uint32_t)DK_V_IP_MF : v;                                             // I8
-    v = (frag & 0x8000u) ? (uint32_t)DK_V_IP_EVIL : v;                                           // I7
-    v = tot > iplen ? (uint32_t)DK_V_IP_TOTLEN_BIG : v;                                          // I6
-    v = tot < 20 ? (uint32_t)DK_V_IP_TOTLEN_SMALL : v;                                           // I5
-    v = (b14 >> 4) != 4 ? (uint32_t)DK_V_IP_VERSION : v;                                         // I2
-    v = et == 0x86ddu ? (uint32_t)DK_V_IPV6 : v;
-    v = et == 0x0806u ? (uint32_t)DK_V_ARP : v;
-    v = (et != 0x0806u && et != 0x0800u && et != 0x86ddu) ? (uint32_t)DK_V_ETH_TYPE : v;        // E2
+
+    uint32_t v;
+    bool chain = true;
+    if (kWaveCheck) {
+        // every check below passes (proto is then 1, 6 or 17; frag & 0xBFFF covers I7, I8, I9)
+        const bool ok = et == 0x0800u && (b14 >> 4) == 4 && tot >= 20 && tot <= iplen && !(frag & 0xBFFFu) &&
+                        a.b8(22) != 0 && ipcs != 0xFFFFu && csum_from_residue(be_residue(hsum)) == ipcs &&
+                        (dst == P.local_ip || dst == 0xFFFFFFFFu) &&
+                        !(src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) &&
+                        (tcp ? (seg >= 20 && seg >= doff && doff >= 20)
+                             : icmp ? seg >= 8 : (proto == 17u && seg >= 8 && a.be16(38) == seg));
+        if (!__ballot(live && !ok)) {
+            v = tcp ? kPendTcp : icmp ? kPendIcmp : kPendUdp;
+            chain = false;
+        }
+    }
+    if (chain) {
+        const uint32_t v4 = tcp ? (seg < 20 ? (uint32_t)DK_V_TCP_SHORT                              // T1
+                                   : seg < doff ? (uint32_t)DK_V_TCP_DOFF_TRUNC                     // T2
+                                   : doff < 20 ? (uint32_t)DK_V_TCP_DOFF_SMALL : kPendTcp)          // T3
+                                : (seg < 8 ? (uint32_t)DK_V_UDP_SHORT                               // U1
+                                   : a.be16(38) != seg ? (uint32_t)DK_V_UDP_LEN : kPendUdp);        // U2
+        v = icmp ? (seg < 8 ? (uint32_t)DK_V_ICMP_SHORT : kPendIcmp) : v4;
+        v = (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) ? (uint32_t)DK_V_IP_SRC : v;   // F2
+        v = (dst != P.local_ip && dst != 0xFFFFFFFFu) ? (uint32_t)DK_V_IP_DST : v;                   // F1
+        v = csum_from_residue(be_residue(hsum)) != ipcs ? (uint32_t)DK_V_IP_CSUM : v;                // I13
+        v = ipcs == 0xFFFFu ? (uint32_t)DK_V_IP_CSUM_FFFF : v;                                       // I12
+        v = (proto != 1u && proto != 6u && proto != 17u) ? (uint32_t)DK_V_IP_PROTO : v;              // I11
+        v = a.b8(22) == 0 ? (uint32_t)DK_V_IP_TTL : v;                                               // I10
+        v = (frag & 0x1FFFu) ? (uint32_t)DK_V_IP_FRAGOFF : v;                                        // I9
+        v = (frag & 0x2000u) ? (uint32_t)DK_V_IP_MF : v;                                             // I8
+        v = (frag & 0x8000u) ? (uint32_t)DK_V_IP_EVIL : v;                                           // I7
+        v = tot > iplen ? (uint32_t)DK_V_IP_TOTLEN_BIG : v;                                          // I6
+        v = tot < 20 ? (uint32_t)DK_V_IP_TOTLEN_SMALL : v;                                           // I5
+        v = (b14 >> 4) != 4 ? (uint32_t)DK_V_IP_VERSION : v;                                         // I2
+        v = et == 0x86ddu ? (uint32_t)DK_V_IPV6 : v;
+        v = et == 0x0806u ? (uint32_t)DK_V_ARP : v;
+        v = (et != 0x0806u && et != 0x0800u && et != 0x86ddu) ? (uint32_t)DK_V_ETH_TYPE : v;        // E2
+    }
 
     const bool pend = v == kPendTcp || v == kPendUdp || v == kPendIcmp;
     L.v = v;
@@ -1505,7 +1526,10 @@ template <bool kOpt>
 __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool live, uint32_t lane, const RegAcc& R,
                                            uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
     Lane L;
-    parse_fast(R, len, P, L);
+#ifndef DK_SMALL_WCHK
+#define DK_SMALL_WCHK 0
+#endif
+    parse_fast<DK_SMALL_WCHK != 0>(R, len, P, L, live);
     if (!live) {
         L.v = kNone;
         L.need = 0;
@@ -1641,7 +1665,16 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
+    // Where the waves of the workgroup meet after zeroing the counters: 0 here; 1 just before a wave's first
+    // count_chunk (its first chunk's window, parse and stores overlap the other waves' arrival); 2 between its first
+    // window's DMA issue and the window read. Every wave passes exactly one init barrier (a wave without chunks after
+    // the loop).
+#ifndef DK_SMALL_BAR
+#define DK_SMALL_BAR 0
+#endif
+#if DK_SMALL_BAR == 0
     __syncthreads();
+#endif
 #ifdef DK_DIAG_STAMPS
     DK_STAMP_T(11, __builtin_amdgcn_s_memtime());
 #endif
@@ -1681,6 +1714,9 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     bool deferred = false;  // wave-uniform: a chunk left frames to the general pass
     // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
     uint64_t had = DK_SMALL_LATE ? 0ull : ~0ull;
+#if DK_SMALL_BAR != 0
+    const uint32_t entered = __builtin_amdgcn_readfirstlane(have ? 1u : 0u);
+#endif
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1697,7 +1733,13 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         Rec rec;
         rec.meta = kNoRec;
         if (k == 0) DK_STAMP(1);
-        small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
+        {
+            const WinPlan pl = small_window_issue(F, B, off, len, live, lane, W);
+#if DK_SMALL_BAR == 2
+            if (k == 0) __syncthreads();
+#endif
+            small_window_read(pl, F, B, off, W, C.R);
+        }
 #if !DK_SMALL_LATE
         if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead (after the window wait)
             off2 = P.off[c2 + r.lane_off];
@@ -1718,6 +1760,9 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         deferred = deferred || dm != 0;
         small_fast<kOpt>(P, i, take, lane, C.R, len, v, fid);
         DK_STAMP(3 + 3 * k);
+#if DK_SMALL_BAR == 1
+        if (k == 0) __syncthreads();
+#endif
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
 #if DK_SMALL_LATE
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
@@ -1730,6 +1775,9 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,
                                                        k < 3 ? 16 + 5 * k : ~0u);
         DK_STAMP(3 + 3 * k);
+#if DK_SMALL_BAR == 1
+        if (k == 0) __syncthreads();
+#endif
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
 #endif
         DK_STAMP(4 + 3 * k);
@@ -1746,6 +1794,9 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
+#if DK_SMALL_BAR != 0
+    if (!entered) __syncthreads();  // a wave without chunks meets the others here
+#endif
 #if DK_SMALL_DEFER
     if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
