@@ -1284,12 +1284,20 @@ void dk_rx_kernel(RxParams P) {
     DK_STAMPW(12, __builtin_amdgcn_s_memrealtime());
     DK_STAMPW(0, __builtin_amdgcn_s_memtime());
     const bool lds_flows = P.flow_mode == kFlowLds;
+    // Where the workgroup's waves meet after zeroing the counters and copying the Active table into LDS: 0 here; 1
+    // between a wave's first frame stream and its first phase C (the first chunk's descriptors and frames load while
+    // the table copy and the other waves' arrival complete). Every wave passes exactly one init barrier.
+#ifndef DK_STG_BAR
+#define DK_STG_BAR 0
+#endif
+#if DK_STG_BAR == 0
     for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     lt_load(P, tid, kBlock);
     __syncthreads();
     DK_STAMPW(1, __builtin_amdgcn_s_memtime());
+#endif
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     StgRec<false> stg[kStage ? kStageK : 1];
@@ -1301,6 +1309,13 @@ void dk_rx_kernel(RxParams P) {
         noff = P.off[c + r.lane_off];
         nlen = P.len[c + r.lane_off];
     }
+#if DK_STG_BAR != 0
+    for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
+    if (lds_flows)
+        for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
+    lt_load(P, tid, kBlock);
+    const uint32_t entered = __builtin_amdgcn_readfirstlane(have ? 1u : 0u);
+#endif
     WaveLds& W = s_wave[wv];
     uint32_t nchunks = 0;
     for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
@@ -1321,6 +1336,9 @@ void dk_rx_kernel(RxParams P) {
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
         if (k < 3) DK_STAMPW(3 + 3 * k, __builtin_amdgcn_s_memtime());
+#if DK_STG_BAR != 0
+        if (k == 0) __syncthreads();
+#endif
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (k < 3) DK_STAMPW(4 + 3 * k, __builtin_amdgcn_s_memtime());
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
@@ -1338,6 +1356,9 @@ void dk_rx_kernel(RxParams P) {
         }
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
     }
+#if DK_STG_BAR != 0
+    if (!entered) __syncthreads();  // a wave without chunks meets the others here
+#endif
 
     DK_STAMPW(11, __builtin_amdgcn_s_memtime());
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, nchunks - 1);
@@ -1957,6 +1978,13 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     const bool finisher = wv >= (uint32_t)kWaves;
     const uint32_t fin = finisher ? (wv - kWaves) / kWaves : 0u;  // which of the stream wave's finishers
     const bool lds_flows = P.flow_mode == kFlowLds;
+    // DK_SPLIT_BAR 1: the finish waves zero the counters and flags and copy the Active table alone, and a stream wave
+    // meets them at the init barrier only before publishing its first chunk (its first frame stream overlaps the init).
+    // Every wave passes exactly one init barrier.
+#ifndef DK_SPLIT_BAR
+#define DK_SPLIT_BAR 0
+#endif
+#if DK_SPLIT_BAR == 0
     for (uint32_t k = tid; k < DK_V_COUNT; k += S::kThreads) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += S::kThreads) s_flow[k] = 0;
@@ -1966,6 +1994,20 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     }
     lt_load(P, tid, S::kThreads);
     __syncthreads();
+#else
+    if (finisher) {
+        constexpr uint32_t kFt = S::kThreads - 64 * kWaves;  // finish-wave threads
+        const uint32_t ft = tid - 64 * kWaves;
+        for (uint32_t k = ft; k < DK_V_COUNT; k += kFt) s_vh[k] = 0;
+        if (lds_flows)
+            for (uint32_t k = ft; k < P.flow_words; k += kFt) s_flow[k] = 0;
+        if (ft < kWaves * kBufs) {
+            (&s_ready[0][0])[ft] = 0;
+            (&s_free[0][0])[ft] = 0;
+        }
+        lt_load(P, ft, kFt);
+    }
+#endif
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
     const Blob B(P.frames, P.frames_bytes);
@@ -1974,7 +2016,14 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     // descriptors one chunk ahead (round 4: loaded at the top of chunk p, a stream wave opened every chunk with a
     // dependent descriptor round trip before its first frame load; C5 -1.3 %).
     DescAhead D(P, r, finisher ? fin : 0u);
+#if DK_SPLIT_BAR != 0
+    if (!__builtin_amdgcn_readfirstlane(finisher ? 1u : 0u)) {  // (a scalar branch: each side holds a barrier)
+#else
     if (!finisher) {
+#endif
+#if DK_SPLIT_BAR != 0
+        const uint32_t entered = __builtin_amdgcn_readfirstlane(D.have ? 1u : 0u);
+#endif
         for (uint32_t p = 0; D.have; p++) {
             const uint32_t b = p % kBufs;
             WaveLds& W = s_buf[b][sw];
@@ -1993,12 +2042,21 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     W.hdr[lane][k] = make_uint4(Rs.w[4 * k], Rs.w[4 * k + 1], Rs.w[4 * k + 2], Rs.w[4 * k + 3]);
+#if DK_SPLIT_BAR != 0
+            if (p == 0) __syncthreads();  // the flags are zeroed
+#endif
             if (lane == 0) lds_publish(&s_ready[sw][b], p + 1);
         }
+#if DK_SPLIT_BAR != 0
+        if (!entered) __syncthreads();
+#endif
     } else {
         // a previous launch's deferred counter rows: the finish waves have nothing to do until their stream wave's
         // first chunk has landed
         combine_pending(P, lane, blockIdx.x * kWaves + sw, gridDim.x * kWaves);
+#if DK_SPLIT_BAR != 0
+        __syncthreads();
+#endif
         StgRec<kTcp> stg[kStg];
         uint32_t nstg = 0, klast = 0;
         for (uint32_t p = fin; D.have; p += (uint32_t)kFin) {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Bit-exact check of tuning-variant libraries (tools/variants.sh) against the oracle before their timings are trusted:
     python tools/variant_parity.py --lib build/variants/x.so [--lib ...]
-Per library: IMIX, 576-byte, 64-byte UDP and 1078-byte TCP batches with a 2 % corrupted tail, frames at 64-byte slots
+Per library: IMIX, 576-byte, 64-byte UDP, 1078-byte and 1500-byte TCP batches with a 2 % corrupted tail, frames at 64-byte slots
 (aligned) and shifted to 2 mod 16; every result array and both counters against OraclePeer. One JSON line per case."""
 import argparse
 import json
@@ -26,7 +26,7 @@ def main():
     from oracle.oracle import OraclePeer
 
     bad_total = 0
-    cases = [("imix", "imix", "tcp"), ("576", 562, "tcp"), ("udp64", 50, "udp"), ("c1_1078", 1064, "tcp")]
+    cases = [("imix", "imix", "tcp"), ("576", 562, "tcp"), ("udp64", 50, "udp"), ("c1_1078", 1064, "tcp"), ("c2_1486", 1486, "tcp")]
     for lp in args.lib:
         eng = RxEngine(Config(synth.BOB_IPV4), lib_path=os.path.abspath(lp))
         for name, ip, kind in cases:
