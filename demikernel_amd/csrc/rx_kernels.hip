@@ -253,11 +253,7 @@ __device__ __forceinline__ void parse_headers(const A& a, uint32_t len, const Rx
 // each check is one compare + select, applied last-to-first so the first failing check in Appendix A order wins. The
 // early-return form made the compiler re-materialise every zeroed Lane field on each of its ~25 exits, i.e. ~12
 // v_mov per check per wave on the path every valid frame takes. I3/I4 (hs < 20, iplen < hs) cannot fire here.
-// kWaveCheck (small-frame kernel, DK_SMALL_WCHK): when no live lane of the wave fails any check, the verdict is the
-// protocol's pending value and the select chain is skipped (one wave-uniform branch).
-template <bool kWaveCheck = false>
-__device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const RxParams& P, Lane& L,
-                                           bool live = true) {
+__device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const RxParams& P, Lane& L) {
     const uint32_t et = a.be16(12);
     const uint32_t iplen = len - 14;
     const uint32_t b14 = a.b8(14);
@@ -273,46 +269,29 @@ __device__ __forceinline__ void parse_fast(const RegAcc& a, uint32_t len, const 
     const uint32_t doff = (b12 >> 4) * 4;
     const bool tcp = proto == 6u;
     const uint32_t stored = tcp ? a.be16(50) : a.be16(40);
-    const bool icmp = proto == 1u;
 
-    uint32_t v;
-    bool chain = true;
-    if (kWaveCheck) {
-        // every check below passes (proto is then 1, 6 or 17; frag & 0xBFFF covers I7, I8, I9)
-        const bool ok = et == 0x0800u && (b14 >> 4) == 4 && tot >= 20 && tot <= iplen && !(frag & 0xBFFFu) &&
-                        a.b8(22) != 0 && ipcs != 0xFFFFu && csum_from_residue(be_residue(hsum)) == ipcs &&
-                        (dst == P.local_ip || dst == 0xFFFFFFFFu) &&
-                        !(src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) &&
-                        (tcp ? (seg >= 20 && seg >= doff && doff >= 20)
-                             : icmp ? seg >= 8 : (proto == 17u && seg >= 8 && a.be16(38) == seg));
-        if (!__ballot(live && !ok)) {
-            v = tcp ? kPendTcp : icmp ? kPendIcmp : kPendUdp;
-            chain = false;
-        }
-    }
-    if (chain) {
-        const uint32_t v4 = tcp ? (seg < 20 ? (uint32_t)DK_V_TCP_SHORT                              // T1
-                                   : seg < doff ? (uint32_t)DK_V_TCP_DOFF_TRUNC                     // T2
-                                   : doff < 20 ? (uint32_t)DK_V_TCP_DOFF_SMALL : kPendTcp)          // T3
-                                : (seg < 8 ? (uint32_t)DK_V_UDP_SHORT                               // U1
-                                   : a.be16(38) != seg ? (uint32_t)DK_V_UDP_LEN : kPendUdp);        // U2
-        v = icmp ? (seg < 8 ? (uint32_t)DK_V_ICMP_SHORT : kPendIcmp) : v4;
-        v = (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) ? (uint32_t)DK_V_IP_SRC : v;   // F2
-        v = (dst != P.local_ip && dst != 0xFFFFFFFFu) ? (uint32_t)DK_V_IP_DST : v;                   // F1
-        v = csum_from_residue(be_residue(hsum)) != ipcs ? (uint32_t)DK_V_IP_CSUM : v;                // I13
-        v = ipcs == 0xFFFFu ? (uint32_t)DK_V_IP_CSUM_FFFF : v;                                       // I12
-        v = (proto != 1u && proto != 6u && proto != 17u) ? (uint32_t)DK_V_IP_PROTO : v;              // I11
-        v = a.b8(22) == 0 ? (uint32_t)DK_V_IP_TTL : v;                                               // I10
-        v = (frag & 0x1FFFu) ? (uint32_t)DK_V_IP_FRAGOFF : v;                                        // I9
-        v = (frag & 0x2000u) ? (uint32_t)DK_V_IP_MF : v;                                             // I8
-        v = (frag & 0x8000u) ? (uint32_t)DK_V_IP_EVIL : v;                                           // I7
-        v = tot > iplen ? (uint32_t)DK_V_IP_TOTLEN_BIG : v;                                          // I6
-        v = tot < 20 ? (uint32_t)DK_V_IP_TOTLEN_SMALL : v;                                           // I5
-        v = (b14 >> 4) != 4 ? (uint32_t)DK_V_IP_VERSION : v;                                         // I2
-        v = et == 0x86ddu ? (uint32_t)DK_V_IPV6 : v;
-        v = et == 0x0806u ? (uint32_t)DK_V_ARP : v;
-        v = (et != 0x0806u && et != 0x0800u && et != 0x86ddu) ? (uint32_t)DK_V_ETH_TYPE : v;        // E2
-    }
+    uint32_t v4 = tcp ? (seg < 20 ? (uint32_t)DK_V_TCP_SHORT                                  // T1
+                         : seg < doff ? (uint32_t)DK_V_TCP_DOFF_TRUNC                         // T2
+                         : doff < 20 ? (uint32_t)DK_V_TCP_DOFF_SMALL : kPendTcp)              // T3
+                      : (seg < 8 ? (uint32_t)DK_V_UDP_SHORT                                   // U1
+                         : a.be16(38) != seg ? (uint32_t)DK_V_UDP_LEN : kPendUdp);            // U2
+    const bool icmp = proto == 1u;
+    uint32_t v = icmp ? (seg < 8 ? (uint32_t)DK_V_ICMP_SHORT : kPendIcmp) : v4;
+    v = (src == 0xFFFFFFFFu || (src & 0xF0u) == 0xE0u || src == 0) ? (uint32_t)DK_V_IP_SRC : v;   // F2
+    v = (dst != P.local_ip && dst != 0xFFFFFFFFu) ? (uint32_t)DK_V_IP_DST : v;                   // F1
+    v = csum_from_residue(be_residue(hsum)) != ipcs ? (uint32_t)DK_V_IP_CSUM : v;                // I13
+    v = ipcs == 0xFFFFu ? (uint32_t)DK_V_IP_CSUM_FFFF : v;                                       // I12
+    v = (proto != 1u && proto != 6u && proto != 17u) ? (uint32_t)DK_V_IP_PROTO : v;              // I11
+    v = a.b8(22) == 0 ? (uint32_t)DK_V_IP_TTL : v;                                               // I10
+    v = (frag & 0x1FFFu) ? (uint32_t)DK_V_IP_FRAGOFF : v;                                        // I9
+    v = (frag & 0x2000u) ? (uint32_t)DK_V_IP_MF : v;                                             // I8
+    v = (frag & 0x8000u) ? (uint32_t)DK_V_IP_EVIL : v;                                           // I7
+    v = tot > iplen ? (uint32_t)DK_V_IP_TOTLEN_BIG : v;                                          // I6
+    v = tot < 20 ? (uint32_t)DK_V_IP_TOTLEN_SMALL : v;                                           // I5
+    v = (b14 >> 4) != 4 ? (uint32_t)DK_V_IP_VERSION : v;                                         // I2
+    v = et == 0x86ddu ? (uint32_t)DK_V_IPV6 : v;
+    v = et == 0x0806u ? (uint32_t)DK_V_ARP : v;
+    v = (et != 0x0806u && et != 0x0800u && et != 0x86ddu) ? (uint32_t)DK_V_ETH_TYPE : v;        // E2
 
     const bool pend = v == kPendTcp || v == kPendUdp || v == kPendIcmp;
     L.v = v;
@@ -1284,20 +1263,12 @@ void dk_rx_kernel(RxParams P) {
     DK_STAMPW(12, __builtin_amdgcn_s_memrealtime());
     DK_STAMPW(0, __builtin_amdgcn_s_memtime());
     const bool lds_flows = P.flow_mode == kFlowLds;
-    // Where the workgroup's waves meet after zeroing the counters and copying the Active table into LDS: 0 here; 1
-    // between a wave's first frame stream and its first phase C (the first chunk's descriptors and frames load while
-    // the table copy and the other waves' arrival complete). Every wave passes exactly one init barrier.
-#ifndef DK_STG_BAR
-#define DK_STG_BAR 0
-#endif
-#if DK_STG_BAR == 0
     for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     lt_load(P, tid, kBlock);
     __syncthreads();
     DK_STAMPW(1, __builtin_amdgcn_s_memtime());
-#endif
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     StgRec<false> stg[kStage ? kStageK : 1];
@@ -1309,13 +1280,6 @@ void dk_rx_kernel(RxParams P) {
         noff = P.off[c + r.lane_off];
         nlen = P.len[c + r.lane_off];
     }
-#if DK_STG_BAR != 0
-    for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
-    if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
-    lt_load(P, tid, kBlock);
-    const uint32_t entered = __builtin_amdgcn_readfirstlane(have ? 1u : 0u);
-#endif
     WaveLds& W = s_wave[wv];
     uint32_t nchunks = 0;
     for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
@@ -1336,9 +1300,6 @@ void dk_rx_kernel(RxParams P) {
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
         if (k < 3) DK_STAMPW(3 + 3 * k, __builtin_amdgcn_s_memtime());
-#if DK_STG_BAR != 0
-        if (k == 0) __syncthreads();
-#endif
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (k < 3) DK_STAMPW(4 + 3 * k, __builtin_amdgcn_s_memtime());
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
@@ -1356,9 +1317,6 @@ void dk_rx_kernel(RxParams P) {
         }
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
     }
-#if DK_STG_BAR != 0
-    if (!entered) __syncthreads();  // a wave without chunks meets the others here
-#endif
 
     DK_STAMPW(11, __builtin_amdgcn_s_memtime());
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, nchunks - 1);
@@ -1547,10 +1505,7 @@ template <bool kOpt>
 __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool live, uint32_t lane, const RegAcc& R,
                                            uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
     Lane L;
-#ifndef DK_SMALL_WCHK
-#define DK_SMALL_WCHK 0
-#endif
-    parse_fast<DK_SMALL_WCHK != 0>(R, len, P, L, live);
+    parse_fast(R, len, P, L);
     if (!live) {
         L.v = kNone;
         L.need = 0;
@@ -1686,16 +1641,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
-    // Where the waves of the workgroup meet after zeroing the counters: 0 here; 1 just before a wave's first
-    // count_chunk (its first chunk's window, parse and stores overlap the other waves' arrival); 2 between its first
-    // window's DMA issue and the window read. Every wave passes exactly one init barrier (a wave without chunks after
-    // the loop).
-#ifndef DK_SMALL_BAR
-#define DK_SMALL_BAR 0
-#endif
-#if DK_SMALL_BAR == 0
     __syncthreads();
-#endif
 #ifdef DK_DIAG_STAMPS
     DK_STAMP_T(11, __builtin_amdgcn_s_memtime());
 #endif
@@ -1735,9 +1681,6 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     bool deferred = false;  // wave-uniform: a chunk left frames to the general pass
     // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
     uint64_t had = DK_SMALL_LATE ? 0ull : ~0ull;
-#if DK_SMALL_BAR != 0
-    const uint32_t entered = __builtin_amdgcn_readfirstlane(have ? 1u : 0u);
-#endif
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
@@ -1754,13 +1697,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         Rec rec;
         rec.meta = kNoRec;
         if (k == 0) DK_STAMP(1);
-        {
-            const WinPlan pl = small_window_issue(F, B, off, len, live, lane, W);
-#if DK_SMALL_BAR == 2
-            if (k == 0) __syncthreads();
-#endif
-            small_window_read(pl, F, B, off, W, C.R);
-        }
+        small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
 #if !DK_SMALL_LATE
         if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead (after the window wait)
             off2 = P.off[c2 + r.lane_off];
@@ -1781,9 +1718,6 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         deferred = deferred || dm != 0;
         small_fast<kOpt>(P, i, take, lane, C.R, len, v, fid);
         DK_STAMP(3 + 3 * k);
-#if DK_SMALL_BAR == 1
-        if (k == 0) __syncthreads();
-#endif
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
 #if DK_SMALL_LATE
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
@@ -1796,9 +1730,6 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,
                                                        k < 3 ? 16 + 5 * k : ~0u);
         DK_STAMP(3 + 3 * k);
-#if DK_SMALL_BAR == 1
-        if (k == 0) __syncthreads();
-#endif
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
 #endif
         DK_STAMP(4 + 3 * k);
@@ -1815,9 +1746,6 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
-#if DK_SMALL_BAR != 0
-    if (!entered) __syncthreads();  // a wave without chunks meets the others here
-#endif
 #if DK_SMALL_DEFER
     if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
@@ -1978,13 +1906,6 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     const bool finisher = wv >= (uint32_t)kWaves;
     const uint32_t fin = finisher ? (wv - kWaves) / kWaves : 0u;  // which of the stream wave's finishers
     const bool lds_flows = P.flow_mode == kFlowLds;
-    // DK_SPLIT_BAR 1: the finish waves zero the counters and flags and copy the Active table alone, and a stream wave
-    // meets them at the init barrier only before publishing its first chunk (its first frame stream overlaps the init).
-    // Every wave passes exactly one init barrier.
-#ifndef DK_SPLIT_BAR
-#define DK_SPLIT_BAR 0
-#endif
-#if DK_SPLIT_BAR == 0
     for (uint32_t k = tid; k < DK_V_COUNT; k += S::kThreads) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += S::kThreads) s_flow[k] = 0;
@@ -1994,20 +1915,6 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     }
     lt_load(P, tid, S::kThreads);
     __syncthreads();
-#else
-    if (finisher) {
-        constexpr uint32_t kFt = S::kThreads - 64 * kWaves;  // finish-wave threads
-        const uint32_t ft = tid - 64 * kWaves;
-        for (uint32_t k = ft; k < DK_V_COUNT; k += kFt) s_vh[k] = 0;
-        if (lds_flows)
-            for (uint32_t k = ft; k < P.flow_words; k += kFt) s_flow[k] = 0;
-        if (ft < kWaves * kBufs) {
-            (&s_ready[0][0])[ft] = 0;
-            (&s_free[0][0])[ft] = 0;
-        }
-        lt_load(P, ft, kFt);
-    }
-#endif
 
     const WaveRange r = wave_range(0, P.n, sw, lane);  // sched 0 over the 4 stream waves of each workgroup
     const Blob B(P.frames, P.frames_bytes);
@@ -2016,14 +1923,7 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
     // descriptors one chunk ahead (round 4: loaded at the top of chunk p, a stream wave opened every chunk with a
     // dependent descriptor round trip before its first frame load; C5 -1.3 %).
     DescAhead D(P, r, finisher ? fin : 0u);
-#if DK_SPLIT_BAR != 0
-    if (!__builtin_amdgcn_readfirstlane(finisher ? 1u : 0u)) {  // (a scalar branch: each side holds a barrier)
-#else
     if (!finisher) {
-#endif
-#if DK_SPLIT_BAR != 0
-        const uint32_t entered = __builtin_amdgcn_readfirstlane(D.have ? 1u : 0u);
-#endif
         for (uint32_t p = 0; D.have; p++) {
             const uint32_t b = p % kBufs;
             WaveLds& W = s_buf[b][sw];
@@ -2042,21 +1942,12 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     W.hdr[lane][k] = make_uint4(Rs.w[4 * k], Rs.w[4 * k + 1], Rs.w[4 * k + 2], Rs.w[4 * k + 3]);
-#if DK_SPLIT_BAR != 0
-            if (p == 0) __syncthreads();  // the flags are zeroed
-#endif
             if (lane == 0) lds_publish(&s_ready[sw][b], p + 1);
         }
-#if DK_SPLIT_BAR != 0
-        if (!entered) __syncthreads();
-#endif
     } else {
         // a previous launch's deferred counter rows: the finish waves have nothing to do until their stream wave's
         // first chunk has landed
         combine_pending(P, lane, blockIdx.x * kWaves + sw, gridDim.x * kWaves);
-#if DK_SPLIT_BAR != 0
-        __syncthreads();
-#endif
         StgRec<kTcp> stg[kStg];
         uint32_t nstg = 0, klast = 0;
         for (uint32_t p = fin; D.have; p += (uint32_t)kFin) {
