@@ -415,9 +415,6 @@ __device__ __forceinline__ uint4 lt_lookup(const RxParams& P, uint32_t rip, uint
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
-// One frame per lane, 256 frames per workgroup tile: phases A, B, C and the result stores. Every lane of the
-// workgroup calls it (phase B is wave-cooperative). Returns the verdict and the flow id (DK_FLOW_NONE if none).
-// Per-wave LDS used by one tile. Strides of 5 and 3 uint4 keep the owner-lane ds_read_b128 conflict-free.
 // One quarter-wave's frame in a phase-B step.
 struct CoopSlot {
     uint32_t boff;  // byte offset of the frame's first granule in the blob
@@ -443,7 +440,9 @@ struct Blob {
     }
 };
 
-// Strides of 5 uint4 keep the owner-lane ds_read_b128 conflict-free (compact 4: DESIGN.md §8).
+// A stride of 5 uint4 spreads the owner lanes' ds_read_b128 of hdr over the banks. The LDS bank
+// conflicts left in the staged kernel are the LDS Active table's random lookups (76 %) and the counter
+// atomics (20 %), by ablation (profiles/r04g_lds_conflicts.json).
 constexpr uint32_t kHdrStride = 5;
 struct WaveLds {
     uint2 rec[64];              // phase B: per rank {owner lane | granules << 8, offset of the frame's first granule}
