@@ -16,12 +16,12 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# TPACKET_V3 path: the next block group's scan overlapped with the current group's pipeline
+# small-frame kernel workgroup size (DK_SMALL_WAVES 4 -> 5 / 8 / 10: fewer counter rows per launch)
 V=build/variants
 H=demikernel_amd/libdk_rx.so
-PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step t_ring 300 $PYT tests/test_gpu_parity.py -k tpacket3
-step gputest 900 $PYT -m gpu tests
-step ring_ab 400 python3 tools/ring_ab.py --lib $H --lib $V/ringprev.so --reps 5 --frames 262144
-step ring_ab2 400 python3 tools/ring_ab.py --lib $H --lib $V/ringprev.so --reps 5 --frames 1048576
+step parity 900 python3 -u tools/variant_parity.py --lib $V/sw5.so --lib $V/sw8.so --lib $V/sw10.so
+step ab_c3 400 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 11 --iters 16 --lib $H --lib $V/sw5.so \
+  --lib $V/sw8.so --lib $V/sw10.so "defer=1"
+step ab_c3r 400 python3 tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 9 --iters 16 --lib $H \
+  --lib $V/sw5.so --lib $V/sw8.so --lib $V/sw10.so "defer=1"
 echo done
