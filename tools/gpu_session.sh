@@ -16,12 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# small-frame kernel workgroup size (DK_SMALL_WAVES 4 -> 5 / 8 / 10: fewer counter rows per launch)
-V=build/variants
-H=demikernel_amd/libdk_rx.so
-step parity 900 python3 -u tools/variant_parity.py --lib $V/sw5.so --lib $V/sw8.so --lib $V/sw10.so
-step ab_c3 400 python3 tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 11 --iters 16 --lib $H --lib $V/sw5.so \
-  --lib $V/sw8.so --lib $V/sw10.so "defer=1"
-step ab_c3r 400 python3 tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 9 --iters 16 --lib $H \
-  --lib $V/sw5.so --lib $V/sw8.so --lib $V/sw10.so "defer=1"
+# round-end rehearsal at HEAD: the GPU tests, smoke() and the default bench line (as the driver runs them)
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
 echo done
