@@ -524,6 +524,50 @@ def test_tpacket3_ring_path_matches_oracle(torch_cuda):
         eng.close()
 
 
+def test_tpacket3_ring_pipelined_groups(torch_cuda):
+    """A long block range goes through dk_rx_process_tpacket3 in groups (the next group's scan overlapped with the
+    current group's pipeline): results equal the oracle on the frames one dk_ring_scan_tpacket3 over the same range
+    returns, and (frames, blocks) equal that scan's — over the whole ring, a range wrapping the ring end, a cap that
+    ends the range inside a later group, and a block of a later group still owned by the kernel."""
+    from demikernel_amd import RxResults
+    from demikernel_amd import ring as RG
+
+    flows = np.concatenate([synth.make_flows(256), synth.make_flows(16, kind="udp")])
+    n = 40000
+    tr = synth.traffic(n, 1486, flows, seed=13)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr, seed=13))
+    bs = 1 << 20
+    ring, used, eoff, elen = RG.build_tpacket3(blob, off, lens, bs, nblocks=None)
+    assert used >= 40  # four groups of >= 4 blocks and >= 4 MiB each
+    per = np.bincount((eoff // bs).astype(np.int64), minlength=used)
+    r = RG.TpacketRing(ring, bs)
+    eng = RxEngine(Config(LOCAL))
+    eng.set_sockets(flows)
+
+    def case(first, nblocks, cap, ctx):
+        s_off, s_len, s_nb = r.scan(first, nblocks, cap)  # one scan over the range: the expected outcome
+        res = RxResults(cap, len(flows), tcp_fields=True, host=True)
+        nf, nb = r.receive(eng, first, nblocks, res)
+        assert (nf, nb) == (len(s_off), s_nb), ctx
+        got = {k: (v if k in ("flow_counts", "verdict_counts") else v[:nf]) for k, v in res.to_numpy().items()}
+        assert_same(got, run_oracle(ring, s_off, s_len, flows), ctx)
+        return nf, nb
+
+    try:
+        assert case(0, used, n, "whole ring") == (n, used)
+        assert case(used - 25, 35, n, "wrapping range")[1] == 35
+        k = (3 * used) // 4 + 1
+        cap = int(per[:k].sum()) + 7
+        assert case(0, used, cap, "cap inside a later group") == (cap - 7, k)
+        j = used // 2 + 3
+        r.release(j, 1)  # block j back to the kernel: the range ends before it
+        assert case(0, used, n, "kernel-owned block") == (int(per[:j].sum()), j)
+    finally:
+        r.close()
+        eng.close()
+
+
 def full_size(n, ip_len, flows, corrupt=0.01, seed=synth.SEED, host_checksums=False, record="libos", defer=False):
     """A batch at a BASELINE config's full size with a `corrupt` tail (synth.corruption_plan), compared with the oracle
     on EVERY frame: all nine result arrays and both counter arrays of the whole batch, bit for bit (the oracle runs
