@@ -84,9 +84,6 @@ thread_local PinnedDescs t_descs;
 constexpr uint32_t kScanThreads = 8;              // host threads a long ring scan may use
 constexpr uint32_t kScanBlocksPerThread = 4;      // a thread walks at least this many blocks ...
 constexpr uint32_t kScanFramesPerThread = 16384;  // ... and this many frames (~0.2 ms of walk: more than a thread start)
-constexpr uint32_t kPipeGroups = 4;               // dk_rx_process_tpacket3: scan / process overlap over this many groups
-constexpr uint32_t kPipeBlocksPerGroup = 4;       // ... of at least this many blocks
-constexpr uint64_t kPipeBytesPerGroup = 4u << 20; // ... and this many ring bytes (a host pipeline call's fixed cost)
 
 uint32_t* status_word(uint8_t* ring, uint64_t base) {
     return reinterpret_cast<uint32_t*>(ring + base + offsetof(tpacket_block_desc, hdr.bh1.block_status));
@@ -206,70 +203,11 @@ int dk_rx_process_tpacket3(dk_rx_ctx* ctx, const void* ring, uint64_t ring_bytes
     *n_frames = *n_blocks = 0;
     int rc = t_descs.ensure(cap ? cap : 1);
     if (rc) return rc;
-    // A long range goes in up to kPipeGroups groups of blocks: the next group's scan runs on a helper thread while the
-    // calling thread pushes the current group through dk_rx_process_host, so only the first group's scan is exposed.
-    // The returned (frames, blocks, rc) are those of one scan over the whole range: a later group that stops early
-    // (block not ready, cap, malformed block) ends the call with the blocks before the stop.
-    const uint64_t nring = block_size ? ring_bytes / block_size : 0;
-    const uint32_t total = (uint32_t)std::min<uint64_t>(nblocks, nring);
-    const uint32_t groups = (uint32_t)std::min<uint64_t>(std::min(kPipeGroups, total / kPipeBlocksPerGroup),
-                                                         (uint64_t)total * block_size / kPipeBytesPerGroup);
-    if (groups < 2 || first_block >= nring) {
-        rc = dk_ring_scan_tpacket3(ring, ring_bytes, block_size, first_block, nblocks, t_descs.off, t_descs.len, cap,
-                                   n_frames, n_blocks);
-        if (rc || *n_frames == 0) return rc;
-        const dk_rx_batch b{static_cast<const uint8_t*>(ring), ring_bytes, t_descs.off, t_descs.len, *n_frames, 0};
-        return dk_rx_process_host(ctx, &b, res, 0);
-    }
-    struct Scan {
-        uint32_t nf = 0, nb = 0;
-        int rc = 0;
-    };
-    uint32_t* const doff = t_descs.off;  // (t_descs is this thread's: the helper thread gets the pointers)
-    uint16_t* const dlen = t_descs.len;
-    auto scan_group = [&](uint32_t g, uint32_t at, Scan& s) {  // group g's blocks into descriptor slots [at, cap)
-        const uint32_t b0 = (uint32_t)((uint64_t)total * g / groups), b1 = (uint32_t)((uint64_t)total * (g + 1) / groups);
-        s.rc = dk_ring_scan_tpacket3(ring, ring_bytes, block_size, (uint32_t)((first_block + b0) % nring), b1 - b0,
-                                     doff + at, dlen + at, cap - at, &s.nf, &s.nb);
-        return b1 - b0;
-    };
-    Scan cur;
-    uint32_t glen = scan_group(0, 0, cur);
-    if (cur.rc) {  // ENOSPC / EBADMSG on the range's first block, as the single scan reports them
-        *n_frames = cur.nf;
-        *n_blocks = cur.nb;
-        return cur.rc;
-    }
-    uint32_t at = 0;  // first descriptor slot of the current group
-    for (uint32_t g = 0;; g++) {
-        // the next group is scanned only when this one was consumed whole and cap has room left
-        const bool more = g + 1 < groups && cur.nb == glen && at + cur.nf < cap;
-        Scan nxt;
-        uint32_t nlen = 0;
-        std::thread th;
-        if (more) {
-            try {
-                th = std::thread([&] { nlen = scan_group(g + 1, at + cur.nf, nxt); });
-            } catch (...) {
-            }
-        }
-        dk_rx_results r = *res;  // this group's frames land at result index `at`
-        for (uint32_t** a : {&r.meta, &r.src_ip, &r.dst_ip, &r.ports, &r.payload, &r.flow_id, &r.tcp_seq, &r.tcp_ack,
-                             &r.tcp_win})
-            if (*a) *a += at;
-        if (r.tcp_opts) r.tcp_opts += at;
-        const dk_rx_batch b{static_cast<const uint8_t*>(ring), ring_bytes, doff + at, dlen + at, cur.nf, 0};
-        rc = cur.nf ? dk_rx_process_host(ctx, &b, &r, 0) : 0;
-        if (th.joinable()) th.join();
-        else if (more) nlen = scan_group(g + 1, at + cur.nf, nxt);  // no helper thread: scan here
-        *n_frames += cur.nf;
-        *n_blocks += cur.nb;
-        if (rc) return rc;
-        if (!more || nxt.rc) return 0;  // a later group's ENOSPC / EBADMSG on its first block: the blocks before it
-        at += cur.nf;
-        cur = nxt;
-        glen = nlen;
-    }
+    rc = dk_ring_scan_tpacket3(ring, ring_bytes, block_size, first_block, nblocks, t_descs.off, t_descs.len, cap,
+                               n_frames, n_blocks);
+    if (rc || *n_frames == 0) return rc;
+    const dk_rx_batch b{static_cast<const uint8_t*>(ring), ring_bytes, t_descs.off, t_descs.len, *n_frames, 0};
+    return dk_rx_process_host(ctx, &b, res, 0);
 }
 
 }  // extern "C"

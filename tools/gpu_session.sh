@@ -16,12 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# TPACKET_V3 path: the next block group's scan overlapped with the current group's pipeline
-V=build/variants
-H=demikernel_amd/libdk_rx.so
-PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step t_ring 300 $PYT tests/test_gpu_parity.py -k tpacket3
-step gputest 900 $PYT -m gpu tests
-step ring_ab 400 python3 tools/ring_ab.py --lib $H --lib $V/ringprev.so --reps 5 --frames 262144
-step ring_ab2 400 python3 tools/ring_ab.py --lib $H --lib $V/ringprev.so --reps 5 --frames 1048576
+# round-end rehearsal at HEAD: the GPU tests, smoke() and the default bench line (as the driver runs them)
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
 echo done
