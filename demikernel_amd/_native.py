@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("DK_RX_LIB_VARIANT", LIB_PATH)
 DK_FLOW_NONE = 0xFFFFFFFF
 DK_RX_BATCH_ALIGNED16 = 1  # dk_rx_batch.flags
 DK_RX_BATCH_DEFER_COUNTS = 2
+DK_RX_MAX_DEFERRED_FLOWS = 32768  # flow_counts defer only for tables up to this size (dk_rx.h)
 DK_FLOW_TCP_ACTIVE, DK_FLOW_TCP_PASSIVE, DK_FLOW_UDP = 1, 2, 3
 
 # enum dk_verdict (include/dk_rx.h), SURVEY.md Appendix A.

@@ -77,6 +77,7 @@ constexpr uint32_t kFlowNone = 0;    // no flow_counts requested
 constexpr uint32_t kFlowLds = 1;     // per-workgroup packed-u16 LDS histogram + scratch rows, combined per launch
 constexpr uint32_t kFlowGlobal = 2;  // per-frame u64 global atomics (tables too large for LDS)
 constexpr uint32_t kMaxLdsFlowWords = 16384;  // 64 KiB of LDS -> up to 32768 flows on the LDS path
+static_assert(2 * kMaxLdsFlowWords == DK_RX_MAX_DEFERRED_FLOWS, "dk_rx.h: flow counts defer on the LDS path only");
 constexpr uint32_t kVerdictWords = (DK_V_COUNT + 3) & ~3u;  // verdict histogram columns of a scratch row
 constexpr uint32_t kMaxTilesPerBlockLds = 255;  // 255 * 256 frames < 65536: a packed u16 counter never wraps
 constexpr uint32_t kRowAlignWords = 32;  // counter rows padded to whole 128-byte lines

@@ -198,9 +198,9 @@ int acquire_slot(dk_rx_ctx* c, hipStream_t stream, StreamSlot** out) {
             if (s.stamp < pick->stamp) pick = &s;
         c->saturated = true;
         if (flush_pending(*pick)) return EIO;  // its deferred rows reach their counters on the old stream first
-        pick->recorded = false;
-        bool ordered = pick->recorded;
-        if (!ordered && hipEventRecord(pick->last, pick->stream) == hipSuccess) ordered = true;
+        // Always record anew: flush_pending may just have queued a reduce launch on the old stream, after any event
+        // recorded earlier.
+        const bool ordered = hipEventRecord(pick->last, pick->stream) == hipSuccess;
         if (ordered) {
             if (hipStreamWaitEvent(stream, pick->last, 0) != hipSuccess) return EIO;
         } else {  // the old stream cannot be recorded on: wait for its work on the host instead

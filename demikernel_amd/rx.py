@@ -186,11 +186,22 @@ class RxEngine:
         _check(self.lib.dk_rx_ctx_create(ctypes.byref(cfg), ctypes.byref(h)), "dk_rx_ctx_create")
         self._ctx = h
         self.nflows = 0
+        # stream handle -> the RxResults of that stream's deferred launch: its pending counter rows hold raw pointers
+        # to the counter arrays (dk_rx.h DK_RX_BATCH_DEFER_COUNTS), so the arrays are kept alive until the next launch
+        # on the stream, a flush, forget_stream or close
+        self._pending = {}
+
+    @property
+    def flow_counts_deferred(self) -> bool:
+        """Whether DK_RX_BATCH_DEFER_COUNTS also defers flow_counts for the installed table (dk_rx.h: tables up to
+        DK_RX_MAX_DEFERRED_FLOWS entries; larger ones count flows inside the launch itself)."""
+        return self.nflows <= N.DK_RX_MAX_DEFERRED_FLOWS
 
     def close(self) -> None:
         if self._ctx:
-            self.lib.dk_rx_ctx_destroy(self._ctx)
+            self.lib.dk_rx_ctx_destroy(self._ctx)  # completes every pending row set first
             self._ctx = None
+        self._pending = {}
 
     def __del__(self):
         try:
@@ -222,6 +233,21 @@ class RxEngine:
             b.flags |= N.DK_RX_BATCH_DEFER_COUNTS
         _check(self.lib.dk_rx_process(self._ctx, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(s.cuda_stream)),
                "dk_rx_process")
+        # This launch completes the stream's previous deferred rows (inside its kernel) and leaves its own pending. The
+        # previous arrays may be released now that the launch is queued: record_stream keeps the caching allocator
+        # from reusing their memory before the work queued on `s` (this kernel) has run.
+        self._release_pending(s)
+        if defer_counts:
+            cnt = [results.t[k] for k in ("flow_counts", "verdict_counts") if k in results.t]
+            if cnt:
+                self._pending[s.cuda_stream] = (cnt, s)
+
+    def _release_pending(self, s) -> None:
+        prev = self._pending.pop(s.cuda_stream, None)
+        if prev is not None:
+            for t in prev[0]:
+                if t.is_cuda:
+                    t.record_stream(s)
 
     def flush_counts(self, stream=None) -> None:
         """dk_rx_counts_flush: the counters of a deferred batch on `stream` become current (one small launch)."""
@@ -229,6 +255,7 @@ class RxEngine:
 
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(self.lib.dk_rx_counts_flush(self._ctx, ctypes.c_void_p(s.cuda_stream)), "dk_rx_counts_flush")
+        self._release_pending(s)  # the flush launch is queued on `s`
 
     def build_id(self) -> str:
         return self.lib.dk_rx_build_id().decode()
@@ -238,6 +265,7 @@ class RxEngine:
         handle) before the stream is destroyed."""
         h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
         _check(self.lib.dk_rx_stream_forget(self._ctx, ctypes.c_void_p(h)), "dk_rx_stream_forget")
+        self._pending.pop(h, None)  # flushed and waited for by dk_rx_stream_forget
 
     def receive_batch_host(self, blob: np.ndarray, off: np.ndarray, lens: np.ndarray, results: RxResults,
                            chunk_frames: int = 0, aligned16: Optional[bool] = None) -> None:

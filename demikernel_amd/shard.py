@@ -149,9 +149,12 @@ class ShardedReceiver:
     def step(self, batch) -> None:
         slot = (self.k // self.every) % len(self.res)
         prev, prev_k = self.pending, self.k - 1
-        # the sets this launch changes: deferred, only the pending one it completes (its own rows stay pending);
+        # the sets this launch changes: deferred, the pending one it completes (its own rows stay pending) — and its
+        # own too when the engine counts flows inside the launch (tables above DK_RX_MAX_DEFERRED_FLOWS, dk_rx.h);
         # otherwise its own
         self._before_change(prev if self.defer else slot)
+        if self.defer and not getattr(self.eng, "flow_counts_deferred", True):
+            self._before_change(slot)
         self.eng.receive_batch(batch, self.res[slot], stream=self.stream, defer_counts=self.defer)
         if self.comm is not None:
             if self.defer:

@@ -65,7 +65,16 @@ extern "C" {
                                        kernel, or dk_rx_counts_flush does. Saves the dependent second launch
                                        (dk_flow_reduce_kernel) per batch when batches follow each other; the counters
                                        are current once a later launch on the stream, or a flush, has run. Ignored by
-                                       dk_rx_process_host (synchronous, counters current at return). */
+                                       dk_rx_process_host (synchronous, counters current at return).
+                                       Scope: verdict_counts are always deferred; flow_counts only while the flow
+                                       table has <= DK_RX_MAX_DEFERRED_FLOWS entries. Larger tables count flows with
+                                       device atomics inside the launch itself, so a caller that double-buffers the
+                                       counters (reads one set while launches add to the other) must treat such a
+                                       launch as writing its flow_counts immediately.
+                                       Lifetime: the pending contributions keep raw pointers to this call's
+                                       flow_counts / verdict_counts arrays; they must stay allocated until the next
+                                       launch on the stream, a flush, dk_rx_stream_forget or dk_rx_ctx_destroy. */
+#define DK_RX_MAX_DEFERRED_FLOWS 32768u /* flow tables up to this size keep per-workgroup flow rows (deferrable) */
 
 /* Largest frame blob of one batch (bytes): offsets are u32 and the engine keeps 256 bytes of the 32-bit range for its
  * out-of-range loads. */

@@ -85,6 +85,13 @@ def test_tcp_header_constants():
         assert re.search(rf"DK_TCP_{name} = {v}", hdr), name
 
 
+def test_defer_scope_constant():
+    """The flow-table size up to which DK_RX_BATCH_DEFER_COUNTS defers flow counts: header == Python mirror (rx.py
+    RxEngine.flow_counts_deferred, shard.py)."""
+    hdr = open(HEADERS[0]).read()
+    assert f"#define DK_RX_MAX_DEFERRED_FLOWS {N.DK_RX_MAX_DEFERRED_FLOWS}u" in hdr
+
+
 def test_verdict_tables():
     lib = N.load_library()
     assert lib.dk_rx_abi_version() == 4

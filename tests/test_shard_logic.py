@@ -108,6 +108,95 @@ def test_gathered_counts_exact(monkeypatch, every, defer, steps):
     assert n_gathers <= -(-steps // every) + 2, (n_gathers, steps, every)
 
 
+class LoggedStream:
+    device = "cpu"
+
+    def __init__(self, name, log):
+        self.name, self.log = name, log
+
+    def wait_event(self, ev):
+        self.log.append(("wait", self.name, ev.id))
+
+    def synchronize(self):
+        pass
+
+
+class LoggedEvent:
+    count = 0
+
+    def __init__(self, log):
+        LoggedEvent.count += 1
+        self.id, self.log = LoggedEvent.count, log
+
+    def record(self, stream=None):
+        self.log.append(("record", self.id, stream.name))
+
+
+class ImmediateFlowEngine(FakeEngine):
+    """A flow table above DK_RX_MAX_DEFERRED_FLOWS (dk_rx.h): with DK_RX_BATCH_DEFER_COUNTS only the verdict counts
+    wait for the next launch; flow counts land in the launch's own set at once."""
+
+    flow_counts_deferred = False
+
+    def __init__(self, inc_f, inc_v, world, log):
+        super().__init__(inc_f, inc_v, world)
+        self.glog = log
+        self.pend_v = None
+
+    def _complete(self):
+        if self.pend_v is not None:
+            self.pend_v.t["verdict_counts"] += self.inc_v
+            self.glog.append(("mutate", id(self.pend_v)))
+            self.pend_v = None
+
+    def receive_batch(self, batch, res, stream=None, defer_counts=False):
+        self._complete()
+        res.t["flow_counts"] += self.inc_f
+        self.glog.append(("mutate", id(res)))
+        if defer_counts:
+            self.pend_v = res
+        else:
+            res.t["verdict_counts"] += self.inc_v
+
+    def counts_allreduce_to(self, res, fo, vo, comm, stream=None):
+        super().counts_allreduce_to(res, fo, vo, comm, stream)
+        self.glog.append(("gather", id(res), stream.name))
+
+
+@pytest.mark.parametrize("every", [1, 2, 3])
+@pytest.mark.parametrize("steps", [2, 5, 9])
+def test_immediate_flow_counts_wait_for_their_sets_gather(monkeypatch, every, steps):
+    """a launch that adds flow counts to its set immediately (large tables) must first wait for that set's
+    previous all-reduce on the side stream: every mutation of a set after its gather is preceded, on the launch stream,
+    by a wait on the event recorded after that gather."""
+    log = []
+    monkeypatch.setattr(torch.cuda, "Stream", lambda device=None: LoggedStream("side", log))
+    monkeypatch.setattr(torch.cuda, "Event", lambda *a, **k: LoggedEvent(log))
+    monkeypatch.setattr(shard, "TorchCountsAllreduce", type("T", (), {}))
+    import demikernel_amd.rx as rx
+
+    monkeypatch.setattr(rx, "RxResults", Res)
+    world = 2
+    inc_f = torch.arange(1, 6, dtype=torch.int64)
+    inc_v = torch.tensor([3, 0, 1, 2], dtype=torch.int64)
+    eng = ImmediateFlowEngine(inc_f, inc_v, world, log)
+    sr = shard.ShardedReceiver(eng, Res(5), Comm(), LoggedStream("main", log), defer=True, gather_every=every)
+    for _ in range(steps):
+        sr.step(None)
+    sr.drain()
+    fo, vo = sr.counts()
+    assert torch.equal(fo, steps * world * inc_f) and torch.equal(vo, steps * world * inc_v)
+    for p, e in enumerate(log):
+        if e[0] != "mutate":
+            continue
+        gathers = [q for q in range(p) if log[q][0] == "gather" and log[q][1] == e[1]]
+        if not gathers:
+            continue
+        q = gathers[-1]
+        done = next(x[1] for x in log[q:] if x[0] == "record" and x[2] == "side")
+        assert ("wait", "main", done) in log[q:p], (p, log)
+
+
 def test_one_gpu_no_collective(monkeypatch):
     monkeypatch.setattr(torch.cuda, "Stream", lambda device=None: FakeStream())
     monkeypatch.setattr(torch.cuda, "Event", lambda *a, **k: FakeEvent())
