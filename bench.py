@@ -361,7 +361,7 @@ def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=5):
             "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
 
 
-def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
+def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0, buffer_size=1 << 24, reorder=3.0):
     """dk_tcp_rx_process over one dk_rx batch's results (nseg 1460-byte TCP segments spread
     over nconns established connections, reordered / duplicated / stray as synth.tcp_streams makes them), Mseg/s from
     HIP events around each call (the connection table is restored from a pristine copy between calls, outside the
@@ -369,11 +369,12 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
     import torch
 
     from demikernel_amd import RxResults, synth
+    from demikernel_amd._native import TCP_ACTIONS as TCP_ACTION_NAMES
     from demikernel_amd.tcp import TcpOut, TcpReceiver
     from oracle import oracle as O
 
     dev = stream.device
-    _, tr, table = synth.tcp_streams(nseg, nconns, 1500, buffer_size=1 << 24)
+    _, tr, table = synth.tcp_streams(nseg, nconns, 1500, buffer_size=buffer_size, reorder=reorder)
     rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
           "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
           "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
@@ -408,7 +409,9 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0):
             break
     tc = (time.perf_counter() - t0) / reps
     return {"mseg_s": round(nseg / t / 1e6, 1), "ms_avg": round(t * 1e3, 4), "segments": nseg, "connections": nconns,
+            "buffer_size": buffer_size, "reorder": reorder,
             "delivered_frac": round(float(hist[1]) / nseg, 3),
+            "actions": {name: int(c) for name, c in zip(TCP_ACTION_NAMES, hist) if c},
             "cpu_baseline": {"mseg_s": round(nseg / tc / 1e6, 2), "cores": 1, "kind": "port", "reps": reps},
             "walk": "wave" if nseg >= 8 * nconns else "lane",
             "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (lanes = connections, "
@@ -437,10 +440,18 @@ def tx_rate(eng, batch, frame_bytes, stream, iters=20):
     e1.record(stream)
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters
-    algo = frame_bytes + batch.n * (DESC_BYTES + 4)
+    # Bytes per frame: the frame read + its descriptor + the write. The fields themselves are 4 bytes (IPv4 + L4
+    # checksum), but an in-place patch cannot reach HBM as less than one 64-byte write (the DRAM burst; WRITE_SIZE
+    # counts exactly 64 B per frame, profiles/pmc_traffic.json): that physical write floor is what the roofline
+    # counts; the 4-byte figure is kept beside it.
+    algo = frame_bytes + batch.n * (DESC_BYTES + 64)
+    algo_fields = frame_bytes + batch.n * (DESC_BYTES + 4)
     return {"gbps": round(frame_bytes / t / 1e9, 1), "kernel_ms_avg": round(t * 1e3, 4),
             "roofline_achieved_gbps": round(algo / t / 1e9, 1), "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_launch": algo,
+            "bytes_counted": "frame + 6 B descriptor + 64 B written per frame (the physical write floor of an in-place "
+                             "patch; the fields are 4 B)",
+            "roofline_frac_field_bytes": round(algo_fields / t / 1e9 / HBM_PEAK_GBS, 4),
             "kernel": "dk_tx_split_kernel" if frame_bytes // max(batch.n, 1) >= 1024 else "dk_tx_kernel"}
 
 
@@ -515,6 +526,42 @@ def rx_extra(name, dev, stream, steps=30, warmup=3, rotate=1, dst_ip=True, tcp_f
                         "frac": round(algo / kern / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo,
                         "traffic": load_traffic_profile(name + ("_libos" if tcp_fields else ""))}}
     return out, eng, batches[0], flows
+
+
+def device_identity(dev) -> dict:
+    """What identifies this rank's GPU in the line (name, PCI location / UUID where torch exposes them)."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    ident = {"device_index": int(dev), "name": p.name}
+    for k in ("pci_bus_id", "pci_device_id", "pci_domain_id"):
+        if hasattr(p, k):
+            ident[k] = int(getattr(p, k))
+    if hasattr(p, "uuid"):
+        ident["uuid"] = str(p.uuid)
+    return ident
+
+
+def scale_fields(world, comm, per_rank, coll_s, gather_every):
+    """The fields by which a multi-GPU line proves itself: how many ranks the product's RCCL
+    communicator holds (dk_comm_count; None when the counters went through the test-only torch stand-in or there is
+    no communicator), each rank's own kernel time next to the max-over-ranks wall time, the collective's own time and
+    how often it runs."""
+    nranks = None
+    kind = "none"
+    if comm is not None and hasattr(comm, "count"):  # demikernel_amd.Comm: the include/dk_comm.h communicator
+        nranks = int(comm.count())
+        kind = "rccl (dk_rx_flow_counts_allreduce_to over dk_comm.h)"
+    elif comm is not None:
+        kind = "TEST ONLY: torch.distributed all_reduce (--counts-via-torch-gloo-test)"
+    rows = sorted(per_rank, key=lambda r: r["rank"])
+    ks = [r["kernel_ms_per_step"] for r in rows]
+    return {"rccl_nranks": nranks, "collective_kind": kind, "world_size": world,
+            "gather_every": gather_every if world > 1 else None,
+            "collective_ms_avg": round(float(np.mean(coll_s)) * 1e3, 4) if coll_s else None,
+            "per_rank": rows,
+            "kernel_ms_per_step_max": round(max(ks), 4) if ks else None,
+            "kernel_ms_per_step_min": round(min(ks), 4) if ks else None}
 
 
 def main():
@@ -602,6 +649,9 @@ def main():
         fc, vc = sr.counts()
         np.savez(args.counts_out, flow_counts=fc.cpu().numpy().view(np.uint64),
                  verdict_counts=vc.cpu().numpy().view(np.uint64), steps=args.steps + args.warmup)
+    mine = {"rank": rank, "kernel_ms_per_step": round(kern_avg * 1e3, 4),
+            "wall_ms_per_step": round(wall / args.steps * 1e3, 4), "frames": batch.n, "frame_bytes": frame_bytes,
+            "gpu": device_identity(dev)}
     if dist is not None:
         cdev = "cuda" if args.backend == "nccl" else "cpu"
         t = torch.tensor([wall], dtype=torch.float64, device=cdev)
@@ -610,8 +660,11 @@ def main():
         tb = torch.tensor([frame_bytes, batch.n], dtype=torch.int64, device=cdev)
         dist.all_reduce(tb)
         total_bytes, total_frames = int(tb[0]), int(tb[1])
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     else:
         total_bytes, total_frames = frame_bytes, batch.n
+        per_rank = [mine]
 
     value = total_bytes * args.steps / wall / 1e9
     algo = frame_bytes + batch.n * (DESC_BYTES + RESULT_BYTES)
@@ -647,8 +700,7 @@ def main():
         ceil_gbs, ceil_cfg = read_ceiling(batch, stream)
         out["roofline"]["measured_read_ceiling"] = {"value": round(ceil_gbs, 1), "unit": "GB/s", "probe": ceil_cfg,
                                                     "frac": round(achieved / ceil_gbs, 4)}
-    if coll:
-        out["collective_ms_avg"] = round(float(np.mean(coll)) * 1e3, 4)
+    out.update(scale_fields(world, comm, per_rank, coll, GATHER_EVERY))
     host = cpu_info()
     if rank == 0 and world == 1 and not args.no_cpu:
         blob_s, off_s, lens_s = host_sample(batch, args.cpu_sample)
@@ -705,7 +757,13 @@ def main():
         out["c2_libos_record"], e, _, _ = rx_extra("c2_tcp1500", dev, stream, tcp_fields=True)
         out["c2_libos_record"]["workload"] += " (LibOS record: + tcp_seq/ack/win, tcp_opts)"
         del e
-        out["c4_imix"], e, _, _ = rx_extra("c4_imix", dev, stream)
+        # IMIX rotates 2 distinct batches (1.7 GB): one 830 MB batch re-read every step gains 3-6 % from the 256 MB
+        # MALL / translation caches; the one-batch figure is kept beside it
+        c4, e, _, _ = rx_extra("c4_imix", dev, stream, rotate=2)
+        del e
+        c4b, e, _, _ = rx_extra("c4_imix", dev, stream, rotate=1)
+        c4["one_batch"] = {k: c4b[k] for k in ("gbps", "mpkt_s", "kernel_ms_avg", "roofline")}
+        out["c4_imix"] = c4
         del e
         out["c5_device"], e5, b5, f5 = rx_extra("c5_tcp1500_10k", dev, stream)
         # C5 end to end: the per-GPU shard in pinned host memory -> HBM -> kernel -> results to pinned host memory
@@ -726,9 +784,10 @@ def main():
         out["tcp_rx"] = tcp_rate(stream)
         # few connections with many segments each (the wave-per-connection walk)
         out["tcp_rx_64conns"] = tcp_rate(stream, 1 << 20, 64, cpu_seconds=1.0)
-        # one connection with 1M segments: its window fills early, the rest is out of window (classified in the
-        # key pass, never walked)
-        out["tcp_rx_1conn"] = tcp_rate(stream, 1 << 20, 1, cpu_seconds=1.0)
+        # one connection with 1M in-order segments (a single LAN stream: no reordering) and a 1 GiB receive window
+        # (the largest TCP window scaling allows, RFC 7323): ~70 % delivered in order, the ~29 % past the window
+        # classified out of window in the key pass and never walked
+        out["tcp_rx_1conn"] = tcp_rate(stream, 1 << 20, 1, cpu_seconds=1.0, buffer_size=1 << 30, reorder=0.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None and hasattr(comm, "destroy"):

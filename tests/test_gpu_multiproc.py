@@ -123,6 +123,14 @@ def test_bench_two_ranks_child_processes(tmp_path):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_frames"] == 2 * per
     assert "TEST ONLY" in line["config"]["collective"] and line["value"] > 0
+    # the line proves its own rank count: no RCCL communicator in the test mode (rccl_nranks null, the stand-in
+    # named), both ranks' own kernel times and shards, the gather period and the collective's own time
+    assert line["rccl_nranks"] is None and "TEST ONLY" in line["collective_kind"] and line["world_size"] == 2
+    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
+    assert sum(r["frames"] for r in line["per_rank"]) == 2 * per
+    assert all(r["kernel_ms_per_step"] > 0 and r["wall_ms_per_step"] > 0 for r in line["per_rank"])
+    assert line["kernel_ms_per_step_max"] >= line["kernel_ms_per_step_min"] > 0
+    assert line["gather_every"] == 8 and line["collective_ms_avg"] > 0
     got = np.load(out, allow_pickle=False)
     assert int(got["steps"]) == steps + warmup
     fc = np.zeros(0, np.uint64)

@@ -196,6 +196,21 @@ def test_streams_through_rx(tcp, n, nconns, batches):
     eng.close()
 
 
+def test_one_stream_gigabyte_window(tcp):
+    """bench.py's tcp_rx_1conn shape: one in-order stream of 2^20 segments through a 1 GiB receive window (the largest
+    TCP window scaling allows): ~70 % delivered in order, the rest past the window end; bit-exact vs the oracle."""
+    n = 1 << 20
+    _, tr, table = synth.tcp_streams(n, 1, 1500, buffer_size=1 << 30, reorder=0.0)
+    rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
+          "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
+          "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
+    exp_t = table.copy()
+    exp = O.tcp_process(exp_t, rx)
+    got_t, got = gpu_process(tcp, table.copy(), rx_device(rx))
+    assert_same(got_t, got, exp_t, exp, "1 conn, 1 GiB window")
+    assert np.mean(got["action"] == N.A["DELIVERED"]) > 0.5
+
+
 def test_rejects_missing_tcp_fields(tcp):
     import ctypes
 
