@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rx_common.h"
+#include "rx_diag.h"
 
 namespace dk {
 namespace {
@@ -387,9 +388,6 @@ __device__ __forceinline__ uint32_t probe_finish(const RxParams& P, const ProbeK
 }
 // UDP binds and TCP listeners: one exact load of the port table (rx_common.h).
 __device__ __forceinline__ uint32_t port_lookup(const RxParams& P, uint32_t base, uint32_t port) {
-#ifdef DK_ABL_NOPROBE  // ablation (tuning only): no table load
-    return port & 1023u;
-#endif
     return P.port_tab[base + port];
 }
 
@@ -766,9 +764,6 @@ __device__ __forceinline__ uint32_t seg_sum_fast(const Chunk& C, const WL& W, ui
         return C.fsum - pre - post;
     }
     resum = true;
-#ifdef DK_ABL_FASTONLY
-    return 0;
-#endif
     return MemAcc{f}.sum_le16(34, (uint32_t)E);
 }
 
@@ -827,16 +822,6 @@ constexpr int kStageK = DK_STAGE_K;
 // Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
 // results (stored, or handed back in rec for staging). Two halves so a kernel can interleave two chunks: rx_front
 // (parse, the first table probe issued, the L4 sum) and rx_back (verdicts, demux, results); rx_finish runs both.
-#ifdef DK_DIAG_STAMPS  // diagnostic build: sub-phase stamps of the small-frame kernel (tools/stamps.py)
-#define DK_SUB_STAMP(j)                                                                                             \
-    do {                                                                                                            \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                                           \
-        if (P.path_stats && lane == 0 && stamp_base != ~0u)                                                         \
-            P.path_stats[4 + 32 * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) + stamp_base + (j)] = t_;   \
-    } while (0)
-#else
-#define DK_SUB_STAMP(j) do {} while (0)
-#endif
 struct FinState {
     Lane L;
     ProbeKey k1;
@@ -869,9 +854,7 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     } else if (fast) {
         parse_fast(R, len, P, L);
     } else {
-#ifndef DK_ABL_FASTONLY  // ablation (tuning only, wrong for other batches): C3-shaped batches need no byte path
         parse_headers(MemAcc{f}, len, P, L);
-#endif
     }
     DK_SUB_STAMP(0);
     // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
@@ -885,23 +868,11 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
         St.s1 = lt_lookup(P, k1.rip, k1.lport_rport);
     } else if (L.v == kPendTcp) {  // the hash only for TCP lanes (a wave of UDP frames skips it)
         h1 = probe_slot(P, k1);
-#ifndef DK_ABL_NOPROBE
         St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
-#else  // ablation (tuning only): a first-slot hit without the load
-        St.s1 = make_uint4(k1.kind << 24 | (h1 & 1023u), k1.lip, k1.rip, k1.lport_rport);
-#endif
     }
-#ifndef DK_ABL_NOPROBE
     if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
-#else
-    if (L.v == kPendUdp) St.s1.x = (L.ports >> 16) & 1023u;
-#endif
     St.h1 = h1;
-#ifdef DK_ABL_FASTONLY
-    if (L.need) L.lsum = seg_sum_fast(C, W, lane, f, (int)L.E, resum);
-#else
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
-#endif
     DK_SUB_STAMP(1);
 }
 
@@ -935,11 +906,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
             const uint32_t c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
             if (c != L.stored) L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
         }
-#ifdef DK_ABL_FASTONLY
-        if (false) {
-#else
         if (L.v == kPendTcp && L.hlen > 20) {
-#endif
             const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20,
                                            kOpt && live && P.res.tcp_opts ? P.res.tcp_opts + i : nullptr);
             if (e) L.v = e;
@@ -962,9 +929,6 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
 
     DK_SUB_STAMP(2);
     const uint32_t v = L.v;
-#ifdef DK_ABL_STOREMOD  // ablation (tuning only; needs n > 65535): results land in a 256 KB L2-resident window
-    i &= 0xFFFFu;
-#endif
     if (live) {
         // fields for delivered / no-socket TCP and UDP and for parsed ARP and ICMPv4 (codes 0..3, dk_rx.h)
         const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;
@@ -981,17 +945,12 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
         }
         rec = Rec{meta, src, dst, ports, pay, fid, seq, ack, win};
         if (!kStage) {
-        st_res<kNtRes>(P.res.meta + i, meta);
-#ifdef DK_ABL_NOSTORE  // ablation (tuning only): one result array
-        if (ports == 0x12345678u)
-#endif
-        {
-        st_res<kNtRes>(P.res.src_ip + i, src);
-        if (P.res.dst_ip) st_res<kNtRes>(P.res.dst_ip + i, dst);
-        st_res<kNtRes>(P.res.ports + i, ports);
-        st_res<kNtRes>(P.res.payload + i, pay);
-        st_res<kNtRes>(P.res.flow_id + i, fid);
-        }
+            st_res<kNtRes>(P.res.meta + i, meta);
+            st_res<kNtRes>(P.res.src_ip + i, src);
+            if (P.res.dst_ip) st_res<kNtRes>(P.res.dst_ip + i, dst);
+            st_res<kNtRes>(P.res.ports + i, ports);
+            st_res<kNtRes>(P.res.payload + i, pay);
+            st_res<kNtRes>(P.res.flow_id + i, fid);
         }
         if (kOpt && !kTcpStaged) {  // optional outputs (kOpt = false: the caller asked for none; fewer live SGPRs)
             if (P.res.tcp_seq) P.res.tcp_seq[i] = seq;
@@ -1000,8 +959,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
         }
     }
     DK_SUB_STAMP(3);
-#ifndef DK_DIAG_STAMPS  // (the stamp build reuses the path-stats buffer)
-    if (kOpt && P.path_stats) {  // diagnostics (dk_diag.h): one atomic per path per wave
+    if (kPathStatsOn && kOpt && P.path_stats) {  // diagnostics (dk_diag.h): one atomic per path per wave
         const uint32_t path = !fast ? 3u : resum ? 2u : big ? 1u : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) {
@@ -1009,7 +967,6 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
             if (m && lane == 0) atomicAdd(P.path_stats + k, (unsigned long long)__popcll(m));
         }
     }
-#endif
     v_out = v;
     fid_out = fid;
 }
@@ -1018,17 +975,6 @@ template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = fa
 __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
                                           uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
-#ifdef DK_DIAG_STREAM_ONLY  // diagnostic build (tuning only): phases A and B alone, results = the raw sums
-#ifdef DK_DIAG_NO_STORE
-    if (live && (C.fsum ^ C.R.w[3] ^ C.R.w[9]) == 0x9E3779B1u)
-#else
-    if (live)
-#endif
-        P.res.meta[i] = C.fsum ^ C.R.w[3] ^ C.R.w[9];
-    v_out = kNone;
-    fid_out = DK_FLOW_NONE;
-    return;
-#endif
     FinState St;
     rx_front<kShift>(P, live, lane, W, off, len, C, St, stamp_base);
     rx_back<kStage, kOpt, kNtRes, kTcpStaged>(P, i, live, lane, off, St, v_out, fid_out, rec, stamp_base);
@@ -1110,12 +1056,7 @@ __device__ __forceinline__ void flow_add(const RxParams& P, bool lds_flows, uint
 }
 __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32_t lane, uint32_t v, uint32_t fid,
                                             bool lds_flows, uint32_t* s_flow, uint32_t* s_vh) {
-#ifdef DK_ABL_NOCOUNT  // ablation (tuning only): no flow / verdict counting
-    return;
-#endif
-#ifndef DK_ABL_NOFLOWCOUNT  // ablation (tuning only)
     const bool dl = live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP);
-#ifndef DK_FLOW_AGG_OFF  // ablation (tuning only): one add per delivered lane
     uint64_t todo = __ballot(dl);
     while (todo) {
         const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
@@ -1126,13 +1067,6 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
         if (__popcll(m) < kFlowAggMin) break;
     }
     if ((todo >> lane) & 1u) flow_add(P, lds_flows, s_flow, fid, 1u);
-#else
-    if (dl) flow_add(P, lds_flows, s_flow, fid, 1u);
-#endif
-#endif
-#ifdef DK_ABL_NOVCOUNT  // ablation (tuning only)
-    return;
-#endif
     if (P.res.verdict_counts) {
         uint64_t todo = __ballot(live);
         while (todo) {
@@ -1156,25 +1090,15 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
 // The kernels' by-value RxParams sits at the start of the kernel-argument segment. Fields used only at a kernel's end
 // (counter rows, the pending-rows combine) are read from there at the point of use: read through the by-value
 // parameter, the compiler loads them at the entry and keeps them in SGPRs across the chunk loop, where they spill to
-// VGPR lanes and cost v_readlane in the loop (DK_KARGS=0 restores that form for A/B).
-#ifndef DK_KARGS
-#define DK_KARGS 1
-#endif
+// VGPR lanes and cost v_readlane in the loop.
 __device__ __forceinline__ const RxParams& kargs(const RxParams& P) {
-#if DK_KARGS
     (void)P;
     return *(const RxParams*)__builtin_amdgcn_kernarg_segment_ptr();  // (a C cast: it leaves the constant space)
-#else
-    return P;
-#endif
 }
 __device__ __forceinline__ void flush_counters(const RxParams& P, uint32_t tid, uint32_t nthreads, bool lds_flows,
                                                const uint32_t* s_flow, const uint32_t* s_vh) {
     const RxParams& K = kargs(P);
     if (!K.row_words) return;
-#ifdef DK_ABL_NOFLUSH  // ablation (tuning only): counters never leave LDS
-    return;
-#endif
     uint32_t* row = K.flow_scratch + (size_t)blockIdx.x * K.row_stride;
     const uint32_t fw = K.flow_words;
     if (lds_flows)
@@ -1239,16 +1163,6 @@ __device__ __forceinline__ void combine_pending_tail(const RxParams& P, uint32_t
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
-#ifdef DK_DIAG_STAMPS  // diagnostic build: per-wave s_memtime stamps of dk_rx_kernel (tools/stamps_staged.py)
-#define DK_STAMPW(slot, t)                                                                                          \
-    do {                                                                                                            \
-        const uint64_t t_ = (t);                                                                                    \
-        if (P.path_stats && lane_id() == 0)                                                                         \
-            P.path_stats[4 + 32 * (blockIdx.x * kWaves + (threadIdx.x >> 6)) + (slot)] = t_;                        \
-    } while (0)
-#else
-#define DK_STAMPW(slot, t) do {} while (0)
-#endif
 template <bool kShift, bool kStage>
 __global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED)
 void dk_rx_kernel(RxParams P) {
@@ -1259,15 +1173,15 @@ void dk_rx_kernel(RxParams P) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6;
-    DK_STAMPW(12, __builtin_amdgcn_s_memrealtime());
-    DK_STAMPW(0, __builtin_amdgcn_s_memtime());
+    DK_STAMPW_RT(12);
+    DK_STAMPW(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
     for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
     lt_load(P, tid, kBlock);
     __syncthreads();
-    DK_STAMPW(1, __builtin_amdgcn_s_memtime());
+    DK_STAMPW(1);
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     StgRec<false> stg[kStage ? kStageK : 1];
@@ -1295,18 +1209,15 @@ void dk_rx_kernel(RxParams P) {
         Rec rec;
         rec.meta = kNoRec;
         Chunk C;
-        if (k < 3) DK_STAMPW(2 + 3 * k, __builtin_amdgcn_s_memtime());
+        if (k < 3) DK_STAMPW(2 + 3 * k);
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
-        if (k < 3) DK_STAMPW(3 + 3 * k, __builtin_amdgcn_s_memtime());
+        if (k < 3) DK_STAMPW(3 + 3 * k);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
-        if (k < 3) DK_STAMPW(4 + 3 * k, __builtin_amdgcn_s_memtime());
+        if (k < 3) DK_STAMPW(4 + 3 * k);
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
         // at the top of the next chunk, after a staged flush, their wait also waited for every store's write ack.
-#ifndef DK_EARLY_DESC
-#define DK_EARLY_DESC 1
-#endif
-        if (DK_EARLY_DESC) asm volatile("" ::"v"(noff), "v"(nlen));
+        asm volatile("" ::"v"(noff), "v"(nlen));
         if (kStage) {  // the last kStageK chunks' results; stored when full and at exit
             stage_put(stg, rec);
             if (++nstg == kStageK) {
@@ -1317,14 +1228,14 @@ void dk_rx_kernel(RxParams P) {
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
     }
 
-    DK_STAMPW(11, __builtin_amdgcn_s_memtime());
+    DK_STAMPW(11);
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, nchunks - 1);
     combine_pending_tail(P, lane, kWaves);  // a previous launch's deferred counter rows, in this wave's tail
-    DK_STAMPW(14, __builtin_amdgcn_s_memtime());
+    DK_STAMPW(14);
     __syncthreads();
     flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
-    DK_STAMPW(15, __builtin_amdgcn_s_memtime());
-    DK_STAMPW(13, __builtin_amdgcn_s_memrealtime());
+    DK_STAMPW(15);
+    DK_STAMPW_RT(13);
 }
 
 // Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
@@ -1374,7 +1285,6 @@ template <bool kShift, class WL, uint32_t kGran = kWinGran>
 __device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F, const Blob& B, uint32_t off,
                                                       uint32_t len, bool live, uint32_t lane, WL& W) {
     WinPlan pl{false, 0};
-#ifndef DK_SMALL_NOWIN
     const bool use = F.vec && !F.big;
     const uint32_t a = off - F.sh;  // the frame's first granule
     const uint64_t lm = __ballot(live);
@@ -1394,7 +1304,6 @@ __device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F
         pl.win = true;
         pl.lo = lo;
     }
-#endif
     return pl;
 }
 // The chunk's register windows: from the DMA'd window in LDS, or by per-lane loads (scattered frames).
@@ -1427,9 +1336,6 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
     uint32_t x[4] = {0, 0, 0, 0};
     C.fsum = 0;
     uint64_t bm = __ballot(F.big);
-#ifdef DK_ABL_FASTONLY
-    bm = 0;
-#endif
     if (bm) {
         while (bm) {
             const uint32_t j = (uint32_t)__builtin_ctzll(bm);
@@ -1487,9 +1393,6 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
 // Every other frame is left to a second pass after the loop (per-chunk masks in the launch scratch, P.defer), which
 // runs the general phase C (rx_finish) on them; results and counts are the same either way. Keeping the general path
 // out of the loop took the loop's code from 95 VGPRs and 71 spilled SGPRs to the fast path's own.
-#ifndef DK_SMALL_DEFER
-#define DK_SMALL_DEFER 1
-#endif
 #ifndef DK_SMALL_PRIO
 #define DK_SMALL_PRIO 1
 #endif
@@ -1517,11 +1420,7 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
         h1 = probe_slot(P, k1);
         s1 = reinterpret_cast<const uint4*>(P.table)[h1];
     }
-#ifdef DK_ABL_NOPROBE  // ablation (tuning only, flows wrong): no table load
-    if (L.v == kPendUdp) s1.x = (L.ports >> 16) & 1023u;
-#else
     if (L.v == kPendUdp) s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
-#endif
     uint32_t lsum = 0;
     if (L.need) {  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
         if (!__ballot(L.E != 64u)) {
@@ -1583,28 +1482,14 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
             if (P.res.tcp_win) P.res.tcp_win[i] = t ? L.winurg : 0u;
         }
     }
-#ifndef DK_DIAG_STAMPS
-    if (kOpt && P.path_stats) {  // diagnostics (dk_diag.h): every frame taken here is a register-window frame (path 0)
-        const uint64_t m = __ballot(live);
+    if (kPathStatsOn && kOpt && P.path_stats) {  // diagnostics (dk_diag.h): every frame taken here is a register-window
+        const uint64_t m = __ballot(live);           // frame (path 0)
         if (m && lane == 0) atomicAdd(P.path_stats + 0, (unsigned long long)__popcll(m));
     }
-#endif
     v_out = v;
     fid_out = fid;
 }
 
-#ifdef DK_DIAG_STAMPS  // diagnostic build (tuning only): per-wave s_memrealtime stamps after the path counters
-// s_memtime (shader clock, per XCD) for durations; slots 12/13 hold s_memrealtime (100 MHz, global) at entry/exit.
-#define DK_STAMP_T(slot, t)                                                                                         \
-    do {                                                                                                            \
-        const uint64_t t_ = (t);                                                                                    \
-        if (P.path_stats && lane == 0 && (slot) < 16)                                                               \
-            P.path_stats[4 + 32 * (blockIdx.x * kSmallWaves + wv) + (slot)] = t_;                                   \
-    } while (0)
-#define DK_STAMP(slot) if ((slot) < 11) DK_STAMP_T(slot, __builtin_amdgcn_s_memtime())
-#else
-#define DK_STAMP(slot) do {} while (0)
-#endif
 template <bool kShift, bool kOpt>
 __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
     __shared__ SmallLds s_wave[kSmallWaves];
@@ -1614,20 +1499,15 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6;
-#ifdef DK_DIAG_STAMPS
-    DK_STAMP_T(12, __builtin_amdgcn_s_memrealtime());
-#endif
+    DK_STAMP_RT(12);
     DK_STAMP(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
     const WaveRange r = wave_range<kSmallWaves>(P.sched, P.n, wv, lane);
-#ifndef DK_SMALL_DESC_EARLY
-#define DK_SMALL_DESC_EARLY 1
-#endif
     uint32_t c, lim, c1 = 0, lim1 = 0, c2 = 0, lim2 = 0;
     bool have = r.chunk(0, c, lim);
     bool have1 = have && r.chunk(1, c1, lim1);
     uint32_t off = 0, len = 0, off1 = 0, len1 = 0;
-#if DK_SMALL_DESC_EARLY  // the first two chunks' descriptors in flight during the LDS init and the barrier
+    // the first two chunks' descriptors in flight during the LDS init and the barrier
     if (have && c + r.lane_off < lim) {
         off = P.off[c + r.lane_off];
         len = P.len[c + r.lane_off];
@@ -1636,102 +1516,61 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = P.off[c1 + r.lane_off];
         len1 = P.len[c1 + r.lane_off];
     }
-#endif
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
     __syncthreads();
-#ifdef DK_DIAG_STAMPS
-    DK_STAMP_T(11, __builtin_amdgcn_s_memtime());
-#endif
+    DK_STAMP(11);
     // The grid is one generation of waves and the chunks do not divide evenly: the waves with one chunk more than the
     // rest (the last round's) set the launch's length, so they issue first on their SIMD (s_setprio; round 4: C3
-    // -2.1 % together with the first descriptors loaded before the barrier, DK_SMALL_DESC_EARLY).
-#if DK_SMALL_PRIO
-    {
+    // -2.1 % together with the first descriptors loaded before the barrier).
+    if (DK_SMALL_PRIO) {
         uint32_t cc, ll;
         const uint32_t kmin = ((P.n + 63) / 64) / (gridDim.x * kSmallWaves);
         if (r.chunk(kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_SMALL_PRIO);
     }
-#endif
     const Blob B(P.frames, P.frames_bytes);
     SmallLds& W = s_wave[wv];
-    // Pipeline: descriptors are loaded two chunks ahead. With DK_SMALL_LATE (default) chunk k + 2's descriptor loads
-    // are issued before chunk k's window DMA, so the window's wait covers them, and chunk k's deferral mask is stored
-    // after its result stores and only when the chunk left frames (`had`), so it sits behind the next window's wait.
-    // Issued after the window (DK_SMALL_LATE=0, rounds 2-3), the descriptor loads and the mask store were caught by the
-    // compiler's wait for the window registers of the per-lane-load path: one more memory round trip per chunk.
-#ifndef DK_SMALL_LATE
-#define DK_SMALL_LATE 1
-#endif
-#if !DK_SMALL_DESC_EARLY
-    if (have && c + r.lane_off < lim) {
-        off = P.off[c + r.lane_off];
-        len = P.len[c + r.lane_off];
-    }
-    if (have1 && c1 + r.lane_off < lim1) {
-        off1 = P.off[c1 + r.lane_off];
-        len1 = P.len[c1 + r.lane_off];
-    }
-#endif
+    // Pipeline: descriptors are loaded two chunks ahead. Chunk k + 2's descriptor loads are issued before chunk k's
+    // window DMA, so the window's wait covers them, and chunk k's deferral mask is stored after its result stores and
+    // only when the chunk left frames (`had`), so it sits behind the next window's wait. (Issued after the window,
+    // rounds 2-3, the descriptor loads and the mask store were caught by the compiler's wait for the window registers of
+    // the per-lane-load path: one more memory round trip per chunk.)
     Chunk C;
     FrameDesc<kShift> F(P.frames, P.frames_bytes, have && c + r.lane_off < lim, off, len);
     const uint32_t nw = gridDim.x * kSmallWaves, gw = blockIdx.x * kSmallWaves + wv;  // deferral mask index k nw + gw
     bool deferred = false;  // wave-uniform: a chunk left frames to the general pass
     // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
-    uint64_t had = DK_SMALL_LATE ? 0ull : ~0ull;
+    uint64_t had = 0;
     for (uint32_t k = 0; have; k++) {
         const uint32_t i = c + r.lane_off;
         const bool live = i < lim;
         const bool have2 = have1 && r.chunk(k + 2, c2, lim2);
         uint32_t off2 = 0, len2 = 0;
-#if DK_SMALL_LATE
         if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead, before this chunk's window DMA
             off2 = P.off[c2 + r.lane_off];
             len2 = P.len[c2 + r.lane_off];
         }
-#endif
         const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + r.lane_off < lim1, off1, len1);
         uint32_t v, fid;
-        Rec rec;
-        rec.meta = kNoRec;
         if (k == 0) DK_STAMP(1);
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
-#if !DK_SMALL_LATE
-        if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead (after the window wait)
-            off2 = P.off[c2 + r.lane_off];
-            len2 = P.len[c2 + r.lane_off];
-        }
-#endif
-        DK_STAMP(2 + 3 * k);
-#if DK_SMALL_DEFER
+        if (k < 3) DK_STAMP(2 + 3 * k);
         if (kShift && __ballot(live && F.vec && !F.big && F.sh != 0)) {  // realign the windows of shifted frames
             uint32_t x[4] = {0, 0, 0, 0};
             if (F.vec && !F.big && F.sh != 0) realign(C.R.w, x, F.sh);
         }
         const bool take = live && small_fast_eligible(F, len, C.R);
         const uint64_t dm = __ballot(live && !take);
-#if !DK_SMALL_LATE
-        if (lane == 0) P.defer[k * nw + gw] = dm;  // every chunk's mask, read back by this wave after the loop
-#endif
         deferred = deferred || dm != 0;
         small_fast<kOpt>(P, i, take, lane, C.R, len, v, fid);
-        DK_STAMP(3 + 3 * k);
+        if (k < 3) DK_STAMP(3 + 3 * k);
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
-#if DK_SMALL_LATE
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
             if (lane == 0) P.defer[k * nw + gw] = dm;
             if (k < 64) had |= 1ull << k;
         }
-#endif
-#else
-        small_big_frames(F, lane, off, B, W, C);
-        rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, live, lane, W, off, len, C, v, fid, rec,
-                                                       k < 3 ? 16 + 5 * k : ~0u);
-        DK_STAMP(3 + 3 * k);
-        count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
-#endif
-        DK_STAMP(4 + 3 * k);
+        if (k < 3) DK_STAMP(4 + 3 * k);
         // rotate the pipeline
         have = have1;
         c = c1;
@@ -1745,7 +1584,6 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
-#if DK_SMALL_DEFER
     if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
         uint32_t cd, limd;
@@ -1766,17 +1604,12 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
             count_chunk(P, mine, lane, v, fid, lds_flows, s_flow, s_vh);
         }
     }
-#endif
     combine_pending_tail(P, lane, kSmallWaves);  // a previous launch's deferred counter rows, in this wave's tail
-#ifdef DK_DIAG_STAMPS
-    DK_STAMP_T(14, __builtin_amdgcn_s_memtime());
-#endif
+    DK_STAMP(14);
     __syncthreads();
     flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh);
-#ifdef DK_DIAG_STAMPS
-    DK_STAMP_T(15, __builtin_amdgcn_s_memtime());
-    DK_STAMP_T(13, __builtin_amdgcn_s_memrealtime());
-#endif
+    DK_STAMP(15);
+    DK_STAMP_RT(13);
 }
 
 // A wave's chunks with their descriptors loaded one chunk ahead: D.off / D.len belong to chunk D.c (0 outside the
@@ -1974,7 +1807,7 @@ __global__ __launch_bounds__(SplitShape<kFin>::kThreads, 1) void dk_rx_split_ker
             Rec rec;
             rec.meta = kNoRec;
             rx_finish<kShift, true, WaveLds, true, false, kTcp>(P, i, live, lane, W, off, len, C, v, fid, rec);
-            if (DK_EARLY_DESC) asm volatile("" ::"v"(D.off), "v"(D.len));  // waited for before the stores (as dk_rx_kernel)
+            asm volatile("" ::"v"(D.off), "v"(D.len));  // waited for before the stores (as dk_rx_kernel)
             if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
             stage_put(stg, rec);
             klast = p;
@@ -2005,9 +1838,6 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
                                                                 uint32_t nflows, uint64_t* counts,
                                                                 uint64_t* verdicts) {
     __shared__ uint64_t s_part[kWaves][2][kReduceCols];
-#ifdef DK_ABL_REDUCE_EMPTY  // ablation (tuning only): the cost of the second launch alone
-    return;
-#endif
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t w = blockIdx.x * kReduceCols + lane;
     const uint32_t r0 = blockIdx.y * kReduceRows, r1 = min(rows, r0 + kReduceRows);
@@ -2034,10 +1864,6 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
         lo += s_part[k][0][lane];
         hi += s_part[k][1][lane];
     }
-#ifdef DK_ABL_REDUCE_NOATOMIC  // ablation (tuning only): loads and sums, no atomics
-    if (lo == 0x123456789ull) counts[0] = hi;
-    return;
-#endif
     if (w >= flow_words) {  // verdict column: a plain u32 count
         const uint32_t v = w - flow_words;
         const uint64_t t = lo + (hi << 16);
@@ -2057,32 +1883,12 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
 // consistent total_length are left untouched; TCP with a bad data offset / UDP shorter than 8 keep only the IPv4 fill
 // (oracle dko_tx_fill_checksums). Frames must not overlap.
 // ---------------------------------------------------------------------------------------------------------------------
-#ifndef DK_TX_STORE
-#define DK_TX_STORE 3  // 0: 16-bit stores; 1: nontemporal 16-bit; 2: the 16-byte block holding the field; 3: bytes [0, 64)
-#endif
-__device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {  // p is 2-byte aligned on the fast path
-#if DK_TX_STORE == 1
-    __builtin_nontemporal_store((uint16_t)bswap16(v), reinterpret_cast<uint16_t*>(p));
-#else
+// A 16-bit field write (frames shorter than 64 bytes or not 16-byte aligned; p is 2-byte aligned on the fast path).
+// Frames of >= 64 bytes rewrite their whole 64-byte header window instead (tx_finish): full-line writes need no
+// partial-write merge below L2 (16-bit stores, nontemporal 16-bit stores and 16-byte block rewrites measured slower,
+// round 1-2, profiles/HISTORY.md).
+__device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
     *reinterpret_cast<uint16_t*>(p) = (uint16_t)bswap16(v);
-#endif
-}
-// Fast-path field write at frame byte k (k even, k < 64, even frame address): DK_TX_STORE 2 rewrites the whole
-// 16-byte block from the register window when the block lies inside the frame (a full-block write needs no
-// read-modify-write below L2), else a 16-bit store.
-template <int k>
-__device__ __forceinline__ void store_field(uint8_t* f, const RegAcc& R, uint32_t len, uint32_t sh, uint32_t v) {
-#if DK_TX_STORE == 2
-    constexpr int b = k / 16;
-    if (sh == 0 && (uint32_t)(16 * b + 16) <= len) {
-        uint32_t d[4] = {R.w[4 * b], R.w[4 * b + 1], R.w[4 * b + 2], R.w[4 * b + 3]};
-        constexpr int j = (k / 4) % 4;
-        d[j] = (k & 2) ? (d[j] & 0xFFFFu) | (bswap16(v) << 16) : (d[j] & 0xFFFF0000u) | bswap16(v);
-        *reinterpret_cast<uint4*>(f + 16 * b) = make_uint4(d[0], d[1], d[2], d[3]);
-        return;
-    }
-#endif
-    store_be16(f + k, v);
 }
 
 // Byte path (misaligned frames, IHL != 5): lane per frame.
@@ -2158,7 +1964,6 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
                                 bswap16(dst >> 16) + proto + seg;
         c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
     }
-#if DK_TX_STORE == 3
     if (len >= 64 && C.sh == 0) {  // rewrite the whole 64-byte header window: full-line writes, no partial-write merge below L2
         uint32_t d[16];
 #pragma unroll
@@ -2166,9 +1971,6 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
         d[6] = (d[6] & 0xFFFF0000u) | bswap16(ipc);
         if (l4 && tcp) d[12] = (d[12] & 0xFFFFu) | (bswap16(c) << 16);
         if (l4 && !tcp) d[10] = (d[10] & 0xFFFF0000u) | bswap16(c);
-#ifdef DK_TX_ABL_NOSTORE  // ablation (tuning only): no window write
-        if ((d[6] ^ d[12] ^ d[10]) != 0x9E3779B1u) return;
-#endif
         if (kStage) {
 #pragma unroll
             for (int k = 0; k < 16; k++) win.d[k] = d[k];
@@ -2176,26 +1978,12 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
             return;
         }
         uint4* q = reinterpret_cast<uint4*>(f);
-#if defined(DK_TX_ABL_NT)  // tuning: nontemporal window stores
-#pragma unroll
-        for (int k = 0; k < 16; k++) __builtin_nontemporal_store(d[k], reinterpret_cast<uint32_t*>(f) + k);
-        return;
-#endif
 #pragma unroll
         for (int k = 0; k < 4; k++) q[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
-#ifdef DK_TX_ABL_W128  // ablation (tuning only, wrong bytes 64..127): whole 128-byte line writes
-        if (len >= 128)
-#pragma unroll
-            for (int k = 4; k < 8; k++) q[k] = make_uint4(d[0], d[1], d[2], d[3]);
-#endif
         return;
     }
-#endif
-    store_field<24>(f, R, len, C.sh, ipc);
-    if (l4) {
-        if (tcp) store_field<50>(f, R, len, C.sh, c);
-        else store_field<40>(f, R, len, C.sh, c);
-    }
+    store_be16(f + 24, ipc);
+    if (l4) store_be16(f + (tcp ? 50 : 40), c);
 }
 
 __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t lane, WaveLds& W, uint32_t off,
@@ -2340,11 +2128,7 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     else
         hipLaunchKernelGGL((dk::dk_rx_kernel<true, false>), dim3(grid), dim3(dk::kBlock), dyn, s, p);
     if (hipGetLastError() != hipSuccess) return 5;
-#ifdef DK_ABL_NOFLUSH
-    if (false) {
-#else
     if (p.row_words && !p.defer_rows) {
-#endif
         const dim3 g2((p.row_words + dk::kReduceCols - 1) / dk::kReduceCols,
                       (grid + dk::kReduceRows - 1) / dk::kReduceRows);
         hipLaunchKernelGGL(dk::dk_flow_reduce_kernel, g2, dim3(dk::kBlock), 0, s, p.flow_scratch, grid, p.row_words,

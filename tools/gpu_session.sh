@@ -16,8 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# round-end rehearsal at HEAD: the GPU tests, smoke() and the default bench line (as the driver runs them)
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+# r05a: the new GPU tests (tests.rs IPv4 vectors + UDP KAT through the HIP path, the 1 GiB-window TCP stream, the
+# two-rank bench line's scaling fields), then the default bench line
+step refvec 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k reference
+step newtests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_tcp.py::test_one_stream_gigabyte_window tests/test_gpu_multiproc.py
 step bench 600 python bench.py
 echo done
