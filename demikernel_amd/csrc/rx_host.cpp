@@ -40,6 +40,8 @@ struct CountScratch {
     size_t ndefer = 0;
     bool pending = false;
     dk::RowCombine pend{};       // rows, nrows, row_words, row_stride, flow_words, nflows, counts, verdicts
+    uint32_t* tail = nullptr;    // the staged kernel's dynamic-tail counters: two sets of dk::kTailSetWords (zeroed)
+    uint32_t tail_set = 0;       // the set the next tail launch uses (each launch zeroes the other one)
 };
 
 // A context's scratch is keyed by stream: calls on different streams never share counter rows, so their
@@ -73,6 +75,7 @@ struct Stage {  // device staging for one pipeline stream
 struct Tuning {
     int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
     int32_t lds_table = -1;  // 0: Active lookups never use the LDS table (DK_RX_LDS_TABLE)
+    int32_t tail = -1;       // staged kernel's dynamic tail rounds (DK_RX_TAIL; 0 off)
     int32_t host_zc = -1;  // dk_rx_process_host: read mapped pinned frames in place (-1/1 when mapped, 0 never)
 };
 
@@ -146,6 +149,7 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
 void free_slot(StreamSlot& s) {  // the caller has flushed and waited for the slot's launches
     if (s.cs.rows) (void)hipFree(s.cs.rows);
     if (s.cs.defer) (void)hipFree(s.cs.defer);
+    if (s.cs.tail) (void)hipFree(s.cs.tail);
     if (s.last) (void)hipEventDestroy(s.last);
     s = StreamSlot{};
 }
@@ -240,6 +244,15 @@ int ensure_counts(StreamSlot& s, uint32_t grid, uint32_t row_stride, size_t ndef
     return 0;
 }
 
+// The slot's dynamic-tail counters, allocated (and zeroed) on first use; they never grow.
+int ensure_tail(StreamSlot& s) {
+    if (s.cs.tail) return 0;
+    if (hipMalloc(&s.cs.tail, 2 * dk::kTailSetWords * sizeof(uint32_t)) != hipSuccess) return ENOMEM;
+    if (hipMemset(s.cs.tail, 0, 2 * dk::kTailSetWords * sizeof(uint32_t)) != hipSuccess) return EIO;  // synchronous
+    s.cs.tail_set = 0;
+    return 0;
+}
+
 // Choose the flow-count mode and the persistent grid, then launch on `stream` with that stream's counter scratch.
 // size_hint = bytes of blob the batch covers (the family and grid follow the mean bytes per frame).
 
@@ -317,6 +330,17 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
+    // The staged kernel's dynamic tail (rx_common.h): with `per` whole round-robin rounds of chunks per wave, the
+    // first per + 1 - d stay round-robin and the rest (d - 1 rounds + the partial one) are grabbed from per-XCD
+    // counters; at least 2 round-robin rounds (the first grab is issued during round ks - 2).
+    p.tail_ks = 0;
+    p.tail_ctr = p.tail_next = nullptr;
+    const int32_t tail_d = T.tail >= 0 ? T.tail : 2;
+    if (family == dk::kFamilyStaged && p.sched == 0 && tail_d > 0) {
+        const uint32_t nwaves = grid * 4u, nchunk = (p.n + 63) / 64;
+        const uint32_t per = nchunk / nwaves;
+        if (per + 1 >= (uint32_t)tail_d + 2) p.tail_ks = per + 1 - (uint32_t)tail_d;
+    }
     // Per-workgroup histogram rows (flow pairs, then verdicts; dk_flow_reduce_kernel adds them up, or the next launch
     // on the stream when this one defers them) and the small-frame kernel's deferral masks: a launch that needs either,
     // or that has a previous launch's rows to combine, uses the stream's scratch slot.
@@ -328,8 +352,13 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
     // per (wave, chunk): at most ceil(n / 64) + 2 chunks per wave of the grid (sched 1's partial chunks)
     const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * dk_rx_small_block_waves() : 0;
-    if (p.row_words || ndefer || has_pending) {
+    if (p.row_words || ndefer || has_pending || p.tail_ks) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
+        if (p.tail_ks) {
+            if ((rc = ensure_tail(*slot))) return rc;
+            p.tail_ctr = slot->cs.tail + (size_t)slot->cs.tail_set * dk::kTailSetWords;
+            p.tail_next = slot->cs.tail + (size_t)(slot->cs.tail_set ^ 1u) * dk::kTailSetWords;
+        }
         if (p.row_words)
             p.row_stride = (p.row_words + dk::kRowAlignWords - 1) / dk::kRowAlignWords * dk::kRowAlignWords;
         if ((rc = ensure_counts(*slot, grid, p.row_stride, ndefer))) return rc;
@@ -347,10 +376,11 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.defer_rows = defer && p.row_words ? 1u : 0u;
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
-                        "small=%u lds_table=%u defer=%u combine=%u\n",
+                        "small=%u lds_table=%u defer=%u combine=%u tail_ks=%u\n",
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
-                p.small, p.lt_words ? p.lt_n : 0u, p.defer_rows, p.comb.nblk);
+                p.small, p.lt_words ? p.lt_n : 0u, p.defer_rows, p.comb.nblk, p.tail_ks);
     rc = dk_launch_rx(p, grid, stream);
+    if (rc == 0 && cs && p.tail_ks) cs->tail_set ^= 1u;  // this launch zeroed the other set for the next one
     if (rc == 0 && cs) {
         if (p.comb.rows) cs->pending = false;
         if (p.row_words) {
@@ -483,6 +513,7 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     t.debug = env_knob("DK_RX_DEBUG");
     t.host_zc = env_knob("DK_RX_HOST_ZC");
     t.lds_table = env_knob("DK_RX_LDS_TABLE");
+    t.tail = env_knob("DK_RX_TAIL");
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
     std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
@@ -812,6 +843,7 @@ int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t* knobs, uint32_t nknobs) {
     t.grid_per_cu = k[5];
     t.debug = k[6] < 0 ? 0 : k[6];
     t.lds_table = k[7];
+    t.tail = k[8];
     t.host_zc = zc;
     c->tune = t;
     c->occ_family = ~0u;

@@ -447,6 +447,7 @@ struct WaveLds {
     uint32_t csum[64];          // phase B: whole-frame LE-half sums by owner lane
     uint4 hdr[64][kHdrStride];  // phase B -> C: granules 0..4 of each big frame (bytes [0, 64) + shift)
     uint4 tail[64];             // phase B -> C: the last granule of each big frame
+    uint32_t cb[16];            // staged kernel: the first frame of each chunk staged since the last flush
 };
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -818,6 +819,7 @@ struct StgRec<true> {
 #define DK_MIN_WAVES_STAGED 3  // 9 x 6 staged words and one round of loads fit in 168 VGPRs without spills
 #endif
 constexpr int kStageK = DK_STAGE_K;
+static_assert(kStageK <= 16, "WaveLds::cb holds the staged chunks' bases");
 
 // Phase C of one chunk (lane per frame) from what the streaming left in C and W: parse, checksum, options, demux,
 // results (stored, or handed back in rec for staging). Two halves so a kernel can interleave two chunks: rx_front
@@ -1021,17 +1023,21 @@ __device__ __forceinline__ void stage_put(T (&stg)[kN], const Rec& rec) {
     for (int q = kN - 1; q > 0; q--) stg[q] = stg[q - 1];
     stg[0] = rec;
 }
-// Store the nst most recent staged chunks: stg[q] holds the results of chunk k_last - q (kNoRec marks idle lanes).
+// Store the nst most recent staged chunks: stg[q] holds the results of the (nst - 1 - q)-th chunk staged since the last
+// flush, whose first frame is cb[nst - 1 - q] (the wave's chunk bases in LDS, written by lane 0 as each chunk is
+// staged: with the dynamic tail a chunk's position is not a function of its round). kNoRec marks idle lanes.
 constexpr uint32_t kNoRec = 0xFFFFFFFFu;  // never a meta word (verdicts < 64)
 __device__ __forceinline__ void flush_staged(const RxParams& P, const StgRec<false> (&stg)[kStageK], uint32_t nst,
-                                             const WaveRange& r, uint32_t k_last) {
+                                             const uint32_t* cb, uint32_t lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int q = kStageK - 1; q >= 0; q--) {
         if ((uint32_t)q >= nst) continue;
-        uint32_t c, lim;
-        (void)r.chunk(k_last - (uint32_t)q, c, lim);
+        const uint32_t c = __builtin_amdgcn_readfirstlane(cb[nst - 1 - (uint32_t)q]);  // uniform: SGPR addressing
         if (stg[q].meta == kNoRec) continue;
-        const uint32_t i = c + r.lane_off;
+        const uint32_t i = c + lane;
         st_res(P.res.meta + i, stg[q].meta);
         st_res(P.res.src_ip + i, stg[q].src);
         if (P.res.dst_ip) st_res(P.res.dst_ip + i, stg[q].dst);
@@ -1155,6 +1161,43 @@ __device__ __forceinline__ void combine_pending_tail(const RxParams& P, uint32_t
     combine_pending(P, lane, nw - 1 - gw, nw);
 }
 
+// The staged kernel's dynamic tail (rx_common.h kTailXcds): chunks j in [lo, lo + T) after the round-robin rounds, in
+// kTailXcds pools [lo + T x / 8, lo + T (x + 1) / 8), pool x handed out by counter x. Wave-uniform state; lane 0 issues
+// the grabs (one returning device-scope atomic each) and readfirstlane broadcasts the old counter value.
+constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
+// Live state is kept to two registers (the kernel is at its VGPR budget): xoff, the pools found empty so far (the pool
+// grabbed from is (XCC id + xoff) mod 8, the id re-read from the hardware register), and gv, lane 0's pending grab;
+// the counter set and the tail range are re-read from the kernel arguments (kargs) where they are used.
+struct TailQ {
+    uint32_t xoff;  // wave-uniform
+    uint32_t gv;    // lane 0: the pending grab's counter value
+    __device__ __forceinline__ static uint32_t pool(uint32_t xoff) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        return (xcc + xoff) & (kTailXcds - 1);
+    }
+    __device__ __forceinline__ void issue(const RxParams& P, uint32_t lane) {
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(kargs(P).tail_ctr + pool(xoff) * kTailStride, 1u);
+        gv = g;
+    }
+    // The chunk the pending grab got, or kNoChunk once every pool is empty (grabbing from the next pools on the way).
+    __device__ __forceinline__ uint32_t resolve(const RxParams& P, uint32_t lane) {
+        const RxParams& K = kargs(P);
+        const uint32_t lo = K.tail_ks * gridDim.x * kWaves, nchunk = (K.n + 63) / 64;
+        const uint32_t T = nchunk > lo ? nchunk - lo : 0u;
+        uint32_t g = __builtin_amdgcn_readfirstlane(gv);
+        for (;;) {
+            const uint32_t x = pool(xoff);
+            const uint32_t plo = lo + ((T * x) >> 3), phi = lo + ((T * (x + 1)) >> 3);
+            if (g < phi - plo) return plo + g;
+            if (++xoff >= kTailXcds) return kNoChunk;
+            issue(P, lane);
+            g = __builtin_amdgcn_readfirstlane(gv);
+        }
+    }
+};
+
 // Persistent kernel: G resident workgroups (host-chosen); each wave walks its 64-frame chunks (wave_range), so
 // per-workgroup state lives across chunks: the verdict histogram and, in kFlowLds mode, a packed-u16 per-flow
 // histogram in LDS (flow f -> half f & 1 of word f >> 1; the host caps tiles per workgroup at 255 so a half never
@@ -1173,6 +1216,10 @@ void dk_rx_kernel(RxParams P) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t wv = tid >> 6;
+    // the dynamic tail (staged kernel, round-robin schedule): zero the counters the stream's next tail launch uses
+    const bool dyn = kStage && P.tail_ctr != nullptr;
+    if (dyn && blockIdx.x == 0 && tid < kTailXcds)
+        __hip_atomic_store(P.tail_next + tid * kTailStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     DK_STAMPW_RT(12);
     DK_STAMPW(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
@@ -1186,6 +1233,8 @@ void dk_rx_kernel(RxParams P) {
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     StgRec<false> stg[kStage ? kStageK : 1];
     uint32_t nstg = 0;  // wave-uniform
+    TailQ Q{0, 0};
+    const uint32_t ks = dyn ? P.tail_ks : ~0u;  // chunks from round ks on come from the tail (host: ks >= 2)
     uint32_t c, lim, nc, nlim;
     bool have = r.chunk(0, c, lim);
     uint32_t noff = 0, nlen = 0;  // descriptors of this wave's next chunk
@@ -1194,16 +1243,25 @@ void dk_rx_kernel(RxParams P) {
         nlen = P.len[c + r.lane_off];
     }
     WaveLds& W = s_wave[wv];
-    uint32_t nchunks = 0;
     for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
-        nchunks = k + 1;
-        const uint32_t i = c + r.lane_off;
+        // The lane id re-materialised per chunk: without this the compiler keeps ~20 lane-derived address constants
+        // of phases A-C in VGPRs across the whole loop, and this kernel sits at its 168-VGPR budget (3 waves/SIMD).
+        uint32_t lane = lane_id();
+        asm volatile("" : "+v"(lane));
+        const uint32_t i = c + lane;
         const bool live = i < lim;
         const uint32_t off = noff, len = nlen;
-        have = r.chunk(k + 1, nc, nlim);
-        if (have && nc + r.lane_off < nlim) {  // prefetch the next chunk's descriptors
-            noff = P.off[nc + r.lane_off];
-            nlen = P.len[nc + r.lane_off];
+        if (k + 1 < ks) {
+            have = r.chunk(k + 1, nc, nlim);
+        } else {  // the tail: the chunk grabbed a round ago
+            const uint32_t j = Q.resolve(P, lane);
+            have = j != kNoChunk;
+            nc = 64 * j;
+            nlim = P.n;
+        }
+        if (have && nc + lane < nlim) {  // prefetch the next chunk's descriptors
+            noff = P.off[nc + lane];
+            nlen = P.len[nc + lane];
         }
         uint32_t v, fid;
         Rec rec;
@@ -1212,6 +1270,10 @@ void dk_rx_kernel(RxParams P) {
         if (k < 3) DK_STAMPW(2 + 3 * k);
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
+        // the grab for chunk k + 2, resolved at the top of the next round: issued after the frame stream (its return
+        // register would be live through the stream's load registers, the kernel's register peak); phase C covers
+        // its latency
+        if (have && k + 2 >= ks) Q.issue(P, lane);
         if (k < 3) DK_STAMPW(3 + 3 * k);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (k < 3) DK_STAMPW(4 + 3 * k);
@@ -1220,8 +1282,9 @@ void dk_rx_kernel(RxParams P) {
         asm volatile("" ::"v"(noff), "v"(nlen));
         if (kStage) {  // the last kStageK chunks' results; stored when full and at exit
             stage_put(stg, rec);
+            if (lane == 0) W.cb[nstg] = c;
             if (++nstg == kStageK) {
-                flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, k);
+                flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, W.cb, lane);
                 nstg = 0;
             }
         }
@@ -1229,7 +1292,7 @@ void dk_rx_kernel(RxParams P) {
     }
 
     DK_STAMPW(11);
-    if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, r, nchunks - 1);
+    if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, W.cb, lane);
     combine_pending_tail(P, lane, kWaves);  // a previous launch's deferred counter rows, in this wave's tail
     DK_STAMPW(14);
     __syncthreads();

@@ -130,6 +130,53 @@ def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid, record):
     assert ("dst_ip" in got) == (sched != "1") and ("tcp_seq" in got) == (record == "libos")
 
 
+@pytest.mark.parametrize("grid", ["7", "40"])
+@pytest.mark.parametrize("tail", ["0", "1", "2", "4", "12"])
+def test_staged_dynamic_tail(torch_cuda, monkeypatch, capfd, tail, grid):
+    """The staged kernel's dynamic tail (rx_common.h kTailXcds): the last rounds of chunks handed out by per-XCD
+    counters. Every depth from off (0) to most of the batch grabbed (12), on grids of 7 and 40 workgroups (many chunks
+    per wave, pools emptied, then the other XCDs' pools drained), IMIX with a corrupted tail, 16-byte aligned and at
+    2 mod 16. Four launches back to back on one stream and engine (the two counter sets alternate, each launch zeroing
+    the next one's), the second and third with deferred counters; every launch's results and counters bit-exact vs
+    the oracle. The debug line shows the round-robin rounds the host chose."""
+    import torch
+
+    monkeypatch.setenv("DK_RX_SMALL", "0")
+    monkeypatch.setenv("DK_RX_STAGE", "1")
+    monkeypatch.setenv("DK_RX_SPLIT", "0")
+    monkeypatch.setenv("DK_RX_TAIL", tail)
+    monkeypatch.setenv("DK_RX_GRID", grid)
+    monkeypatch.setenv("DK_RX_DEBUG", "1")
+    n = 60000
+    flows = np.concatenate([synth.make_flows(300), synth.make_flows(20, kind="udp")])
+    tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=44), flows, seed=45)
+    for misalign in (None, [2]):
+        blob, off, lens = synth.build_numpy(tr)
+        if misalign:
+            blob = np.concatenate([np.zeros(2, np.uint8), blob])
+            off = off + 2
+        synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
+        exp = run_oracle(blob, off, lens, flows)
+        eng = RxEngine(Config(LOCAL), device=0)
+        eng.set_sockets(flows)
+        b = FrameBatch.from_numpy(blob, off, lens, device=0)
+        rs = [eng.results(n) for _ in range(4)]
+        for k, r in enumerate(rs):
+            eng.receive_batch(b, r, defer_counts=k in (1, 2))
+        torch.cuda.synchronize()
+        for k, r in enumerate(rs):
+            assert_same(r.to_numpy(), exp, f"tail={tail} grid={grid} misalign={misalign} launch {k}")
+        eng.close()
+    ks = [int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("tail_ks=")]
+    assert len(ks) == 8, ks
+    nwaves, nchunk = 4 * int(grid), (n + 63) // 64
+    per, d = nchunk // nwaves, int(tail)
+    want = per + 1 - d if d > 0 and per + 1 >= d + 2 else 0
+    assert ks == [want] * 8, (ks, want)
+    if tail == "2" and grid == "7":
+        assert want > 0
+
+
 @pytest.mark.parametrize("family", ["staged", "unstaged"])
 @pytest.mark.parametrize("align", [64, 16, 4, 2])
 def test_packed_layouts(torch_cuda, monkeypatch, family, align):

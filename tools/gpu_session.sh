@@ -16,9 +16,11 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05a: the new GPU tests (tests.rs IPv4 vectors + UDP KAT through the HIP path, the 1 GiB-window TCP stream, the
-# two-rank bench line's scaling fields), then the default bench line
-step refvec 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k reference
-step newtests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_tcp.py::test_one_stream_gigabyte_window tests/test_gpu_multiproc.py
-step bench 600 python bench.py
+# r05b: the staged kernel's dynamic tail — parity first, then the IMIX A/B over tail depths (2 rotating batches,
+# deferred counters as the bench runs them), then per-wave exit timelines with and without the tail
+step parity 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "dynamic_tail or kernel_variants or full_size_c4 or packed_layouts or deferred or golden"
+step ab_imix 600 python tools/tune_ab.py --workload c4_imix --rotate 2 --reps 7 --iters 20 "defer=1,tail=0" "defer=1,tail=1" "defer=1,tail=2" "defer=1,tail=3" "defer=1,tail=4"
+step ab_imix1 600 python tools/tune_ab.py --workload c4_imix --rotate 1 --reps 5 --iters 20 "defer=1,tail=0" "defer=1,tail=2"
+step stamps 600 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail=0
+step stamps_t2 600 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail=2
 echo done

@@ -2,7 +2,7 @@
 """Per-wave timeline of the staged receive kernel (dk_rx_kernel) from a -DDK_DIAG_STAMPS build (tuning tool).
 
     python tools/stamps_staged.py build/variants/stamps.so [--workload c1_tcp1078] [--rotate 3]
-Stamps per wave (s_memtime unless noted): 0 entry, 1 after the LDS init / table copy / barrier, per chunk k < 3:
+--tuning tail=0 etc. sets dk_diag_rx_set_tuning knobs. Stamps per wave (s_memtime unless noted): 0 entry, 1 after the LDS init / table copy / barrier, per chunk k < 3:
 2+3k before phase A+B, 3+3k after it, 4+3k after phase C; 11 after the loop, 14 after the staged flush and the pending
 combine, 15 after the barrier and the counter rows; 12/13 s_memrealtime at entry/exit. Prints quantiles (µs)."""
 import argparse
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--workload", default="c1_tcp1078")
     ap.add_argument("--rotate", type=int, default=3)
+    ap.add_argument("--tuning", default="", help="dk_diag_rx_set_tuning knobs, e.g. tail=0")
     args = ap.parse_args()
     import torch
 
@@ -32,6 +33,8 @@ def main():
     made = [bench.make_batch(e, args.workload, 0, synth.SEED + 1000 * k, 1) for k in range(args.rotate)]
     rot = [m[0] for m in made]
     e.set_sockets(made[0][1])
+    if args.tuning:
+        e.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in args.tuning.split(","))})
     r = e.results(rot[0].n)
     lib = e.lib
     lib.dk_diag_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
@@ -53,7 +56,10 @@ def main():
         mhz = float(np.median((st[:, 15] - st[:, 0]) / np.maximum(st[:, 13] - st[:, 12], 1) * 100.0))
         us = lambda x: x / mhz  # noqa: E731
         row = {"waves": len(st), "mhz": round(mhz, 1), "start": q((st[:, 12] - t0) * 0.01),
-               "exit": q((st[:, 13] - t0) * 0.01), "setup": q(us(st[:, 1] - st[:, 0]))}
+               "exit": q((st[:, 13] - t0) * 0.01), "setup": q(us(st[:, 1] - st[:, 0])),
+               "exit_spread_us": round(float(st[:, 13].max() - st[:, 13].min()) * 0.01, 2),
+               "exit_p10_to_max_us": round(float(st[:, 13].max() - np.percentile(st[:, 13], 10)) * 0.01, 2),
+               "tuning": args.tuning}
         for k in range(3):
             have = st[:, 2 + 3 * k] != 0
             if not have.any():
