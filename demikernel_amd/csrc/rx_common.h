@@ -106,9 +106,8 @@ struct RowCombine {
 // rounds stay round-robin (chunk j = wave + k * nwaves: the grid sweeps the blob in address order); the remaining
 // chunks are split into kTailXcds pools handed out by one counter per pool, each counter on its own 256-byte span (one
 // shared line serialises every grab at one memory channel, round 4: +42 %). A wave grabs from the pool of its XCD
-// (HW_REG_XCC_ID), then from the others once that is empty; each grab is issued a chunk before its descriptors are
-// needed, so its latency is hidden. A launch zeroes the counter set the stream's next tail launch will use (two sets
-// per stream slot, alternating).
+// (HW_REG_XCC_ID) only; each grab is issued a chunk before its descriptors are needed, so its latency is hidden. A
+// launch zeroes the counter set the stream's next tail launch will use (two sets per stream slot, alternating).
 constexpr uint32_t kTailXcds = 8;
 constexpr uint32_t kTailStride = 64;  // words between counters
 constexpr uint32_t kTailSetWords = kTailXcds * kTailStride;

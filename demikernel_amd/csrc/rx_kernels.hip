@@ -1165,36 +1165,31 @@ __device__ __forceinline__ void combine_pending_tail(const RxParams& P, uint32_t
 // kTailXcds pools [lo + T x / 8, lo + T (x + 1) / 8), pool x handed out by counter x. Wave-uniform state; lane 0 issues
 // the grabs (one returning device-scope atomic each) and readfirstlane broadcasts the old counter value.
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
-// Live state is kept to two registers (the kernel is at its VGPR budget): xoff, the pools found empty so far (the pool
-// grabbed from is (XCC id + xoff) mod 8, the id re-read from the hardware register), and gv, lane 0's pending grab;
-// the counter set and the tail range are re-read from the kernel arguments (kargs) where they are used.
+// A wave grabs only from its own XCD's pool: every XCD runs the same number of waves over a pool of the same size.
+// (Stealing from the other pools once the own one was empty cost every wave up to seven dependent atomic round trips
+// at its very end, where nothing hides them: IMIX 141.8 -> 160.8 us, session r05b.) The grab that finds the pool
+// empty was issued a chunk earlier, so ending costs nothing. Live state: gv, lane 0's pending grab; the pool
+// (HW_REG_XCC_ID), the counter set and the tail range are re-read where used (the kernel is at its VGPR budget).
 struct TailQ {
-    uint32_t xoff;  // wave-uniform
-    uint32_t gv;    // lane 0: the pending grab's counter value
-    __device__ __forceinline__ static uint32_t pool(uint32_t xoff) {
+    uint32_t gv;  // lane 0: the pending grab's counter value
+    __device__ __forceinline__ static uint32_t pool() {
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        return (xcc + xoff) & (kTailXcds - 1);
+        return xcc & (kTailXcds - 1);
     }
     __device__ __forceinline__ void issue(const RxParams& P, uint32_t lane) {
         uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(kargs(P).tail_ctr + pool(xoff) * kTailStride, 1u);
+        if (lane == 0) g = atomicAdd(kargs(P).tail_ctr + pool() * kTailStride, 1u);
         gv = g;
     }
-    // The chunk the pending grab got, or kNoChunk once every pool is empty (grabbing from the next pools on the way).
-    __device__ __forceinline__ uint32_t resolve(const RxParams& P, uint32_t lane) {
+    // The chunk the pending grab got, or kNoChunk once the pool is empty.
+    __device__ __forceinline__ uint32_t resolve(const RxParams& P) const {
         const RxParams& K = kargs(P);
         const uint32_t lo = K.tail_ks * gridDim.x * kWaves, nchunk = (K.n + 63) / 64;
         const uint32_t T = nchunk > lo ? nchunk - lo : 0u;
-        uint32_t g = __builtin_amdgcn_readfirstlane(gv);
-        for (;;) {
-            const uint32_t x = pool(xoff);
-            const uint32_t plo = lo + ((T * x) >> 3), phi = lo + ((T * (x + 1)) >> 3);
-            if (g < phi - plo) return plo + g;
-            if (++xoff >= kTailXcds) return kNoChunk;
-            issue(P, lane);
-            g = __builtin_amdgcn_readfirstlane(gv);
-        }
+        const uint32_t g = __builtin_amdgcn_readfirstlane(gv), x = pool();
+        const uint32_t plo = lo + ((T * x) >> 3), phi = lo + ((T * (x + 1)) >> 3);
+        return g < phi - plo ? plo + g : kNoChunk;
     }
 };
 
@@ -1233,7 +1228,7 @@ void dk_rx_kernel(RxParams P) {
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
     StgRec<false> stg[kStage ? kStageK : 1];
     uint32_t nstg = 0;  // wave-uniform
-    TailQ Q{0, 0};
+    TailQ Q{0};
     const uint32_t ks = dyn ? P.tail_ks : ~0u;  // chunks from round ks on come from the tail (host: ks >= 2)
     uint32_t c, lim, nc, nlim;
     bool have = r.chunk(0, c, lim);
@@ -1254,7 +1249,7 @@ void dk_rx_kernel(RxParams P) {
         if (k + 1 < ks) {
             have = r.chunk(k + 1, nc, nlim);
         } else {  // the tail: the chunk grabbed a round ago
-            const uint32_t j = Q.resolve(P, lane);
+            const uint32_t j = Q.resolve(P);
             have = j != kNoChunk;
             nc = 64 * j;
             nlim = P.n;

@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05b: the staged kernel's dynamic tail — parity first, then the IMIX A/B over tail depths (2 rotating batches,
+# r05c: the dynamic tail without stealing (own-XCD pool only)
 # deferred counters as the bench runs them), then per-wave exit timelines with and without the tail
 step parity 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "dynamic_tail or kernel_variants or full_size_c4 or packed_layouts or deferred or golden"
 step ab_imix 600 python tools/tune_ab.py --workload c4_imix --rotate 2 --reps 7 --iters 20 "defer=1,tail=0" "defer=1,tail=1" "defer=1,tail=2" "defer=1,tail=3" "defer=1,tail=4"
