@@ -104,10 +104,11 @@ struct RowCombine {
 // Dynamic tail of the staged kernel (round 5). With round-robin chunks a wave's chunk count is fixed and its chunks'
 // sizes are random (IMIX), so the waves finish over ~25 us and the launch waits for the slowest. The first tail_ks
 // rounds stay round-robin (chunk j = wave + k * nwaves: the grid sweeps the blob in address order); the remaining
-// chunks are split into kTailXcds pools handed out by one counter per pool, each counter on its own 256-byte span (one
-// shared line serialises every grab at one memory channel, round 4: +42 %). A wave grabs from the pool of its XCD
-// (HW_REG_XCC_ID) only; each grab is issued a chunk before its descriptors are needed, so its latency is hidden. A
-// launch zeroes the counter set the stream's next tail launch will use (two sets per stream slot, alternating).
+// chunks are split into tail_pools (<= kTailXcds) pools, one per group of workgroups that share an XCD, handed out by
+// one counter per pool, each on its own 256-byte span (one shared line serialises every grab at one memory channel,
+// round 4: +42 %). A wave grabs from its own pool only; each grab is issued a chunk before its descriptors are
+// needed, so its latency is hidden. A launch zeroes the counter set the stream's next tail launch will use (two sets
+// per stream slot, alternating).
 constexpr uint32_t kTailXcds = 8;
 constexpr uint32_t kTailStride = 64;  // words between counters
 constexpr uint32_t kTailSetWords = kTailXcds * kTailStride;
@@ -147,6 +148,7 @@ struct RxParams {
     uint32_t small;          // launch the small-frame kernel (minimum-size frames)
     uint32_t defer_rows;     // leave this launch's counter rows pending (no dk_flow_reduce_kernel after it)
     uint32_t tail_ks;        // staged kernel: round-robin rounds per wave before the dynamic tail (0: none)
+    uint32_t tail_pools;     // pools of the tail (8, 4, 2 or 1: divides the grid); workgroup b grabs from b mod this
     uint32_t* tail_ctr;      // this launch's kTailXcds grab counters (zero at launch), nullptr: no dynamic tail
     uint32_t* tail_next;     // the counter set the stream's next tail launch uses: zeroed by this launch
     RowCombine comb;         // a previous launch's pending rows, combined in this launch

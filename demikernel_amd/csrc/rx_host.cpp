@@ -334,12 +334,14 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     // first per + 1 - d stay round-robin and the rest (d - 1 rounds + the partial one) are grabbed from per-XCD
     // counters; at least 2 round-robin rounds (the first grab is issued during round ks - 2).
     p.tail_ks = 0;
+    p.tail_pools = 1;
     p.tail_ctr = p.tail_next = nullptr;
     const int32_t tail_d = T.tail >= 0 ? T.tail : 2;
     if (family == dk::kFamilyStaged && p.sched == 0 && tail_d > 0) {
         const uint32_t nwaves = grid * 4u, nchunk = (p.n + 63) / 64;
         const uint32_t per = nchunk / nwaves;
         if (per + 1 >= (uint32_t)tail_d + 2) p.tail_ks = per + 1 - (uint32_t)tail_d;
+        p.tail_pools = grid % 8 == 0 ? 8u : grid % 4 == 0 ? 4u : grid % 2 == 0 ? 2u : 1u;
     }
     // Per-workgroup histogram rows (flow pairs, then verdicts; dk_flow_reduce_kernel adds them up, or the next launch
     // on the stream when this one defers them) and the small-frame kernel's deferral masks: a launch that needs either,

@@ -1165,30 +1165,30 @@ __device__ __forceinline__ void combine_pending_tail(const RxParams& P, uint32_t
 // kTailXcds pools [lo + T x / 8, lo + T (x + 1) / 8), pool x handed out by counter x. Wave-uniform state; lane 0 issues
 // the grabs (one returning device-scope atomic each) and readfirstlane broadcasts the old counter value.
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
-// A wave grabs only from its own XCD's pool: every XCD runs the same number of waves over a pool of the same size.
-// (Stealing from the other pools once the own one was empty cost every wave up to seven dependent atomic round trips
-// at its very end, where nothing hides them: IMIX 141.8 -> 160.8 us, session r05b.) The grab that finds the pool
-// empty was issued a chunk earlier, so ending costs nothing. Live state: gv, lane 0's pending grab; the pool
-// (HW_REG_XCC_ID), the counter set and the tail range are re-read where used (the kernel is at its VGPR budget).
+// Pools are keyed by blockIdx.x mod tail_pools (the host takes the largest of 8, 4, 2, 1 that divides the grid, so every
+// pool has the same number of waves): workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md: dispatch deals blocks
+// round-robin over the 8 XCDs), so with 8 pools each pool's counter is grabbed from one XCD — a speed property only;
+// correctness needs just that every pool's waves drain it. A wave grabs only from its own pool (stealing from the
+// other pools once the own one was empty cost every wave up to seven dependent atomic round trips at its very end,
+// where nothing hides them: IMIX 141.8 -> 160.8 us, session r05b). The grab that finds the pool empty was issued a
+// chunk earlier, so ending costs nothing. Live state: gv, lane 0's pending grab; the pool, the counter set and the
+// tail range are re-read where used (the kernel is at its VGPR budget).
 struct TailQ {
     uint32_t gv;  // lane 0: the pending grab's counter value
-    __device__ __forceinline__ static uint32_t pool() {
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        return xcc & (kTailXcds - 1);
-    }
     __device__ __forceinline__ void issue(const RxParams& P, uint32_t lane) {
+        const RxParams& K = kargs(P);
         uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(kargs(P).tail_ctr + pool() * kTailStride, 1u);
+        if (lane == 0) g = atomicAdd(K.tail_ctr + (blockIdx.x & (K.tail_pools - 1)) * kTailStride, 1u);
         gv = g;
     }
     // The chunk the pending grab got, or kNoChunk once the pool is empty.
     __device__ __forceinline__ uint32_t resolve(const RxParams& P) const {
         const RxParams& K = kargs(P);
         const uint32_t lo = K.tail_ks * gridDim.x * kWaves, nchunk = (K.n + 63) / 64;
-        const uint32_t T = nchunk > lo ? nchunk - lo : 0u;
-        const uint32_t g = __builtin_amdgcn_readfirstlane(gv), x = pool();
-        const uint32_t plo = lo + ((T * x) >> 3), phi = lo + ((T * (x + 1)) >> 3);
+        const uint32_t T = nchunk > lo ? nchunk - lo : 0u, x = blockIdx.x & (K.tail_pools - 1);
+        const uint32_t sh = 31u - (uint32_t)__builtin_clz(K.tail_pools);  // pools: a power of two
+        const uint32_t g = __builtin_amdgcn_readfirstlane(gv);
+        const uint32_t plo = lo + ((T * x) >> sh), phi = lo + ((T * (x + 1)) >> sh);
         return g < phi - plo ? plo + g : kNoChunk;
     }
 };
