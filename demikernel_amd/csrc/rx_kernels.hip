@@ -1601,15 +1601,19 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
     uint64_t had = 0;
     for (uint32_t k = 0; have; k++) {
-        const uint32_t i = c + r.lane_off;
+        // the lane id re-materialised per chunk (as in dk_rx_kernel): lane-derived constants are not held in VGPRs
+        // across the loop
+        uint32_t lane = lane_id();
+        asm volatile("" : "+v"(lane));
+        const uint32_t i = c + lane;
         const bool live = i < lim;
         const bool have2 = have1 && r.chunk(k + 2, c2, lim2);
         uint32_t off2 = 0, len2 = 0;
-        if (have2 && c2 + r.lane_off < lim2) {  // descriptors two chunks ahead, before this chunk's window DMA
-            off2 = P.off[c2 + r.lane_off];
-            len2 = P.len[c2 + r.lane_off];
+        if (have2 && c2 + lane < lim2) {  // descriptors two chunks ahead, before this chunk's window DMA
+            off2 = P.off[c2 + lane];
+            len2 = P.len[c2 + lane];
         }
-        const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + r.lane_off < lim1, off1, len1);
+        const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + lane < lim1, off1, len1);
         uint32_t v, fid;
         if (k == 0) DK_STAMP(1);
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);

@@ -16,11 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05c: the dynamic tail without stealing (own-XCD pool only)
-# deferred counters as the bench runs them), then per-wave exit timelines with and without the tail
-step parity 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "dynamic_tail or kernel_variants or full_size_c4 or packed_layouts or deferred or golden"
-step ab_imix 600 python tools/tune_ab.py --workload c4_imix --rotate 2 --reps 7 --iters 20 "defer=1,tail=0" "defer=1,tail=1" "defer=1,tail=2" "defer=1,tail=3" "defer=1,tail=4"
-step ab_imix1 600 python tools/tune_ab.py --workload c4_imix --rotate 1 --reps 5 --iters 20 "defer=1,tail=0" "defer=1,tail=2"
-step stamps 600 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail=0
-step stamps_t2 600 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail=2
+# r05e: small-frame kernel with the lane id re-materialised per chunk (89 -> 80 VGPRs fit 6 waves/SIMD without
+# spills): parity of the 6-wave build, then C3 A/B 5 vs 6 waves (8 rotating batches, deferred counters)
+step parity6 600 python tools/variant_parity.py --lib build/variants/sm6.so
+step ab_c3 600 python tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/sm6.so "defer=1"
+step ab_c3r 600 python tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 7 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/sm6.so "defer=1"
 echo done
