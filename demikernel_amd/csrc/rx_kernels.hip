@@ -1354,7 +1354,9 @@ __device__ __forceinline__ WinPlan small_window_issue(const FrameDesc<kShift>& F
     if (hi > lo && hi - lo <= kGran * 16 && !__ballot(live && !inwin)) {
         const uint32_t G = (hi - lo + 15) >> 4;  // wave-uniform
         const uint32_t sl = win_slot(lane);  // the granule this lane's slot holds (slots 64 k + lane)
-        for (uint32_t k = 0; k * 64 < G; k++) {
+#pragma unroll
+        for (uint32_t k = 0; k < kWinLoads; k++) {  // unrolled: no loop counters, uniform branches per piece
+            if (k * 64 >= G) break;
             const uint32_t g = 64 * k + sl;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(B.rs, (lds_void*)&W.win[64 * k], 16, g < G ? lo + 16 * g : kOob,
                                                      0, 0, DK_NT_LOADS ? 2 : 0);
@@ -1556,7 +1558,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = lane_id();
-    const uint32_t wv = tid >> 6;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS bases (DMA m0) in SGPRs
     DK_STAMP_RT(12);
     DK_STAMP(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
