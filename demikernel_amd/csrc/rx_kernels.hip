@@ -1317,7 +1317,9 @@ struct SmallLds {
     uint4 win[kWinLoads * 64];   // the chunk's frame window (whole 1 KiB DMA pieces)
 };
 #ifndef DK_MIN_WAVES_SMALL
-#define DK_MIN_WAVES_SMALL 5  // 96 VGPRs: no spills (6 waves spilled 16-22 VGPRs to scratch: C3 +11 %)
+#define DK_MIN_WAVES_SMALL 6  // 80 VGPRs, no spills since round 5 (lane id re-materialised per chunk, uniform wave
+                              // index): C3 -3.9 % vs 5 waves, random ports +0.8 % (session r05f). Before, 6 waves
+                              // spilled 16-22 VGPRs to scratch (C3 +11 %, round 3).
 #endif
 #ifndef DK_SMALL_WAVES
 #define DK_SMALL_WAVES 4  // waves per workgroup of the small-frame kernel
