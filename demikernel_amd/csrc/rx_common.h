@@ -146,6 +146,7 @@ struct RxParams {
     uint32_t stage;          // launch the instantiation that stages result stores in registers (large frames)
     uint32_t split;          // launch the split (stream waves / finish waves) kernel (large frames)
     uint32_t small;          // launch the small-frame kernel (minimum-size frames)
+    uint32_t small_kmin;     // small-frame kernel: whole chunks per wave (ceil(n / 64) / waves of the grid)
     uint32_t defer_rows;     // leave this launch's counter rows pending (no dk_flow_reduce_kernel after it)
     uint32_t tail_ks;        // staged kernel: round-robin rounds per wave before the dynamic tail (0: none)
     uint32_t tail_pools;     // pools of the tail (8, 4, 2 or 1: divides the grid); workgroup b grabs from b mod this

@@ -330,6 +330,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
+    p.small_kmin = p.small ? ((p.n + 63) / 64) / (grid * dk_rx_small_block_waves()) : 0u;
     // The staged kernel's dynamic tail (rx_common.h): with `per` whole round-robin rounds of chunks per wave, the
     // first per + 1 - d stay round-robin and the rest (d - 1 rounds + the partial one) are grabbed from per-XCD
     // counters; at least 2 round-robin rounds (the first grab is issued during round ks - 2).

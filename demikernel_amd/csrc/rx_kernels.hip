@@ -1054,6 +1054,13 @@ __device__ __forceinline__ void flush_staged(const RxParams& P, const StgRec<fal
 // one each. One elephant flow (the tcp-echo shape, C1) is then one LDS add per chunk instead of 64 serialised adds on
 // one LDS word; many flows (C2, C5) pay one extra round.
 constexpr uint32_t kFlowAggMin = 4;
+// A value the compiler must treat as lane-varying. Atomics whose address it can prove uniform get the LLVM atomic
+// optimizer's expansion (exec save, mbcnt, a one-lane re-issue: ~10 instructions each) even where a single lane already
+// issues them, as the leader-lane adds below do.
+__device__ __forceinline__ uint32_t opaque_v(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 __device__ __forceinline__ void flow_add(const RxParams& P, bool lds_flows, uint32_t* s_flow, uint32_t fid,
                                          uint32_t cnt) {
     if (lds_flows) atomicAdd(&s_flow[fid >> 1], cnt << ((fid & 1u) * 16));
@@ -1068,7 +1075,7 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
         const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
         const uint32_t f0 = __builtin_amdgcn_readlane(fid, leader);
         const uint64_t m = __ballot(fid == f0) & todo;
-        if (lane == leader) flow_add(P, lds_flows, s_flow, f0, (uint32_t)__popcll(m));
+        if (lane == leader) flow_add(P, lds_flows, s_flow, opaque_v(f0), opaque_v((uint32_t)__popcll(m)));
         todo &= ~m;
         if (__popcll(m) < kFlowAggMin) break;
     }
@@ -1079,7 +1086,7 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
             const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
             const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
             const uint64_t m = __ballot(live && v == v0);
-            if (lane == leader) atomicAdd(&s_vh[v0], (uint32_t)__popcll(m));
+            if (lane == leader) atomicAdd(&s_vh[opaque_v(v0)], opaque_v((uint32_t)__popcll(m)));
             todo &= ~m;
         }
     }
@@ -1474,58 +1481,66 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
         L.v = kNone;
         L.need = 0;
     }
-    // first socket-table load before the checksum arithmetic (as rx_front)
+    // Branch-free for the common frame (round 5): every lane computes the ICMP verdict, the T4 / U3 checksum compare
+    // and the first-slot demux, and selects; only the rare second steps (a TCP probe walk past a taken slot, the
+    // Passive / 0.0.0.0 lookup after a miss) are wave-uniform branches. (The if / else-if chain of rx_back cost the
+    // wave ~60 SALU per chunk in exec-mask bookkeeping, taken or not.)
+    const bool tcp = L.v == kPendTcp, udp = L.v == kPendUdp, icmp = L.v == kPendIcmp;
+    const uint32_t dport = L.ports >> 16;
+    // One table load per lane before the checksum arithmetic: TCP the hashed Active slot, UDP the 16 bytes of the port
+    // table holding (local_ip, dport)'s word (the port table starts 16-byte aligned, after the Active slots), other
+    // lanes the table's first slot (loaded, unused).
     const ProbeKey k1{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)};
-    uint32_t h1 = 0;
-    uint4 s1 = make_uint4(0, 0, 0, 0);
-    if (L.v == kPendTcp) {
-        h1 = probe_slot(P, k1);
-        s1 = reinterpret_cast<const uint4*>(P.table)[h1];
-    }
-    if (L.v == kPendUdp) s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
-    uint32_t lsum = 0;
-    if (L.need) {  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
-        if (!__ballot(L.E != 64u)) {
-            lsum = hsum2(R.w[8] & 0xFFFF0000u, 0);
+    const uint32_t h1 = tcp ? probe_slot(P, k1) : 0u;
+    const uint4* T4 = reinterpret_cast<const uint4*>(P.table);
+    const uint4* U4 = reinterpret_cast<const uint4*>(P.port_tab + kPortUdpLocal);
+    const uint4 s1 = *(tcp ? T4 + h1 : udp ? U4 + (dport >> 2) : T4);
+    uint32_t lsum;  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
+    if (!__ballot(L.need && L.E != 64u)) {
+        lsum = hsum2(R.w[8] & 0xFFFF0000u, 0);
 #pragma unroll
-            for (int k = 9; k < 16; k++) lsum = hsum2(R.w[k], lsum);
-        } else {
-            const int t = 32 - 8 * (int)L.E;
+        for (int k = 9; k < 16; k++) lsum = hsum2(R.w[k], lsum);
+    } else {
+        const int t = 32 - 8 * (int)L.E;
+        lsum = 0;
 #pragma unroll
-            for (int k = 8; k < 16; k++) {
-                const uint32_t sh = (uint32_t)min(max(t + 32 * k, 0), 32);
-                uint32_t m = (uint32_t)(0xFFFFFFFFull >> sh);
-                if (k == 8) m &= 0xFFFF0000u;
-                lsum = hsum2(R.w[k] & m, lsum);
-            }
+        for (int k = 8; k < 16; k++) {
+            const uint32_t sh = (uint32_t)min(max(t + 32 * k, 0), 32);
+            uint32_t m = (uint32_t)(0xFFFFFFFFull >> sh);
+            if (k == 8) m &= 0xFFFF0000u;
+            lsum = hsum2(R.w[k] & m, lsum);
         }
     }
-    uint32_t fid = DK_FLOW_NONE;
-    if (L.v == kPendIcmp) {  // as rx_back (icmpv4/header.rs:55-57, protocol.rs:37-56)
-        const uint32_t type = (L.mhi >> 8) & 0xFFu;
-        L.v = mod_ffff(lsum) != 0 ? (uint32_t)DK_V_ICMP_CSUM
-              : (type < 15 && ((kIcmpTypes >> type) & 1u)) ? (uint32_t)DK_V_ICMP : (uint32_t)DK_V_ICMP_TYPE;
-    } else if (L.v == kPendTcp || L.v == kPendUdp) {
-        const bool tcp = L.v == kPendTcp;
-        if (L.need) {  // T4 / U3 (tcp/header.rs:203-207, udp/header.rs:78-88)
-            const uint32_t sm = lsum - bswap16(L.stored);
-            const uint32_t lip = P.local_ip;
-            const uint32_t pseudo = bswap16(L.src & 0xFFFFu) + bswap16(L.src >> 16) + bswap16(lip & 0xFFFFu) +
-                                    bswap16(lip >> 16) + (tcp ? 6u : 17u) + (L.E - L.S);
-            if (csum_from_residue(mod_ffff(be_residue(sm) + pseudo)) != L.stored)
-                L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
-        }
-        const uint32_t dport = L.ports >> 16;
-        if (L.v == kPendTcp) {  // Active(local, remote), then Passive(local) (tcp/peer.rs:241-251)
-            fid = probe_finish(P, k1, h1, s1);
-            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortTcpPassive, dport);
-            L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
-        } else if (L.v == kPendUdp) {  // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
-            fid = s1.x;
-            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortUdpAny, dport);
-            L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
-        }
-    }
+    // ICMPv4 (as rx_back: icmpv4/header.rs:55-57, protocol.rs:37-56)
+    const uint32_t type = (L.mhi >> 8) & 0xFFu;
+    const uint32_t vicmp = mod_ffff(lsum) != 0 ? (uint32_t)DK_V_ICMP_CSUM
+                           : (type < 15 && ((kIcmpTypes >> type) & 1u)) ? (uint32_t)DK_V_ICMP : (uint32_t)DK_V_ICMP_TYPE;
+    // T4 / U3 (tcp/header.rs:203-207, udp/header.rs:78-88): the stored field summed as zero, pseudo-header with the
+    // configured local address
+    const uint32_t sm = lsum - bswap16(L.stored);
+    const uint32_t lip = P.local_ip;
+    const uint32_t pseudo = bswap16(L.src & 0xFFFFu) + bswap16(L.src >> 16) + bswap16(lip & 0xFFFFu) +
+                            bswap16(lip >> 16) + (tcp ? 6u : 17u) + (L.E - L.S);
+    const bool bad = L.need && csum_from_residue(mod_ffff(be_residue(sm) + pseudo)) != L.stored;
+    // demux, first step: Active(local, remote) in the first slot (tcp/peer.rs:241-251), (local_ip, dport) for UDP
+    // (udp/peer.rs:147-165)
+    const uint32_t uw = (dport & 2u) ? ((dport & 1u) ? s1.w : s1.z) : ((dport & 1u) ? s1.y : s1.x);
+    const bool hit = s1.x != 0 && (s1.x >> 24) == k1.kind && s1.y == k1.lip && s1.z == k1.rip && s1.w == k1.lport_rport;
+    const bool l4 = (tcp || udp) && !bad;
+    uint32_t fid = !l4 ? DK_FLOW_NONE : tcp ? (hit ? s1.x & 0xFFFFFFu : DK_FLOW_NONE) : uw;
+    // rare: the Active key further along its probe sequence (the first slot taken by another key)
+    const bool walk = l4 && tcp && !hit && s1.x != 0;
+    if (__ballot(walk))
+        if (walk) fid = probe_finish(P, k1, h1, s1);
+    // rare: the second lookup, Passive(local) for TCP, (0.0.0.0, dport) for UDP
+    const bool second = l4 && fid == DK_FLOW_NONE;
+    if (__ballot(second))
+        if (second) fid = port_lookup(P, tcp ? kPortTcpPassive : kPortUdpAny, dport);
+    L.v = icmp ? vicmp
+          : (tcp || udp) ? (bad ? (tcp ? (uint32_t)DK_V_TCP_CSUM : (uint32_t)DK_V_UDP_CSUM)
+                            : fid == DK_FLOW_NONE ? (tcp ? (uint32_t)DK_V_TCP_NOSOCK : (uint32_t)DK_V_UDP_NOSOCK)
+                                                  : (tcp ? (uint32_t)DK_V_OK_TCP : (uint32_t)DK_V_OK_UDP))
+                         : L.v;
     const uint32_t v = L.v;
     if (live) {
         const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;
@@ -1588,8 +1603,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     // -2.1 % together with the first descriptors loaded before the barrier).
     if (DK_SMALL_PRIO) {
         uint32_t cc, ll;
-        const uint32_t kmin = ((P.n + 63) / 64) / (gridDim.x * kSmallWaves);
-        if (r.chunk(kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_SMALL_PRIO);
+        if (r.chunk(P.small_kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_SMALL_PRIO);  // (host: chunks / waves)
     }
     const Blob B(P.frames, P.frames_bytes);
     SmallLds& W = s_wave[wv];

@@ -16,12 +16,11 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05f: small-frame kernel with a uniform wave index and an unrolled window DMA (83 VGPRs at 5 waves/SIMD; 80 at 6):
-# parity of the 6-wave build, C3 A/B 5 vs 6 waves, SQ counter passes of both
-step parity6 600 python tools/variant_parity.py --lib /root/repo/build/variants/sm6.so
-step ab_c3 600 python tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 40 --lib demikernel_amd/libdk_rx.so --lib /root/repo/build/variants/sm6.so "defer=1"
-step ab_c3r 600 python tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 7 --iters 40 --lib demikernel_amd/libdk_rx.so --lib /root/repo/build/variants/sm6.so "defer=1"
-step pmc5 600 bash tools/pmc_kernel.sh c3_udp64 r05f_c3_w5 --rotate 8 --defer
-step pmc6 600 bash tools/pmc_kernel.sh c3_udp64 r05f_c3_w6 --rotate 8 --defer --lib /root/repo/build/variants/sm6.so
-step trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r05f/trace -o run --output-format csv -- python3 tools/kbench.py --workload c3_udp64 --iters 40 --rotate 8 --defer
+# r05h: small_fast branch-free for the common frame + leader-lane atomics without the atomic optimizer's expansion +
+# the priority division on the host: the whole receive parity file, C3 A/B against the previous commit, SQ counters
+step parity 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py
+step ab_c3 600 python tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
+step ab_c3r 600 python tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 7 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
+step ab_imix 600 python tools/tune_ab.py --workload c4_imix --rotate 2 --reps 5 --iters 20 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
+step pmc6 600 bash tools/pmc_kernel.sh c3_udp64 r05h_c3 --rotate 8 --defer
 echo done
