@@ -417,6 +417,7 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 struct CoopSlot {
     uint32_t boff;  // byte offset of the frame's first granule in the blob
     uint32_t nb, j, acc;
+    uint32_t lg;    // granules between the frame's 64-byte line start and its first granule (0..3)
     bool has;
 };
 
@@ -498,9 +499,11 @@ struct FrameDesc {
     uint32_t sh;         // f - a, even (a = granule base)
     uint32_t span;       // bytes from a to the frame end
     uint32_t nblk;       // big frames: granules covering [a, f + len)
+    uint32_t lg;         // a's granule within its 64-byte line (0..3): quarter-wave spans start at the line (coop_issue)
     __device__ __forceinline__ FrameDesc(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t off,
                                          uint32_t len) {
         inb = live && (uint64_t)off + len <= frames_bytes;
+        lg = ((uint32_t)reinterpret_cast<uintptr_t>(frames + off) >> 4) & 3u;
         const uint32_t fmod = (uint32_t)reinterpret_cast<uintptr_t>(frames + off) & 15u;
         sh = kShift ? fmod : 0u;
         vec = inb && (kShift ? (fmod & 1u) == 0 : fmod == 0);
@@ -567,17 +570,19 @@ __device__ __forceinline__ CoopPlan coop_plan(const FrameDesc<kShift>& F, uint32
     pl.nmed = 0;
     pl.maxit = 1;
     if (pl.ncoop == 0) return pl;
-    const bool med = F.big && F.nblk <= kMedGran;
+    // a frame's granules counted from its 64-byte line start (the quarter-wave's loads cover whole lines, below)
+    const uint32_t lspan = F.big ? F.nblk + F.lg : 0u;
+    const bool med = F.big && lspan <= kMedGran;
     const uint64_t mm = __ballot(med), lm = cm & ~mm;
     pl.nmed = (uint32_t)__popcll(mm);
     if (F.big) {
         const uint64_t m = med ? mm : lm;
         const uint32_t rank = (med ? 0u : pl.nmed) +
                               __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        W.rec[rank] = make_uint2(lane | (F.nblk << 8), off - F.sh);  // one ds_read_b64 per round
+        W.rec[rank] = make_uint2(lane | (F.lg << 6) | (F.nblk << 8), off - F.sh);  // one ds_read_b64 per round
     }
-    if (__ballot(F.nblk > kCoopSpan)) {
-        uint32_t mx = F.nblk;
+    if (__ballot(lspan > kCoopSpan)) {
+        uint32_t mx = lspan;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
         pl.maxit = __builtin_amdgcn_readfirstlane((mx - 1) / kCoopSpan + 1);
@@ -599,18 +604,24 @@ __device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r,
             const uint32_t k = k0 + (r + h) * 4 + q;
             S.sl[h].has = k < k1;
             const uint2 rec = S.sl[h].has ? W.rec[k] : make_uint2(0, 0);
-            S.sl[h].j = rec.x & 0xFFu;
+            S.sl[h].j = rec.x & 0x3Fu;
+            S.sl[h].lg = (rec.x >> 6) & 3u;
             S.sl[h].nb = rec.x >> 8;  // 0 for an empty slot: every load is then out of range
             S.sl[h].boff = rec.y;
             S.sl[h].acc = 0;
         }
     }
+    // Granule b of the frame is loaded by lane l16 = (b + lg) mod 16 of load u = (b + lg) / 16 (iteration it): each
+    // load's 16 lanes cover one 256-byte span that starts on a 64-byte line, i.e. 4 whole lines. Spans from the frame's
+    // first granule instead touched 5 lines each for frames at 16-48 mod 64 — the TPACKET_V3 ring's frames at
+    // tp_mac = 82 — and uncached host memory fetched the shared lines twice: 6 x 5 = 30 PCIe line reads for a 1500-byte
+    // frame that spans 24-25 lines. Lanes below lg load at kOob (zeros, no access).
     const uint32_t b0 = it * 16 * U + l16;
 #pragma unroll
     for (uint32_t h = 0; h < R; h++)
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
-            const uint32_t b = b0 + 16 * u;
+            const uint32_t b = b0 + 16 * u - S.sl[h].lg;  // wraps below the frame: out of range
             // kHdrT (the TX kernels): each frame's first 16 granules (its first 256 bytes, u = 0) with the default
             // policy instead of nontemporal, so the header-window rewrite finds its line in L2 (TX C2 -3 %; the
             // receive kernels measured +1.4 % with it)
@@ -630,9 +641,10 @@ __device__ __forceinline__ void coop_consume(CoopStep<U, R>& S, WaveLds& W, uint
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
             S.sl[h].acc = block_sum(S.d[h][u], S.sl[h].acc);
-            if (b0 + 16 * u + 1 == S.sl[h].nb) W.tail[S.sl[h].j] = S.d[h][u];  // nb == 0: never
+            if (b0 + 16 * u - S.sl[h].lg + 1 == S.sl[h].nb) W.tail[S.sl[h].j] = S.d[h][u];  // nb == 0: never
         }
-        if (S.sl[h].has && it == 0 && l16 < kHdrGran) W.hdr[S.sl[h].j][l16] = S.d[h][0];
+        const uint32_t hb = l16 - S.sl[h].lg;  // header granule hb of the frame (wraps below it)
+        if (S.sl[h].has && it == 0 && hb < kHdrGran) W.hdr[S.sl[h].j][hb] = S.d[h][0];
     }
 }
 
