@@ -417,7 +417,6 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 struct CoopSlot {
     uint32_t boff;  // byte offset of the frame's first granule in the blob
     uint32_t nb, j, acc;
-    uint32_t lg;    // granules between the frame's 64-byte line start and its first granule (0..3)
     bool has;
 };
 
@@ -499,11 +498,9 @@ struct FrameDesc {
     uint32_t sh;         // f - a, even (a = granule base)
     uint32_t span;       // bytes from a to the frame end
     uint32_t nblk;       // big frames: granules covering [a, f + len)
-    uint32_t lg;         // a's granule within its 64-byte line (0..3): quarter-wave spans start at the line (coop_issue)
     __device__ __forceinline__ FrameDesc(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t off,
                                          uint32_t len) {
         inb = live && (uint64_t)off + len <= frames_bytes;
-        lg = ((uint32_t)reinterpret_cast<uintptr_t>(frames + off) >> 4) & 3u;
         const uint32_t fmod = (uint32_t)reinterpret_cast<uintptr_t>(frames + off) & 15u;
         sh = kShift ? fmod : 0u;
         vec = inb && (kShift ? (fmod & 1u) == 0 : fmod == 0);
@@ -570,19 +567,17 @@ __device__ __forceinline__ CoopPlan coop_plan(const FrameDesc<kShift>& F, uint32
     pl.nmed = 0;
     pl.maxit = 1;
     if (pl.ncoop == 0) return pl;
-    // a frame's granules counted from its 64-byte line start (the quarter-wave's loads cover whole lines, below)
-    const uint32_t lspan = F.big ? F.nblk + F.lg : 0u;
-    const bool med = F.big && lspan <= kMedGran;
+    const bool med = F.big && F.nblk <= kMedGran;
     const uint64_t mm = __ballot(med), lm = cm & ~mm;
     pl.nmed = (uint32_t)__popcll(mm);
     if (F.big) {
         const uint64_t m = med ? mm : lm;
         const uint32_t rank = (med ? 0u : pl.nmed) +
                               __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        W.rec[rank] = make_uint2(lane | (F.lg << 6) | (F.nblk << 8), off - F.sh);  // one ds_read_b64 per round
+        W.rec[rank] = make_uint2(lane | (F.nblk << 8), off - F.sh);  // one ds_read_b64 per round
     }
-    if (__ballot(lspan > kCoopSpan)) {
-        uint32_t mx = lspan;
+    if (__ballot(F.nblk > kCoopSpan)) {
+        uint32_t mx = F.nblk;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
         pl.maxit = __builtin_amdgcn_readfirstlane((mx - 1) / kCoopSpan + 1);
@@ -604,24 +599,18 @@ __device__ __forceinline__ void coop_issue(uint32_t k0, uint32_t k1, uint32_t r,
             const uint32_t k = k0 + (r + h) * 4 + q;
             S.sl[h].has = k < k1;
             const uint2 rec = S.sl[h].has ? W.rec[k] : make_uint2(0, 0);
-            S.sl[h].j = rec.x & 0x3Fu;
-            S.sl[h].lg = (rec.x >> 6) & 3u;
+            S.sl[h].j = rec.x & 0xFFu;
             S.sl[h].nb = rec.x >> 8;  // 0 for an empty slot: every load is then out of range
             S.sl[h].boff = rec.y;
             S.sl[h].acc = 0;
         }
     }
-    // Granule b of the frame is loaded by lane l16 = (b + lg) mod 16 of load u = (b + lg) / 16 (iteration it): each
-    // load's 16 lanes cover one 256-byte span that starts on a 64-byte line, i.e. 4 whole lines. Spans from the frame's
-    // first granule instead touched 5 lines each for frames at 16-48 mod 64 — the TPACKET_V3 ring's frames at
-    // tp_mac = 82 — and uncached host memory fetched the shared lines twice: 6 x 5 = 30 PCIe line reads for a 1500-byte
-    // frame that spans 24-25 lines. Lanes below lg load at kOob (zeros, no access).
     const uint32_t b0 = it * 16 * U + l16;
 #pragma unroll
     for (uint32_t h = 0; h < R; h++)
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
-            const uint32_t b = b0 + 16 * u - S.sl[h].lg;  // wraps below the frame: out of range
+            const uint32_t b = b0 + 16 * u;
             // kHdrT (the TX kernels): each frame's first 16 granules (its first 256 bytes, u = 0) with the default
             // policy instead of nontemporal, so the header-window rewrite finds its line in L2 (TX C2 -3 %; the
             // receive kernels measured +1.4 % with it)
@@ -641,10 +630,9 @@ __device__ __forceinline__ void coop_consume(CoopStep<U, R>& S, WaveLds& W, uint
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
             S.sl[h].acc = block_sum(S.d[h][u], S.sl[h].acc);
-            if (b0 + 16 * u - S.sl[h].lg + 1 == S.sl[h].nb) W.tail[S.sl[h].j] = S.d[h][u];  // nb == 0: never
+            if (b0 + 16 * u + 1 == S.sl[h].nb) W.tail[S.sl[h].j] = S.d[h][u];  // nb == 0: never
         }
-        const uint32_t hb = l16 - S.sl[h].lg;  // header granule hb of the frame (wraps below it)
-        if (S.sl[h].has && it == 0 && hb < kHdrGran) W.hdr[S.sl[h].j][hb] = S.d[h][0];
+        if (S.sl[h].has && it == 0 && l16 < kHdrGran) W.hdr[S.sl[h].j][l16] = S.d[h][0];
     }
 }
 
@@ -1493,66 +1481,58 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
         L.v = kNone;
         L.need = 0;
     }
-    // Branch-free for the common frame (round 5): every lane computes the ICMP verdict, the T4 / U3 checksum compare
-    // and the first-slot demux, and selects; only the rare second steps (a TCP probe walk past a taken slot, the
-    // Passive / 0.0.0.0 lookup after a miss) are wave-uniform branches. (The if / else-if chain of rx_back cost the
-    // wave ~60 SALU per chunk in exec-mask bookkeeping, taken or not.)
-    const bool tcp = L.v == kPendTcp, udp = L.v == kPendUdp, icmp = L.v == kPendIcmp;
-    const uint32_t dport = L.ports >> 16;
-    // One table load per lane before the checksum arithmetic: TCP the hashed Active slot, UDP the 16 bytes of the port
-    // table holding (local_ip, dport)'s word (the port table starts 16-byte aligned, after the Active slots), other
-    // lanes the table's first slot (loaded, unused).
+    // first socket-table load before the checksum arithmetic (as rx_front)
     const ProbeKey k1{DK_FLOW_TCP_ACTIVE, P.local_ip, L.src, (L.ports >> 16) | (L.ports << 16)};
-    const uint32_t h1 = tcp ? probe_slot(P, k1) : 0u;
-    const uint4* T4 = reinterpret_cast<const uint4*>(P.table);
-    const uint4* U4 = reinterpret_cast<const uint4*>(P.port_tab + kPortUdpLocal);
-    const uint4 s1 = *(tcp ? T4 + h1 : udp ? U4 + (dport >> 2) : T4);
-    uint32_t lsum;  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
-    if (!__ballot(L.need && L.E != 64u)) {
-        lsum = hsum2(R.w[8] & 0xFFFF0000u, 0);
+    uint32_t h1 = 0;
+    uint4 s1 = make_uint4(0, 0, 0, 0);
+    if (L.v == kPendTcp) {
+        h1 = probe_slot(P, k1);
+        s1 = reinterpret_cast<const uint4*>(P.table)[h1];
+    }
+    if (L.v == kPendUdp) s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+    uint32_t lsum = 0;
+    if (L.need) {  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
+        if (!__ballot(L.E != 64u)) {
+            lsum = hsum2(R.w[8] & 0xFFFF0000u, 0);
 #pragma unroll
-        for (int k = 9; k < 16; k++) lsum = hsum2(R.w[k], lsum);
-    } else {
-        const int t = 32 - 8 * (int)L.E;
-        lsum = 0;
+            for (int k = 9; k < 16; k++) lsum = hsum2(R.w[k], lsum);
+        } else {
+            const int t = 32 - 8 * (int)L.E;
 #pragma unroll
-        for (int k = 8; k < 16; k++) {
-            const uint32_t sh = (uint32_t)min(max(t + 32 * k, 0), 32);
-            uint32_t m = (uint32_t)(0xFFFFFFFFull >> sh);
-            if (k == 8) m &= 0xFFFF0000u;
-            lsum = hsum2(R.w[k] & m, lsum);
+            for (int k = 8; k < 16; k++) {
+                const uint32_t sh = (uint32_t)min(max(t + 32 * k, 0), 32);
+                uint32_t m = (uint32_t)(0xFFFFFFFFull >> sh);
+                if (k == 8) m &= 0xFFFF0000u;
+                lsum = hsum2(R.w[k] & m, lsum);
+            }
         }
     }
-    // ICMPv4 (as rx_back: icmpv4/header.rs:55-57, protocol.rs:37-56)
-    const uint32_t type = (L.mhi >> 8) & 0xFFu;
-    const uint32_t vicmp = mod_ffff(lsum) != 0 ? (uint32_t)DK_V_ICMP_CSUM
-                           : (type < 15 && ((kIcmpTypes >> type) & 1u)) ? (uint32_t)DK_V_ICMP : (uint32_t)DK_V_ICMP_TYPE;
-    // T4 / U3 (tcp/header.rs:203-207, udp/header.rs:78-88): the stored field summed as zero, pseudo-header with the
-    // configured local address
-    const uint32_t sm = lsum - bswap16(L.stored);
-    const uint32_t lip = P.local_ip;
-    const uint32_t pseudo = bswap16(L.src & 0xFFFFu) + bswap16(L.src >> 16) + bswap16(lip & 0xFFFFu) +
-                            bswap16(lip >> 16) + (tcp ? 6u : 17u) + (L.E - L.S);
-    const bool bad = L.need && csum_from_residue(mod_ffff(be_residue(sm) + pseudo)) != L.stored;
-    // demux, first step: Active(local, remote) in the first slot (tcp/peer.rs:241-251), (local_ip, dport) for UDP
-    // (udp/peer.rs:147-165)
-    const uint32_t uw = (dport & 2u) ? ((dport & 1u) ? s1.w : s1.z) : ((dport & 1u) ? s1.y : s1.x);
-    const bool hit = s1.x != 0 && (s1.x >> 24) == k1.kind && s1.y == k1.lip && s1.z == k1.rip && s1.w == k1.lport_rport;
-    const bool l4 = (tcp || udp) && !bad;
-    uint32_t fid = !l4 ? DK_FLOW_NONE : tcp ? (hit ? s1.x & 0xFFFFFFu : DK_FLOW_NONE) : uw;
-    // rare: the Active key further along its probe sequence (the first slot taken by another key)
-    const bool walk = l4 && tcp && !hit && s1.x != 0;
-    if (__ballot(walk))
-        if (walk) fid = probe_finish(P, k1, h1, s1);
-    // rare: the second lookup, Passive(local) for TCP, (0.0.0.0, dport) for UDP
-    const bool second = l4 && fid == DK_FLOW_NONE;
-    if (__ballot(second))
-        if (second) fid = port_lookup(P, tcp ? kPortTcpPassive : kPortUdpAny, dport);
-    L.v = icmp ? vicmp
-          : (tcp || udp) ? (bad ? (tcp ? (uint32_t)DK_V_TCP_CSUM : (uint32_t)DK_V_UDP_CSUM)
-                            : fid == DK_FLOW_NONE ? (tcp ? (uint32_t)DK_V_TCP_NOSOCK : (uint32_t)DK_V_UDP_NOSOCK)
-                                                  : (tcp ? (uint32_t)DK_V_OK_TCP : (uint32_t)DK_V_OK_UDP))
-                         : L.v;
+    uint32_t fid = DK_FLOW_NONE;
+    if (L.v == kPendIcmp) {  // as rx_back (icmpv4/header.rs:55-57, protocol.rs:37-56)
+        const uint32_t type = (L.mhi >> 8) & 0xFFu;
+        L.v = mod_ffff(lsum) != 0 ? (uint32_t)DK_V_ICMP_CSUM
+              : (type < 15 && ((kIcmpTypes >> type) & 1u)) ? (uint32_t)DK_V_ICMP : (uint32_t)DK_V_ICMP_TYPE;
+    } else if (L.v == kPendTcp || L.v == kPendUdp) {
+        const bool tcp = L.v == kPendTcp;
+        if (L.need) {  // T4 / U3 (tcp/header.rs:203-207, udp/header.rs:78-88)
+            const uint32_t sm = lsum - bswap16(L.stored);
+            const uint32_t lip = P.local_ip;
+            const uint32_t pseudo = bswap16(L.src & 0xFFFFu) + bswap16(L.src >> 16) + bswap16(lip & 0xFFFFu) +
+                                    bswap16(lip >> 16) + (tcp ? 6u : 17u) + (L.E - L.S);
+            if (csum_from_residue(mod_ffff(be_residue(sm) + pseudo)) != L.stored)
+                L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
+        }
+        const uint32_t dport = L.ports >> 16;
+        if (L.v == kPendTcp) {  // Active(local, remote), then Passive(local) (tcp/peer.rs:241-251)
+            fid = probe_finish(P, k1, h1, s1);
+            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortTcpPassive, dport);
+            L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
+        } else if (L.v == kPendUdp) {  // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
+            fid = s1.x;
+            if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortUdpAny, dport);
+            L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
+        }
+    }
     const uint32_t v = L.v;
     if (live) {
         const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;

@@ -16,15 +16,13 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05h: (1) small_fast branch-free common path + leader atomics without the optimizer expansion + priority split on
-# the host (prev.so = the commit before); (2) line-aligned quarter-wave spans (pre_la.so = without them): the whole
-# receive parity file, A/B on C3 / IMIX / C2, the ring/layout PCIe experiment for both builds, C3 SQ counters
-step parity 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py
-step ab_c3 600 python tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/pre_la.so --lib build/variants/prev.so "defer=1"
+# r05i: line-aligned spans and the branch-free small_fast reverted (no gain, C3 +8 %: session r05h); kept: leader
+# atomics without the optimizer expansion + the priority split on the host (prev.so = without them). C3 A/B, the ring
+# experiment extended to the memory registration (ring layout in hipHostMalloc memory, packed layout in registered
+# mmap memory), C3 SQ counters of the kept build
+step ab_c3 600 python tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
 step ab_c3r 600 python tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 7 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
-step ab_imix 600 python tools/tune_ab.py --workload c4_imix --rotate 2 --reps 5 --iters 20 --lib demikernel_amd/libdk_rx.so --lib build/variants/pre_la.so "defer=1"
-step ab_c2 600 python tools/tune_ab.py --workload c2_tcp1500 --reps 5 --iters 20 --lib demikernel_amd/libdk_rx.so --lib build/variants/pre_la.so "defer=1"
-step ring_new 600 python tools/ring_bytes.py
-step ring_pre 600 env DK_RX_LIB_VARIANT=build/variants/pre_la.so python tools/ring_bytes.py
-step pmc6 600 bash tools/pmc_kernel.sh c3_udp64 r05h_c3 --rotate 8 --defer
+step ring 600 python tools/ring_bytes.py
+step pmc6 600 bash tools/pmc_kernel.sh c3_udp64 r05i_c3 --rotate 8 --defer
+step smallparity 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "small or udp64 or kernel_variants or corpus or golden or reference"
 echo done
