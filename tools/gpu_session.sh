@@ -16,13 +16,12 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05i: line-aligned spans and the branch-free small_fast reverted (no gain, C3 +8 %: session r05h); kept: leader
-# atomics without the optimizer expansion + the priority split on the host (prev.so = without them). C3 A/B, the ring
-# experiment extended to the memory registration (ring layout in hipHostMalloc memory, packed layout in registered
-# mmap memory), C3 SQ counters of the kept build
-step ab_c3 600 python tools/tune_ab.py --workload c3_udp64 --rotate 8 --reps 9 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
-step ab_c3r 600 python tools/tune_ab.py --workload c3_udp64_random_ports --rotate 8 --reps 7 --iters 40 --lib demikernel_amd/libdk_rx.so --lib build/variants/prev.so "defer=1"
+# r05j: evidence at the current kernels (dynamic tail, small kernel at 6 waves/SIMD, leader atomics): the GPU suite,
+# smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, the ring experiment with
+# pinned descriptors
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r05j
 step ring 600 python tools/ring_bytes.py
-step pmc6 600 bash tools/pmc_kernel.sh c3_udp64 r05i_c3 --rotate 8 --defer
-step smallparity 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "small or udp64 or kernel_variants or corpus or golden or reference"
 echo done

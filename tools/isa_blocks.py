@@ -14,6 +14,8 @@ def classify(op):
         return "valu"
     if op.startswith("s_waitcnt") or op.startswith("s_nop") or op.startswith("s_setprio"):
         return "wait"
+    if op.startswith("s_cbranch") or op.startswith("s_branch"):
+        return "branch"
     if op.startswith("s_load") or op.startswith("s_buffer_load"):
         return "smem"
     if op.startswith("s_"):

@@ -54,9 +54,15 @@ def main():
     res = RxResults(n, len(flows), host=True)
     nbytes = int(lens.astype(np.int64).sum())
 
+    def pinned_desc(off, ln):  # descriptors in pinned memory, as bench.py host_path passes them
+        o = torch.from_numpy(np.ascontiguousarray(off, np.uint32).view(np.int32)).pin_memory()
+        l_ = torch.from_numpy(np.ascontiguousarray(ln, np.uint16).view(np.int16)).pin_memory()
+        return o.numpy().view(np.uint32), l_.numpy().view(np.uint16), (o, l_)
+
     def timed(blob_np, off, ln):
         pinned = torch.empty(blob_np.nbytes, dtype=torch.uint8, pin_memory=True)
         pinned.numpy()[:] = blob_np
+        off, ln, keep = pinned_desc(off, ln)
         rates = []
         for _ in range(args.reps + 1):
             t = time.perf_counter()
@@ -72,6 +78,7 @@ def main():
         buf[:] = blob_np
         lib = N.load_library()
         assert lib.dk_ring_register(buf.ctypes.data, buf.nbytes) == 0
+        off, ln, keep = pinned_desc(off, ln)
         try:
             rates = []
             for _ in range(args.reps + 1):
@@ -101,6 +108,7 @@ def main():
     try:
         off, ln, nb = r.scan(0, used, n)
         assert len(off) == n
+        off, ln, keep = pinned_desc(off, ln)
         rates = []
         for _ in range(args.reps + 1):
             t = time.perf_counter()
