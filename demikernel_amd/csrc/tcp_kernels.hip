@@ -430,7 +430,9 @@ __global__ __launch_bounds__(kWalkBlock) void dk_tcp_walk_kernel(Params P) {
 // classified in parallel (see the loop below): segments whose process_packet outcome needs no state machine are
 // taken at once — in-order data with no SYN/FIN/RST that ends inside the window and does not end exactly at the
 // out-of-order store's first entry or a pending FIN (NO_ACK / ACK_UNSENT with no state change, else DELIVERED = one
-// push and RCV.NXT += length, nothing drained from the store, or NO_DATA), entirely old segments (DUPLICATE) and segments past the window (OUT_OF_WINDOW). The window end
+// push and RCV.NXT += length, nothing drained from the store, or NO_DATA), the same for a partial retransmission
+// (starts before RCV.NXT, ends after it: its old front trimmed, the rest as in order), entirely old segments
+// (DUPLICATE) and segments past the window (OUT_OF_WINDOW). The window end
 // RCV.NXT + buffer - (RCV.NXT - reader_next) is reader_next + buffer for the whole batch, since nothing reads during
 // it. The first other segment goes through process() with every lane executing it redundantly (same inputs; the
 // out-of-order store is a RegStore, entry k in lane k), then the parallel check resumes at the next lane.
@@ -438,12 +440,42 @@ constexpr uint32_t kWave = 64;
 
 using WaveScan = rocprim::warp_scan<uint32_t, kWave>;
 
-// kAhead: segment records kAhead windows ahead, frame indices kAhead + 1 (1 for many connections, where occupancy
-// hides the record latency; more for few connections, where one wave's window loop is the whole run and each window
-// otherwise waits out a record load).
-template <int kAhead>
+// kRing = false (many connections, where occupancy hides the latency): each window's records are loaded one window
+// ahead into registers. kRing = true (few connections, where one wave's window loop is the whole run): the frame
+// indices and records stream into LDS rings by LDS-DMA loads (global_load_lds), kRingH windows ahead, with explicit
+// waits (below). Register prefetch does not survive the compiler here: the window loop holds stores and inner loops,
+// and the compiler waits for every outstanding load before such a loop (a 1-connection batch ran at 1.2 µs per
+// 64-segment window, one load latency each, with records prefetched four windows ahead in registers).
+constexpr uint32_t kRingH = 6, kIdxSlots = 16, kRecSlots = 8;
+static_assert(2 * kRingH + 1 <= kIdxSlots && kRingH + 1 <= kRecSlots, "ring slots cover the windows in flight");
+static_assert(2 * kRingH - 2 == 10, "the s_waitcnt immediate below");
+typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+__device__ __forceinline__ uint32_t lds_read_u32(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+// one window's frame indices (a_i), records (a_g) and the frame indices of window + kRingH (a_f)
+__device__ __forceinline__ void lds_read_window(uint32_t a_i, uint32_t a_g, uint32_t a_f, uint32_t& i, uint4& g,
+                                                uint32_t& f) {
+    u32x4 q;
+    asm volatile("ds_read_b32 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(i), "=&v"(q), "=&v"(f)
+                 : "v"(a_i), "v"(a_g), "v"(a_f)
+                 : "memory");
+    g = make_uint4(q.x, q.y, q.z, q.w);
+}
+
+template <bool kRing>
 __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     __shared__ WaveScan::storage_type scan_tmp;
+    __shared__ uint32_t sidx[kRing ? kIdxSlots : 1][kWave];
+    __shared__ uint4 srec[kRing ? kRecSlots : 1][kWave];
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     dk_tcp_conn* t = P.conns + c;
     const uint32_t k0 = P.range[2 * c], cnt = P.range[2 * c + 1] - k0, all = P.range[2 * c + 2] - k0;
@@ -461,25 +493,11 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     Out o{P.out.deliv + d0, 0, all + DK_TCP_DELIV_EXTRA};
     const uint32_t wend = w.reader + w.bufsz;
     uint32_t open_until = w.state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u;
-    // Software pipeline over windows: frame indices kAhead + 1 windows ahead, records kAhead windows ahead (register
-    // rings iq / gq: slot j holds window base / 64 + j).
-    uint32_t iq[kAhead + 1];
-    uint4 gq[kAhead];
-#pragma unroll
-    for (int j = 0; j <= kAhead; j++) iq[j] = j * kWave + lane < cnt ? P.svals[k0 + j * kWave + lane] : 0u;
-#pragma unroll
-    for (int j = 0; j < kAhead; j++) gq[j] = j * kWave + lane < cnt ? P.rec[iq[j]] : make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t base = 0; base < cnt; base += kWave) {
+    // Loads are unconditional: positions past the connection's last segment read its last one again (unused).
+    const uint32_t last = cnt ? cnt - 1 : 0u;
+    const auto window = [&](uint32_t base, uint32_t i, uint4 g) {
         const uint32_t lim = min(cnt - base, kWave);
         const bool have = lane < lim;
-        const uint32_t i = iq[0];
-        const uint4 g = gq[0];
-#pragma unroll
-        for (int j = 0; j < kAhead; j++) iq[j] = iq[j + 1];
-#pragma unroll
-        for (int j = 0; j + 1 < kAhead; j++) gq[j] = gq[j + 1];
-        gq[kAhead - 1] = base + kAhead * kWave + lane < cnt ? P.rec[iq[kAhead - 1]] : make_uint4(0u, 0u, 0u, 0u);
-        iq[kAhead] = base + (kAhead + 1) * kWave + lane < cnt ? P.svals[k0 + base + (kAhead + 1) * kWave + lane] : 0u;
         const uint32_t flags = (g.z >> 16) & 0xFFu, off = g.w & 0xFFFFu, len = g.w >> 16;
         const bool simple = have && !(flags & 0x07u);
         const bool ack_ok = (flags & 0x10u) && le(g.y, w.snd);
@@ -509,9 +527,12 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
                 beyond = true;
                 for (uint32_t k = 0; k < DK_TCP_OOO_MAX; k++) beyond = beyond && lt(s.start(k) + (s.len(k) - 1), g.x);
             }
+            // candidates: data ending after RCV.NXT at lo and inside the window, starting at it or before (a partial
+            // retransmission: its old front is trimmed and the rest delivered)
             uint32_t rel = 0;
-            if (mine && simple && !beyond && ack_ok && len > 0 && ge(g.x, w.rn) && !ge(g.x + (len - 1), wend))
-                rel = (g.x - w.rn) + len;
+            const uint32_t dend = g.x + len;
+            if (mine && simple && !beyond && ack_ok && len > 0 && lt(w.rn, dend) && !ge(dend - 1u, wend))
+                rel = dend - w.rn;
             uint32_t mx_prev;  // max over the lanes before this one (DPP scan)
             WaveScan().exclusive_scan(rel, mx_prev, 0u, scan_tmp, rocprim::maximum<uint32_t>());
             const uint32_t mx = max(mx_prev, rel);
@@ -523,15 +544,21 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
             const uint32_t seg_end = full ? g.x + (full - 1) : g.x;
             bool ok;
             uint8_t act;
-            uint32_t vlen = len;
+            uint32_t voff = off, vlen = len;
+            const bool drains = ack_ok && len > 0 && ((w.nooo && dend == front) || (w.fin_pending && dend == w.fin_seq));
             if (g.x == rn) {
-                ok = simple && !beyond && (len == 0 || !ge(g.x + (len - 1), wend)) &&
-                     !(ack_ok && len > 0 &&
-                       ((w.nooo && g.x + len == front) || (w.fin_pending && g.x + len == w.fin_seq)));
+                ok = simple && !beyond && (len == 0 || !ge(dend - 1u, wend)) && !drains;
                 act = fast_action;
             } else if (lt(g.x, rn)) {
-                ok = lt(seg_end, rn);
-                act = DK_TCP_DUPLICATE;
+                if (lt(seg_end, rn)) {
+                    ok = true;
+                    act = DK_TCP_DUPLICATE;
+                } else {  // check_segment_in_window trims the old front (ctrlblk.rs:480-500); then as in order
+                    ok = simple && !beyond && !ge(dend - 1u, wend) && !drains;
+                    act = fast_action;
+                    voff = off + (rn - g.x);
+                    vlen = dend - rn;
+                }
             } else if (ge(g.x, wend)) {
                 ok = true;
                 act = DK_TCP_OUT_OF_WINDOW;
@@ -550,8 +577,8 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
             const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
             if (taken) {
                 P.out.action[i] = act;
-                P.out.view[i] = dk_tcp_view{i, off, vlen};
-                if (pushed && o.n + before < o.cap) o.d[o.n + before] = dk_tcp_view{i, off, len};
+                P.out.view[i] = dk_tcp_view{i, voff, vlen};
+                if (pushed && o.n + before < o.cap) o.d[o.n + before] = dk_tcp_view{i, voff, vlen};
             }
             o.n += (uint32_t)__builtin_popcountll(pm);
             if (f > lo) w.rn += (uint32_t)__builtin_amdgcn_readlane(mx, f - 1);
@@ -567,6 +594,58 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
             }
             if (w.state != DK_TCP_ESTABLISHED) open_until = i_f + 1;  // this segment closed the connection
             lo = f + 1;
+        }
+    };
+    if constexpr (kRing) {
+        // Window u's indices land in sidx[u % 16] (DMA issued at window u - 2H, read at u - H and u), its records in
+        // srec[u % 8] (issued at window u - H, read at u). Window v issues records(v + H), then indices(v + 2H), so
+        // at least 2H - 2 vector-memory operations follow indices(v + H) and 2H - 1 follow records(v): vmcnt(2H - 2)
+        // has both landed whatever else (result stores) was issued in between (vmcnt retires in order).
+        const auto idx_dma = [&](uint32_t u) {
+            __builtin_amdgcn_global_load_lds((const void*)(P.svals + k0 + min(u * kWave + lane, last)),
+                                             (lds_void*)&sidx[u % kIdxSlots][0], 4, 0, 0);
+        };
+        const auto rec_dma = [&](uint32_t u, uint32_t fi) {
+            __builtin_amdgcn_global_load_lds((const void*)(P.rec + fi), (lds_void*)&srec[u % kRecSlots][0], 16, 0, 0);
+        };
+        // The ring is read by inline-asm LDS loads: the compiler cannot tell ring slots apart and would wait for every
+        // LDS-DMA load (vmcnt(0)) before each LDS read.
+        const auto idx_at = [&](uint32_t u) { return lds_addr(&sidx[u % kIdxSlots][lane]); };
+        if (cnt) {  // (k0 may be n then)
+            for (uint32_t u = 0; u < kRingH; u++) idx_dma(u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (uint32_t u = 0; u < kRingH; u++) {
+                rec_dma(u, lds_read_u32(idx_at(u)));
+                idx_dma(u + kRingH);
+            }
+        }
+        for (uint32_t v = 0; v * kWave < cnt; v++) {
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            uint32_t i, fi;
+            uint4 g;
+            lds_read_window(idx_at(v), lds_addr(&srec[v % kRecSlots][lane]), idx_at(v + kRingH), i, g, fi);
+            rec_dma(v + kRingH, fi);
+            idx_dma(v + 2 * kRingH);
+            window(v * kWave, i, g);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write outlives the workgroup
+    } else {
+        // frame indices two windows ahead, records one
+        const auto idx = [&](uint32_t u) { return P.svals[k0 + min(u * kWave + lane, last)]; };
+        uint32_t i = 0, i1 = 0;
+        uint4 g = make_uint4(0u, 0u, 0u, 0u);
+        if (cnt) {
+            i = idx(0);
+            i1 = idx(1);
+            g = P.rec[i];
+        }
+        for (uint32_t v = 0; v * kWave < cnt; v++) {
+            const uint32_t i2 = idx(v + 2);
+            const uint4 g1 = P.rec[i1];
+            window(v * kWave, i, g);
+            i = i1;
+            i1 = i2;
+            g = g1;
         }
     }
     if (lane == 0) {
@@ -589,11 +668,8 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
 // Which walk runs: `force` (DK_TCP_WALK=lane|wave, read once at dk_tcp_ctx_create: 0 lane, 1 wave, -1 the rule);
 // otherwise the wave walk when connections average at least kWaveWalkMinSegs segments in the batch.
 constexpr uint32_t kWaveWalkMinSegs = 8;
-// Up to this many connections (waves) the wave walk prefetches DK_TCP_DEEP_AHEAD windows of records: a few waves per
-// SIMD at most, so the extra registers cost no occupancy.
-#ifndef DK_TCP_DEEP_AHEAD
-#define DK_TCP_DEEP_AHEAD 4
-#endif
+// Up to this many connections (waves) the wave walk streams through LDS rings (kRing): 8 waves per CU at most on
+// 256 CUs, 12 KiB of LDS each.
 #ifndef DK_TCP_DEEP_MAX_CONNS
 #define DK_TCP_DEEP_MAX_CONNS 2048
 #endif
@@ -739,9 +815,9 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     if (nconns) {
         if (use_wave_walk(n, nconns, t->walk))
             if (nconns <= kDeepAheadMaxConns)
-                hipLaunchKernelGGL(dk_tcp_wave_walk_kernel<DK_TCP_DEEP_AHEAD>, dim3(nconns), dim3(kWave), 0, s, P);
+                hipLaunchKernelGGL(dk_tcp_wave_walk_kernel<true>, dim3(nconns), dim3(kWave), 0, s, P);
             else
-                hipLaunchKernelGGL(dk_tcp_wave_walk_kernel<1>, dim3(nconns), dim3(kWave), 0, s, P);
+                hipLaunchKernelGGL(dk_tcp_wave_walk_kernel<false>, dim3(nconns), dim3(kWave), 0, s, P);
         else
             hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
     }

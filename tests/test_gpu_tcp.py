@@ -106,6 +106,16 @@ SCENARIOS = {
     "long_runs": (S.conns(rn=1), [(0, 1 + 10 * k, 1, S.ACK, 10) for k in range(150)] +
                   [(0, 3001, 1, S.ACK, 10), (0, 1, 1, S.ACK, 10)] +
                   [(0, 1501 + 10 * k, 1, S.ACK, 10) for k in range(149)] + [(0, 2991, 1, S.ACK, 20)]),
+    # partial retransmissions inside in-order runs (the wave walk's parallel check trims and delivers them): plain,
+    # one re-trimming the next in-order segment, one without ACK, one ending at the store's front (drains), one
+    # ending past the window end, then a segment past the window
+    "partial_runs": (S.conns(rn=1, bufsz=5000), [(0, 4001, 1, S.ACK, 100)] +
+                     [(0, 1 + 100 * k, 1, S.ACK, 100) for k in range(30)] +
+                     [(0, 2951, 1, S.ACK, 100), (0, 3001, 1, S.ACK, 100), (0, 3050, 1, S.PSH, 100)] +
+                     [(0, 3101 + 100 * k, 1, S.ACK, 100) for k in range(8)] +
+                     [(0, 3851, 1, S.ACK, 150), (0, 4051, 1, S.ACK, 100)] +
+                     [(0, 4151 + 100 * k, 1, S.ACK, 100) for k in range(8)] +
+                     [(0, 4901, 1, S.ACK, 200), (0, 5001, 1, S.ACK, 10)]),
     # segments the key pass classifies without a walk (past the window end: OUT_OF_WINDOW; ending before the table's
     # RCV.NXT: DUPLICATE) queued behind a FIN / an RST that closes the connection become UNPROCESSED
     # (dk_tcp_fix_kernel); before the close they keep their class

@@ -16,12 +16,11 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05j: evidence at the current kernels (dynamic tail, small kernel at 6 waves/SIMD, leader atomics): the GPU suite,
-# smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, the ring experiment with
-# pinned descriptors
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r05j
-step ring 600 python tools/ring_bytes.py
+# r05l: the wave walk streams few-connection batches through LDS rings (LDS-DMA); partial retransmissions on the
+# parallel check. TCP GPU tests, the 1 / 64 / 16k connection rates, kernel stats of the 1-connection case
+step tcptest 600 python -u -m pytest tests/test_gpu_tcp.py -m gpu -x -q --timeout 300 --timeout-method thread
+step tcp1 300 python tools/tcpbench.py --nconns 1 --buffer-size 1073741824 --reorder 0 --iters 10
+step tcpn 300 python tools/tcpbench.py --nconns 64 16384 --iters 10 --cpu-seconds 0.5
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/prof1 -o run --output-format csv -- \
+  python3 $R/tools/tcpbench.py --nconns 1 --buffer-size 1073741824 --reorder 0 --iters 10 --cpu-seconds 0.2 > $O/prof1.log 2>&1 || exit 11
 echo done
