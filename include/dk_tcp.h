@@ -21,8 +21,9 @@
  * Conventions as dk_rx.h: 0 or a positive errno; device pointers; asynchronous on the caller's stream. A context holds
  * one set of scratch buffers: calls on one context are serialised — a call on another stream than the previous call
  * first waits (on the device) for the previous call's work — so use one context per stream for concurrent batches.
- * The engine picks its per-connection walk from the batch (one lane per connection, or one wave per connection at
- * >= 8 segments per connection); the environment variable DK_TCP_WALK=lane|wave, read when the context is created,
+ * The engine picks its per-connection walk from the batch (one lane per connection; one wave per connection at
+ * >= 8 segments per connection; 8 waves per connection relaying its state at >= 1,024 segments per connection and
+ * <= 4,096 connections); the environment variable DK_TCP_WALK=lane|wave|relay, read when the context is created,
  * forces one. Results are identical.
  */
 #ifndef DK_TCP_H

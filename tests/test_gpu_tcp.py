@@ -17,10 +17,11 @@ from oracle.oracle import OraclePeer
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["lane", "wave"])
+@pytest.fixture(scope="module", params=["lane", "wave", "relay"])
 def tcp(request):
-    """Every test runs through both walks: lanes = connections, and one wave per connection with the parallel
-    in-order check (DK_TCP_WALK forces the choice the engine otherwise makes from segments per connection)."""
+    """Every test runs through every walk: lanes = connections, one wave per connection with the parallel in-order
+    check, and 16 waves per connection relaying its state window to window (DK_TCP_WALK forces the choice the engine
+    otherwise makes from segments per connection)."""
     import os
 
     import torch
@@ -116,6 +117,17 @@ SCENARIOS = {
                      [(0, 3851, 1, S.ACK, 150), (0, 4051, 1, S.ACK, 100)] +
                      [(0, 4151 + 100 * k, 1, S.ACK, 100) for k in range(8)] +
                      [(0, 4901, 1, S.ACK, 200), (0, 5001, 1, S.ACK, 10)]),
+    # retransmitted SYNs inside in-order runs (the relay walk's check takes the reached ones as data): partial, at
+    # RCV.NXT, past it, partial without ACK, partial ending at the store's front (drains), partial ending past the
+    # window end, entirely old
+    "syn_runs": (S.conns(rn=1, bufsz=6000), [(0, 5001, 1, S.ACK, 100)] +
+                 [(0, 1 + 100 * k, 1, S.ACK, 100) for k in range(20)] +
+                 [(0, 1951, 1, S.SYN | S.ACK, 100), (0, 2001, 1, S.ACK, 100), (0, 2101, 1, S.SYN | S.ACK, 50),
+                  (0, 2500, 1, S.SYN | S.ACK, 10)] +
+                 [(0, 2101 + 100 * k, 1, S.ACK, 100) for k in range(10)] + [(0, 3050, 1, S.SYN, 100)] +
+                 [(0, 3101 + 100 * k, 1, S.ACK, 100) for k in range(18)] + [(0, 4850, 1, S.SYN | S.ACK, 150)] +
+                 [(0, 5101 + 100 * k, 1, S.ACK, 100) for k in range(8)] +
+                 [(0, 5850, 1, S.SYN | S.ACK, 200), (0, 100, 1, S.SYN | S.ACK, 50)]),
     # segments the key pass classifies without a walk (past the window end: OUT_OF_WINDOW; ending before the table's
     # RCV.NXT: DUPLICATE) queued behind a FIN / an RST that closes the connection become UNPROCESSED
     # (dk_tcp_fix_kernel); before the close they keep their class

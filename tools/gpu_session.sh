@@ -16,11 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05l: the wave walk streams few-connection batches through LDS rings (LDS-DMA); partial retransmissions on the
-# parallel check. TCP GPU tests, the 1 / 64 / 16k connection rates, kernel stats of the 1-connection case
+# r05r: relay walk: threshold pre-check + reached retransmitted SYNs as data
 step tcptest 600 python -u -m pytest tests/test_gpu_tcp.py -m gpu -x -q --timeout 300 --timeout-method thread
-step tcp1 300 python tools/tcpbench.py --nconns 1 --buffer-size 1073741824 --reorder 0 --iters 10
-step tcpn 300 python tools/tcpbench.py --nconns 64 16384 --iters 10 --cpu-seconds 0.5
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/prof1 -o run --output-format csv -- \
-  python3 $R/tools/tcpbench.py --nconns 1 --buffer-size 1073741824 --reorder 0 --iters 10 --cpu-seconds 0.2 > $O/prof1.log 2>&1 || exit 11
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 64 --relay-waves 4 8 16
 echo done
