@@ -133,9 +133,9 @@ def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid, record):
 @pytest.mark.parametrize("grid", ["7", "40"])
 @pytest.mark.parametrize("tail", ["0", "1", "2", "4", "12"])
 def test_staged_dynamic_tail(torch_cuda, monkeypatch, capfd, tail, grid):
-    """The staged kernel's dynamic tail (rx_common.h kTailXcds): the last rounds of chunks handed out by per-XCD
-    counters. Every depth from off (0) to most of the batch grabbed (12), on grids of 7 and 40 workgroups (many chunks
-    per wave, pools emptied, then the other XCDs' pools drained), IMIX with a corrupted tail, 16-byte aligned and at
+    """The staged kernel's dynamic tail (rx_common.h kTailXcds): the last rounds of chunks handed out by per-pool
+    counters (pools keyed by workgroup index). Every depth from off (0) to most of the batch grabbed (12), on grids of
+    7 (one pool) and 40 workgroups (8 pools; many chunks per wave), IMIX with a corrupted tail, 16-byte aligned and at
     2 mod 16. Four launches back to back on one stream and engine (the two counter sets alternate, each launch zeroing
     the next one's), the second and third with deferred counters; every launch's results and counters bit-exact vs
     the oracle. The debug line shows the round-robin rounds the host chose."""
