@@ -16,7 +16,6 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05r: relay walk: threshold pre-check + reached retransmitted SYNs as data
-step tcptest 600 python -u -m pytest tests/test_gpu_tcp.py -m gpu -x -q --timeout 300 --timeout-method thread
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 64 --relay-waves 4 8 16
+# r05t: C4 / C5 at the node-wide size (16M frames as 8 ranks' shards) on one GPU
+step nodewide 900 python -u -m pytest tests/test_gpu_node_wide.py -v -s --timeout 800 --timeout-method thread
 echo done
