@@ -16,6 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05t: C4 / C5 at the node-wide size (16M frames as 8 ranks' shards) on one GPU
-step nodewide 900 python -u -m pytest tests/test_gpu_node_wide.py -v -s --timeout 800 --timeout-method thread
+# r05u: the ring and packed host paths through staged copies (DMA of each chunk's byte range, DK_RX_HOST_ZC=0) vs
+# zero-copy reads in place
+DK_RX_HOST_ZC=0 step ringcopy 600 python tools/ring_bytes.py
+step ringzc 600 python tools/ring_bytes.py
 echo done
