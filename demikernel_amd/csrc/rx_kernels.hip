@@ -1329,7 +1329,8 @@ struct SmallLds {
                               // spilled 16-22 VGPRs to scratch (C3 +11 %, round 3).
 #endif
 #ifndef DK_SMALL_WAVES
-#define DK_SMALL_WAVES 4  // waves per workgroup of the small-frame kernel
+#define DK_SMALL_WAVES 8  // waves per workgroup of the small-frame kernel: 8 since round 5 (at 6 waves/SIMD, half the
+                          // counter rows: C3 -2.7 %, random ports -2 %, session r05v; 4 was ahead at 5 waves/SIMD)
 #endif
 constexpr uint32_t kSmallWaves = DK_SMALL_WAVES;
 constexpr int kSmallBlock = 64 * DK_SMALL_WAVES;

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
     ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
     ap.add_argument("--frames", type=int, default=0, help="frames per batch (0: the workload's own)")
+    ap.add_argument("--defer", action="store_true", help="deferred counters (DK_RX_BATCH_DEFER_COUNTS), as bench.py runs")
     ap.add_argument("--check", action="store_true", help="also compare every variant's results and counters with the "
                                                           "first variant's on one fresh launch")
     args = ap.parse_args()
@@ -75,7 +76,8 @@ def main():
             for k, (e, r) in engines.items():
                 if hasattr(e.lib, "dk_diag_rx_set_tuning"):  # later builds read them once per context
                     e.set_tuning(**knobs)
-                run = (lambda b: e.tx_checksum(b)) if args.tx else (lambda b: e.receive_batch(b, r))  # noqa: E731
+                run = ((lambda b: e.tx_checksum(b)) if args.tx else  # noqa: E731
+                       (lambda b: e.receive_batch(b, r, defer_counts=args.defer)))
                 run(batch)
                 ev0.record()
                 for it in range(args.iters):

@@ -16,8 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05u: the ring and packed host paths through staged copies (DMA of each chunk's byte range, DK_RX_HOST_ZC=0) vs
-# zero-copy reads in place
-DK_RX_HOST_ZC=0 step ringcopy 600 python tools/ring_bytes.py
-step ringzc 600 python tools/ring_bytes.py
+# r05w: the small kernel with 8 waves per workgroup as the default build: GPU suite, then C3 A/B against the 4-wave
+# build (results compared)
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --iters 20 --reps 15 --check build/variants/sw4.so demikernel_amd/libdk_rx.so
+step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --iters 20 --reps 15 build/variants/sw4.so demikernel_amd/libdk_rx.so
 echo done
