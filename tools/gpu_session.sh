@@ -16,9 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05w: the small kernel with 8 waves per workgroup as the default build: GPU suite, then C3 A/B against the 4-wave
-# build (results compared)
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --iters 20 --reps 15 --check build/variants/sw4.so demikernel_amd/libdk_rx.so
-step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --iters 20 --reps 15 build/variants/sw4.so demikernel_amd/libdk_rx.so
+# r05y: the staging kernel with 8 / 12 waves per workgroup (one workgroup per CU at 12: a third of the counter rows
+# and LDS-table copies) vs 4; IMIX (2 rotating batches) and C1, results compared
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --iters 10 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/st12.so build/variants/st8.so
+step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/st12.so build/variants/st8.so
 echo done
