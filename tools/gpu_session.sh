@@ -16,8 +16,11 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05y: the staging kernel with 8 / 12 waves per workgroup (one workgroup per CU at 12: a third of the counter rows
-# and LDS-table copies) vs 4; IMIX (2 rotating batches) and C1, results compared
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --iters 10 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/st12.so build/variants/st8.so
-step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/st12.so build/variants/st8.so
+# r05z: evidence at the current kernels (small kernel 8 waves per workgroup, TCP relay walk): the GPU suite, smoke(),
+# the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, the C3 SQ counters
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r05z
+step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r05z_c3 --rotate 8 --defer
 echo done
