@@ -126,8 +126,17 @@ class FrameBatch:
         return cls(blob_pinned, o, ln, aligned16=aligned)
 
     def c_struct(self) -> N.DkRxBatch:
-        return N.DkRxBatch(_ptr(self.blob), self.frames_bytes, _ptr(self.off), _ptr(self.len), self.n,
-                           N.DK_RX_BATCH_ALIGNED16 if self.aligned16 else 0)
+        """The ABI struct, rebuilt only when a field changed (a receive loop's per-call Python cost is what keeps a
+        ~20 us kernel fed)."""
+        key = (self.blob.data_ptr(), self.frames_bytes, self.off.data_ptr(), self.len.data_ptr(), self.n,
+               self.aligned16)
+        c = self.__dict__.get("_cs")
+        if c is None or c[0] != key:
+            c = (key, N.DkRxBatch(_ptr(self.blob), self.frames_bytes, _ptr(self.off), _ptr(self.len), self.n,
+                                  N.DK_RX_BATCH_ALIGNED16 if self.aligned16 else 0))
+            self._cs = c
+        b = c[1]
+        return N.DkRxBatch(b.frames, b.frames_bytes, b.off, b.len, b.n, b.flags)  # a copy: callers set flags
 
 
 class RxResults:
@@ -155,7 +164,13 @@ class RxResults:
             self.t["tcp_opts"] = torch.zeros(max(n, 1) * N.TCP_OPTS_DTYPE.itemsize, dtype=torch.uint8, **kw)
 
     def c_struct(self) -> N.DkRxResults:
-        return N.DkRxResults(*[_ptr(self.t.get(name)) for name in N.RESULT_FIELDS])
+        """The ABI struct, rebuilt when an array was replaced (the arrays are fixed at construction)."""
+        key = tuple(map(id, self.t.values()))
+        c = self.__dict__.get("_cs")
+        if c is None or c[0] != key:
+            c = (key, N.DkRxResults(*[_ptr(self.t.get(name)) for name in N.RESULT_FIELDS]))
+            self._cs = c
+        return c[1]
 
     def zero_counts(self) -> None:
         for k in ("flow_counts", "verdict_counts"):
@@ -235,12 +250,15 @@ class RxEngine:
                "dk_rx_process")
         # This launch completes the stream's previous deferred rows (inside its kernel) and leaves its own pending. The
         # previous arrays may be released now that the launch is queued: record_stream keeps the caching allocator
-        # from reusing their memory before the work queued on `s` (this kernel) has run.
+        # from reusing their memory before the work queued on `s` (this kernel) has run — unless they are this
+        # launch's own arrays, which stay pending (a receive loop over one result set).
+        cnt = [results.t[k] for k in ("flow_counts", "verdict_counts") if k in results.t] if defer_counts else []
+        prev = self._pending.get(s.cuda_stream)
+        if prev is not None and cnt and len(prev[0]) == len(cnt) and all(a is b for a, b in zip(prev[0], cnt)):
+            return
         self._release_pending(s)
-        if defer_counts:
-            cnt = [results.t[k] for k in ("flow_counts", "verdict_counts") if k in results.t]
-            if cnt:
-                self._pending[s.cuda_stream] = (cnt, s)
+        if cnt:
+            self._pending[s.cuda_stream] = (cnt, s)
 
     def _release_pending(self, s) -> None:
         prev = self._pending.pop(s.cuda_stream, None)

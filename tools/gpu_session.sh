@@ -16,11 +16,14 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05z: evidence at the current kernels (small kernel 8 waves per workgroup, TCP relay walk): the GPU suite, smoke(),
-# the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, the C3 SQ counters
+# r05za: receive_batch's per-call Python cost (ABI structs cached, no record_stream for the same pending arrays): the
+# GPU suite, then bench.py's C3 / C1 extras (HIP-event region vs the kernel's own duration)
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r05z
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r05z_c3 --rotate 8 --defer
+step c3 300 python -c "
+import json, torch, bench
+torch.cuda.set_device(0); s = torch.cuda.current_stream(0)
+for name, rot in (('c3_udp64', 8), ('c1_tcp1078', 3)):
+    out = bench.rx_extra(name, 0, s, steps=40, warmup=4, rotate=rot)[0]
+    print(json.dumps({'name': name, 'kernel_ms_avg': out['kernel_ms_avg'], 'frac': out['roofline']['frac'], 'gbps': out['gbps']}), flush=True)
+"
 echo done
