@@ -16,14 +16,13 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05za: receive_batch's per-call Python cost (ABI structs cached, no record_stream for the same pending arrays): the
-# GPU suite, then bench.py's C3 / C1 extras (HIP-event region vs the kernel's own duration)
+# r05zb: evidence at the current build (small kernel 8 waves per workgroup, TCP relay walk, lighter receive_batch):
+# the GPU suite, smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and
+# IMIX SQ counters
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step c3 300 python -c "
-import json, torch, bench
-torch.cuda.set_device(0); s = torch.cuda.current_stream(0)
-for name, rot in (('c3_udp64', 8), ('c1_tcp1078', 3)):
-    out = bench.rx_extra(name, 0, s, steps=40, warmup=4, rotate=rot)[0]
-    print(json.dumps({'name': name, 'kernel_ms_avg': out['kernel_ms_avg'], 'frac': out['roofline']['frac'], 'gbps': out['gbps']}), flush=True)
-"
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r05zb
+step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r05zb_c3 --rotate 8 --defer
+step pmc4 400 bash tools/pmc_kernel.sh c4_imix r05zb_c4 --rotate 2 --defer
 echo done
