@@ -16,13 +16,28 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zb: evidence at the current build (small kernel 8 waves per workgroup, TCP relay walk, lighter receive_batch):
-# the GPU suite, smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and
-# IMIX SQ counters
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r05zb
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r05zb_c3 --rotate 8 --defer
-step pmc4 400 bash tools/pmc_kernel.sh c4_imix r05zb_c4 --rotate 2 --defer
+# r05zd: the bench's ring_path_rate vs ring_bytes' ring path on the same frames and engine (which factor costs ~5 %)
+step ringq 400 python -c "
+import json, time, numpy as np, torch, bench
+from demikernel_amd import Config, RxEngine, RxResults, synth
+from demikernel_amd import ring as RG
+torch.cuda.set_device(0)
+n = 1 << 19
+flows = synth.make_flows(1024)
+tr = synth.traffic(n, np.full(n, 1486, np.uint16), flows, seed=synth.SEED + 5)
+packed, poff, lens = synth.build_numpy(tr)
+eng = RxEngine(Config(synth.BOB_IPV4)); eng.set_sockets(flows)
+def tool_like(reps=5):
+    ring, used, _, elen = RG.build_tpacket3(packed, poff.astype(np.int64), lens, 1 << 22)
+    r = RG.TpacketRing(ring, 1 << 22)
+    res = RxResults(n, len(flows), host=True)
+    nbytes = int(lens.astype(np.int64).sum()); rates = []
+    for _ in range(reps + 1):
+        t = time.perf_counter(); r.receive(eng, 0, used, res); rates.append(nbytes / (time.perf_counter() - t) / 1e9)
+    r.close()
+    return round(float(np.median(rates[1:])), 2), [round(x, 1) for x in rates]
+batch = synth.build_device(tr, eng, seed=synth.SEED + 5)
+for rep in range(3):
+    print(json.dumps({'rep': rep, 'tool_like': tool_like(), 'bench_ring': bench.ring_path_rate(eng, batch, flows, n)}), flush=True)
+"
 echo done
