@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module", params=["lane", "wave", "relay"])
 def tcp(request):
     """Every test runs through every walk: lanes = connections, one wave per connection with the parallel in-order
-    check, and 16 waves per connection relaying its state window to window (DK_TCP_WALK forces the choice the engine
+    check, and 8 waves per connection relaying its state window to window (DK_TCP_WALK forces the choice the engine
     otherwise makes from segments per connection)."""
     import os
 
@@ -231,6 +231,35 @@ def test_one_stream_gigabyte_window(tcp):
     got_t, got = gpu_process(tcp, table.copy(), rx_device(rx))
     assert_same(got_t, got, exp_t, exp, "1 conn, 1 GiB window")
     assert np.mean(got["action"] == N.A["DELIVERED"]) > 0.5
+
+
+FUZZ = [  # (seed, segments, connections, reorder, dup, oow, rare, fin, rst, buffer)
+    (1, 40000, 1, 0.0, 0.05, 0.01, 0.01, 1.0, 0.0, 1 << 30),   # one stream, many retransmissions and stray copies
+    (2, 40000, 1, 2.0, 0.02, 0.005, 0.005, 1.0, 0.0, 1 << 26),  # one reordered stream: stores and drains in runs
+    (7, 20000, 1, 0.0, 0.02, 0.005, 0.01, 1.0, 0.0, 1 << 16),   # a small window: full after ~45 segments
+    (3, 60000, 3, 1.0, 0.03, 0.0, 0.01, 0.0, 1.0, 1 << 26),     # RSTs land mid-stream
+    (4, 60000, 5, 0.5, 0.0, 0.0, 0.02, 1.0, 0.0, 1 << 22),      # rare SYN / no-ACK / unsent-ACK copies only
+    (5, 80000, 40, 4.0, 0.02, 0.01, 0.002, 0.5, 0.2, 1 << 20),  # heavy reordering: the store fills and drains
+    (6, 30000, 2, 0.0, 0.2, 0.0, 0.05, 1.0, 0.0, 1 << 24),      # a retransmission storm
+]
+
+
+@pytest.mark.parametrize("case", FUZZ, ids=[f"seed{c[0]}" for c in FUZZ])
+def test_walks_fuzzed_streams(tcp, case):
+    """Streams whose segments keep the state machine busy inside long runs (the relay walk's threshold check, its
+    epochs and its fallback; the wave walk's parallel check): retransmission storms, stray copies with SYN / without
+    ACK / with an unsent ACK, RSTs and FINs mid-batch, reordering that fills the out-of-order store, windows that
+    fill; every walk bit-exact vs the oracle on the actions, views, deliveries and the connection table."""
+    seed, n, nconns, reorder, dup, oow, rare, fin, rst, buf = case
+    _, tr, table = synth.tcp_streams(n, nconns, 1500 if seed % 2 else None, reorder=reorder, dup=dup, oow=oow,
+                                     rare=rare, fin=fin, rst=rst, buffer_size=buf, seed=500 + seed)
+    rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
+          "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
+          "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
+    exp_t = table.copy()
+    exp = O.tcp_process(exp_t, rx)
+    got_t, got = gpu_process(tcp, table.copy(), rx_device(rx))
+    assert_same(got_t, got, exp_t, exp, f"fuzz seed {seed}")
 
 
 def test_rejects_missing_tcp_fields(tcp):
