@@ -16,8 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zf: the staging kernel at 2 waves/SIMD with bigger steps (2 / 3 large rounds, 4 / 5 medium-step rounds: a chunk's
-# stream in fewer dependent steps) vs the default (3 waves/SIMD, 1 large round, 2): IMIX (2 rotating batches) and C1
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --iters 10 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/sa.so build/variants/sb.so
-step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/sa.so build/variants/sb.so
+# r05zg: the staging kernel's medium steps with one more round streamed into LDS by LDS-DMA (DK_MED_DMA=1: 12 medium
+# frames per step instead of 8, no more VGPRs) vs the default; IMIX (2 rotating batches) and C1, results compared
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --iters 10 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/md1.so
+step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --iters 20 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/md1.so
 echo done
