@@ -16,8 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zg: the staging kernel's medium steps with one more round streamed into LDS by LDS-DMA (DK_MED_DMA=1: 12 medium
-# frames per step instead of 8, no more VGPRs) vs the default; IMIX (2 rotating batches) and C1, results compared
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --iters 10 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/md1.so
-step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --iters 20 --reps 11 --check demikernel_amd/libdk_rx.so build/variants/md1.so
+# r05zh: IMIX (2 rotating batches) on the split kernel (stream + finish waves) vs the staging kernel, and the
+# contiguous schedule (sched 1) vs round-robin tiles
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --scheds 0,1 --knob DK_RX_SPLIT=0,1 --iters 10 --reps 7 demikernel_amd/libdk_rx.so
 echo done
