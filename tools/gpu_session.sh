@@ -16,7 +16,12 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zh: IMIX (2 rotating batches) on the split kernel (stream + finish waves) vs the staging kernel, and the
-# contiguous schedule (sched 1) vs round-robin tiles
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --scheds 0,1 --knob DK_RX_SPLIT=0,1 --iters 10 --reps 7 demikernel_amd/libdk_rx.so
+# r05zi: the staging kernel's tail with 32-frame halves at the end of each pool (DK_RX_TAIL_HALF, % of a pool's
+# waves): parity of the dynamic-tail test, IMIX A/B at 2 rotating batches and 1, the exit spread
+step parity 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "dynamic_tail or full_size_c4 or kernel_variants"
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --knob DK_RX_TAIL_HALF=0,25,50,100,200 --check --iters 10 --reps 7 demikernel_amd/libdk_rx.so
+step ab_imix1 300 python tools/abtest.py --workload c4_imix --rotate 1 --defer --grids 0 --knob DK_RX_TAIL_HALF=0,50,100 --iters 10 --reps 7 demikernel_amd/libdk_rx.so
+step st_h0 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail_half=0
+step st_h50 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail_half=50
+step st_h100 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail_half=100
 echo done
