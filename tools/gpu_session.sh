@@ -16,12 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zi: the staging kernel's tail with 32-frame halves at the end of each pool (DK_RX_TAIL_HALF, % of a pool's
-# waves): parity of the dynamic-tail test, IMIX A/B at 2 rotating batches and 1, the exit spread
-step parity 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "dynamic_tail or full_size_c4 or kernel_variants"
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --knob DK_RX_TAIL_HALF=0,25,50,100,200 --check --iters 10 --reps 7 demikernel_amd/libdk_rx.so
-step ab_imix1 300 python tools/abtest.py --workload c4_imix --rotate 1 --defer --grids 0 --knob DK_RX_TAIL_HALF=0,50,100 --iters 10 --reps 7 demikernel_amd/libdk_rx.so
-step st_h0 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail_half=0
-step st_h50 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail_half=50
-step st_h100 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail_half=100
+# r05zj: grids that give every wave the same number of chunks (C3: 16,384 chunks; 683 workgroups x 8 waves = 3
+# chunks each, 512 x 8 = 4 each; the rule's 768 leaves a third of the waves a chunk short) and for IMIX
+step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --knob DK_RX_GRID=-1,683,640,512,768 --iters 20 --reps 9 demikernel_amd/libdk_rx.so
+step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --knob DK_RX_GRID=-1,683,512 --iters 20 --reps 9 demikernel_amd/libdk_rx.so
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --knob DK_RX_GRID=-1,745,683,640 --iters 10 --reps 7 demikernel_amd/libdk_rx.so
 echo done
