@@ -16,9 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zj: grids that give every wave the same number of chunks (C3: 16,384 chunks; 683 workgroups x 8 waves = 3
-# chunks each, 512 x 8 = 4 each; the rule's 768 leaves a third of the waves a chunk short) and for IMIX
-step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --knob DK_RX_GRID=-1,683,640,512,768 --iters 20 --reps 9 demikernel_amd/libdk_rx.so
-step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --knob DK_RX_GRID=-1,683,512 --iters 20 --reps 9 demikernel_amd/libdk_rx.so
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --knob DK_RX_GRID=-1,745,683,640 --iters 10 --reps 7 demikernel_amd/libdk_rx.so
+# r05zk: the small-frame kernel's first window DMA issued before the LDS init and the barrier (ew1: the compiler's
+# barrier, which then waits for the DMA; ew2: a barrier that waits for LDS writes only)
+step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --check --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/ew1.so build/variants/ew2.so
+step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --check --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/ew1.so build/variants/ew2.so
 echo done
