@@ -188,7 +188,7 @@ DIAG_FUNCTIONS = [
     ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p, c_uint32]),
     ("dk_diag_tx_set_tuning", c_int, [c_int32, c_int32, c_int32]),
 ]
-DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table", "tail"]
+DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table", "tail", "udp_table"]
 
 ALL_FUNCTIONS = FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS + DEMI_FUNCTIONS + COMM_FUNCTIONS
 

@@ -81,4 +81,59 @@ inline bool build_lds_table(const std::vector<uint32_t>& slots, uint32_t cap, ui
     return true;
 }
 
+// The compact UDP bind table (rx_common.h) from the port table's kPortUdpLocal words (65,536, DK_FLOW_NONE where no
+// bind): 2 (mask + 1) words, the seed that placed every bind, and the 128-byte lines of the port table the binds' words
+// occupy (the host reads the compact table instead when that is more than it takes). Cuckoo insertion (a displaced
+// word moves to its other bucket) with up to 500 displacements per bind, seeds 0..63. Returns false (local binds stay
+// on the port table) for no binds, more than kUbMaxBinds, a flow id >= 0xFFFF, or no seed that places them all.
+inline bool build_udp_table(const uint32_t* local, std::vector<uint32_t>& out, uint32_t& mask, uint32_t& seed,
+                            uint32_t& direct_lines) {
+    std::vector<uint32_t> keys;  // port | fid << 16
+    direct_lines = 0;
+    uint32_t last_line = ~0u;
+    for (uint32_t port = 0; port < 65536; port++) {
+        const uint32_t fid = local[port];
+        if (fid == DK_FLOW_NONE) continue;
+        if (fid >= 0xFFFFu || keys.size() >= kUbMaxBinds) return false;
+        keys.push_back(port | fid << 16);
+        if (port >> 5 != last_line) direct_lines++;
+        last_line = port >> 5;
+    }
+    if (keys.empty()) return false;
+    uint32_t nb = 16;
+    while (nb < keys.size()) nb <<= 1;
+    const uint32_t m = nb - 1;
+    for (uint32_t sd = 0; sd < 64; sd++) {
+        out.assign(2 * (size_t)nb, kUbEmpty);
+        bool ok = true;
+        for (size_t k = 0; k < keys.size() && ok; k++) {
+            uint32_t e = keys[k], from = ~0u;  // from: the bucket e was displaced out of
+            for (int kick = 0;; kick++) {
+                const uint32_t h = ub_hash(e & 0xFFFFu, sd), b1 = h & m, b2 = (h >> 16) & m;
+                bool placed = false;
+                for (uint32_t b : {b1, b2})
+                    for (uint32_t w = 0; w < 2 && !placed; w++)
+                        if (out[2 * b + w] == kUbEmpty) {
+                            out[2 * b + w] = e;
+                            placed = true;
+                        }
+                if (placed) break;
+                if (kick == 500) {
+                    ok = false;
+                    break;
+                }
+                const uint32_t b = from == b1 ? b2 : b1;  // not back into the bucket it just left
+                std::swap(e, out[2 * b + (uint32_t)(kick & 1)]);
+                from = b;
+            }
+        }
+        if (ok) {
+            mask = m;
+            seed = sd;
+            return true;
+        }
+    }
+    return false;
+}
+
 }  // namespace dk

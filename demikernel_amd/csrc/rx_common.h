@@ -72,6 +72,26 @@ DK_HD uint32_t lt_bucket(uint32_t h, uint32_t nb) { return mulhi32(h, nb); }
 DK_HD uint32_t lt_slot(uint32_t h, uint32_t d, uint32_t n) { return mulhi32(fmix32(h ^ (d * 0x9E3779B1u + 0x7F4A7C15u)), n); }
 DK_HD uint32_t lt_words(uint32_t n, uint32_t nb) { return (3 * n + nb + 3) & ~3u; }
 
+// UDP binds on the configured address as a compact table (round 5). The port table's local-bind words span 256 KB:
+// binds on scattered ports put nearly every lane's load on its own line (C3 with its 1,024 binds on random ports:
+// that load was 14 % of the launch, against 1.4 % with consecutive ports; ablation, session r05zl). The compact table
+// is a two-choice cuckoo table of 2^k buckets of two words (load <= 1/2: 8 KB for 1,024 binds), word = port |
+// flow_id << 16 (flow ids < 0xFFFF; kUbEmpty empty); a port's two buckets come from one hash, h & mask and
+// (h >> 16) & mask, read together (two 8-byte LDS reads). The small-frame kernel has an instantiation that copies it
+// into LDS at the start and looks binds up there; the host launches it when the binds' port-table words span more
+// lines than the table and the copy costs no occupancy (C3 on random ports -10 %, session r05zo). Everything else
+// reads the port table.
+constexpr uint32_t kUbMaxBinds = 1u << 15;  // 2^15 buckets at most: the bucket indices are 16-bit halves of h
+constexpr uint32_t kUbEmpty = 0xFFFFFFFFu;
+DK_HD uint32_t ub_hash(uint32_t port, uint32_t seed) { return fmix32(port * 0x9E3779B1u + seed); }
+DK_HD bool ub_hit(uint32_t e, uint32_t port) { return ((e ^ port) & 0xFFFFu) == 0 && (e >> 16) != 0xFFFFu; }
+// The flow bound to `port` from the words of its two buckets (s.x, s.y: the first; s.z, s.w: the second), or
+// DK_FLOW_NONE.
+DK_HD uint32_t ub_pick(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1, uint32_t port) {
+    return ub_hit(a0, port) ? a0 >> 16 : ub_hit(a1, port) ? a1 >> 16 : ub_hit(b0, port) ? b0 >> 16
+         : ub_hit(b1, port) ? b1 >> 16 : DK_FLOW_NONE;
+}
+
 // Per-flow counting strategy (chosen per launch by the host).
 constexpr uint32_t kFlowNone = 0;    // no flow_counts requested
 constexpr uint32_t kFlowLds = 1;     // per-workgroup packed-u16 LDS histogram + scratch rows, combined per launch
@@ -130,6 +150,9 @@ struct RxParams {
     uint32_t lt_words;         // 0: Active lookups probe the global table instead
     uint32_t lt_off;           // word offset of the LDS copy in dynamic LDS (after the flow histogram)
     uint32_t lt_n, lt_b;       // keys, buckets
+    const uint32_t* ub;  // the compact UDP bind table (above) the small-frame kernel copies to dynamic LDS at word
+                         // ub_off and reads there; nullptr: the port table
+    uint32_t ub_off, ub_words, ub_mask, ub_seed;  // ub_words = 2 (ub_mask + 1)
     uint32_t nflows;
     uint32_t flow_mode;      // kFlow*
     uint32_t flow_words;     // kFlowLds: ceil(nflows / 2), else 0
@@ -173,6 +196,7 @@ struct TxParams {
 // Receive kernel families (launch_batch picks one per launch).
 namespace dk {
 constexpr uint32_t kFamilyUnstaged = 0, kFamilyStaged = 1, kFamilySplit = 2, kFamilySmall = 3;
+constexpr uint32_t kFamilySmallUb = 4;  // occupancy queries only: the small-frame kernel with the LDS bind table
 }
 int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident workgroups per CU (0 on error)
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);

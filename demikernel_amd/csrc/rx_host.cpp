@@ -70,12 +70,14 @@ struct Stage {  // device staging for one pipeline stream
 };
 
 // Tuning overrides (-1 = the host rule). Read once from the environment at dk_rx_ctx_create (DK_RX_STAGE, DK_RX_SPLIT,
-// DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID, DK_RX_GRID_PER_CU, DK_RX_DEBUG) or set by dk_diag_rx_set_tuning; never read on
-// the launch path.
+// DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID, DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE, DK_RX_TAIL, DK_RX_UDP_TABLE)
+// or set by dk_diag_rx_set_tuning; never read on the launch path.
 struct Tuning {
     int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
     int32_t lds_table = -1;  // 0: Active lookups never use the LDS table (DK_RX_LDS_TABLE)
     int32_t tail = -1;       // staged kernel's dynamic tail rounds (DK_RX_TAIL; 0 off)
+    int32_t udp_table = -1;  // small-frame kernel, local UDP binds: 0 the port table, 1 the LDS bind table whenever it
+                             // fits (DK_RX_UDP_TABLE)
     int32_t host_zc = -1;  // dk_rx_process_host: read mapped pinned frames in place (-1/1 when mapped, 0 never)
 };
 
@@ -83,11 +85,15 @@ struct Tuning {
 
 struct dk_rx_ctx {
     dk_rx_cfg cfg{};
-    uint32_t* table = nullptr;  // device: (mask + 1) * 4 u32 of Active slots, the kPortTabWords port table, then the
-                                // LDS Active table's lt_words (rx_common.h; 0 when it was not built)
+    uint32_t* table = nullptr;  // device: (mask + 1) * 4 u32 of Active slots, the kPortTabWords port table, the LDS
+                                // Active table's lt_words, then the compact UDP bind table's ub_words (rx_common.h; 0
+                                // when not built)
     uint32_t table_mask = 0;
     uint32_t lt_n = 0, lt_b = 0, lt_words = 0;
     uint32_t lt_occ_dyn = ~0u, lt_occ_family = ~0u, lt_occ_blocks = 0;  // occupancy cache with the LDS table
+    uint32_t ub_words = 0, ub_seed = 0;  // the compact UDP bind table (rx_common.h; 0 words: not built)
+    bool ub_scattered = false;  // the local binds' port-table words span more lines than the compact table
+    uint32_t ub_occ_dyn = ~0u, ub_occ_blocks = 0;  // small-kernel occupancy cache with the table in LDS
     uint32_t nflows = 0;
     // host pipeline state (lazily allocated)
     Stage stages[kPipeStreams];
@@ -143,6 +149,9 @@ int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask
     c->table_mask = mask;
     c->lt_n = c->lt_b = c->lt_words = 0;
     c->lt_occ_family = ~0u;
+    c->ub_words = 0;
+    c->ub_scattered = false;
+    c->ub_occ_dyn = ~0u;
     return 0;
 }
 
@@ -323,6 +332,21 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
             dyn = dyn2;
         }
     }
+    // Local UDP binds (rx_common.h): the small-frame kernel's instantiation with the compact bind table in LDS when the
+    // binds' port-table words are scattered and the table costs no occupancy; else the port table.
+    if (c->ub_words && p.small && (T.udp_table > 0 || (T.udp_table < 0 && c->ub_scattered))) {
+        const uint32_t off = (dyn / 4 + 3) & ~3u;
+        const uint32_t dyn2 = (off + c->ub_words) * 4;
+        if (c->ub_occ_dyn != dyn2) {
+            c->ub_occ_blocks = (uint32_t)std::max(dk_rx_resident_blocks(dyn2, dk::kFamilySmallUb), 0);
+            c->ub_occ_dyn = dyn2;
+        }
+        if (std::min(c->ub_occ_blocks, fam_cap) >= per_cu) {
+            p.ub = c->table + (size_t)(c->table_mask + 1) * 4 + dk::kPortTabWords + c->lt_words;
+            p.ub_off = off;
+            dyn = dyn2;
+        }
+    }
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
     const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
@@ -379,9 +403,10 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.defer_rows = defer && p.row_words ? 1u : 0u;
     if (T.debug > 0)
         fprintf(stderr, "dk_rx: n=%u tiles=%u grid=%u occ=%u cus=%u flow_mode=%u words=%u sched=%u stage=%u split=%u "
-                        "small=%u lds_table=%u defer=%u combine=%u tail_ks=%u\n",
+                        "small=%u lds_table=%u defer=%u combine=%u tail_ks=%u udp_table=%u\n",
                 p.n, ntiles, grid, c->occ_blocks, c->cu_count, p.flow_mode, p.flow_words, p.sched, p.stage, p.split,
-                p.small, p.lt_words ? p.lt_n : 0u, p.defer_rows, p.comb.nblk, p.tail_ks);
+                p.small, p.lt_words ? p.lt_n : 0u, p.defer_rows, p.comb.nblk, p.tail_ks,
+                p.ub ? 1u : 0u);
     rc = dk_launch_rx(p, grid, stream);
     if (rc == 0 && cs && p.tail_ks) cs->tail_set ^= 1u;  // this launch zeroed the other set for the next one
     if (rc == 0 && cs) {
@@ -471,6 +496,11 @@ dk::RxParams base_params(const dk_rx_ctx* c) {
     p.lt_words = p.lt_off = 0;
     p.lt_n = c->lt_n;
     p.lt_b = c->lt_b;
+    p.ub = nullptr;
+    p.ub_off = 0;
+    p.ub_words = c->ub_words;
+    p.ub_mask = c->ub_words ? c->ub_words / 2 - 1 : 0u;
+    p.ub_seed = c->ub_seed;
     p.nflows = c->nflows;
     return p;
 }
@@ -517,6 +547,7 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     t.host_zc = env_knob("DK_RX_HOST_ZC");
     t.lds_table = env_knob("DK_RX_LDS_TABLE");
     t.tail = env_knob("DK_RX_TAIL");
+    t.udp_table = env_knob("DK_RX_UDP_TABLE");
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
     std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
@@ -601,6 +632,14 @@ int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
             slots.insert(slots.end(), lt.begin(), lt.end());
         }
     }
+    uint32_t ub_mask = 0, ub_seed = 0, ub_lines = 0, ub_w = 0;
+    {
+        std::vector<uint32_t> ub;
+        if (dk::build_udp_table(slots.data() + (size_t)cap * 4 + dk::kPortUdpLocal, ub, ub_mask, ub_seed, ub_lines)) {
+            ub_w = (uint32_t)ub.size();
+            slots.insert(slots.end(), ub.begin(), ub.end());
+        }
+    }
     DeviceGuard g(c->cfg.device);
     int rc = upload_table(c, slots, mask);
     if (rc == 0) {
@@ -608,6 +647,10 @@ int dk_rx_flow_table_set(dk_rx_ctx* c, const dk_flow* flows, uint32_t n) {
         c->lt_n = lt_n;
         c->lt_b = lt_b;
         c->lt_words = lt_w;
+        c->ub_words = ub_w;
+        c->ub_seed = ub_seed;
+        c->ub_scattered = ub_w && ub_lines > ub_w / 32;  // 32 words per 128-byte line
+        c->ub_occ_dyn = ~0u;
     }
     return rc;
 }
@@ -847,6 +890,7 @@ int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t* knobs, uint32_t nknobs) {
     t.debug = k[6] < 0 ? 0 : k[6];
     t.lds_table = k[7];
     t.tail = k[8];
+    t.udp_table = k[9];
     t.host_zc = zc;
     c->tune = t;
     c->occ_family = ~0u;

@@ -390,12 +390,36 @@ __device__ __forceinline__ uint32_t probe_finish(const RxParams& P, const ProbeK
 __device__ __forceinline__ uint32_t port_lookup(const RxParams& P, uint32_t base, uint32_t port) {
     return P.port_tab[base + port];
 }
+// The bind on (local_ip, port), issued ahead of the checksum work: kUb (the small-frame kernel's instantiation with
+// the compact bind table in LDS, rx_common.h) its two buckets' words in s, else the port table's word in s.x;
+// udp_local_finish reads the flow id out once it is needed.
+extern __shared__ __attribute__((aligned(16))) uint32_t dk_dyn_lds[];
+template <bool kUb>
+__device__ __forceinline__ void udp_local_issue(const RxParams& P, uint32_t port, uint4& s) {
+    if (kUb) {
+        const uint2* T = reinterpret_cast<const uint2*>(dk_dyn_lds + P.ub_off);
+        const uint32_t h = ub_hash(port, P.ub_seed);
+        const uint2 a = T[h & P.ub_mask], b = T[(h >> 16) & P.ub_mask];
+        s = make_uint4(a.x, a.y, b.x, b.y);
+    } else {
+        s.x = P.port_tab[kPortUdpLocal + port];
+    }
+}
+template <bool kUb>
+__device__ __forceinline__ uint32_t udp_local_finish(uint32_t port, const uint4& s) {
+    return kUb ? ub_pick(s.x, s.y, s.z, s.w, port) : s.x;
+}
+// The LDS copy of the compact bind table (before the workgroup's first barrier).
+__device__ __forceinline__ void ub_load(const RxParams& P, uint32_t tid, uint32_t nthreads) {
+    const uint4* src = reinterpret_cast<const uint4*>(P.ub);
+    uint4* dst = reinterpret_cast<uint4*>(dk_dyn_lds + P.ub_off);
+    for (uint32_t k = tid; k < P.ub_words / 4; k += nthreads) dst[k] = src[k];
+}
 
 // The LDS Active table (rx_common.h): copied from global memory at the kernel start (before the workgroup's first
 // barrier), then a lookup is two dependent LDS reads and a key compare. Returns the slot the global probe would have
 // hit first ({kind << 24 | flow_id, local_ip, remote_ip, ports}), or zeros (an empty slot: probe_finish stops there,
 // and the Passive lookup follows as it would after a miss in the global table).
-extern __shared__ __attribute__((aligned(16))) uint32_t dk_dyn_lds[];
 __device__ __forceinline__ void lt_load(const RxParams& P, uint32_t tid, uint32_t nthreads) {
     const uint4* src = reinterpret_cast<const uint4*>(P.lt);
     uint4* dst = reinterpret_cast<uint4*>(dk_dyn_lds + P.lt_off);
@@ -831,7 +855,7 @@ struct FinState {
     uint4 s1;
     bool fast, resum, big, inb;
 };
-template <bool kShift, class WL>
+template <bool kShift, class WL, bool kUb = false>
 __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t lane, WL& W, uint32_t off,
                                          uint32_t len, const Chunk& C, FinState& St, uint32_t stamp_base = ~0u) {
     Lane& L = St.L;
@@ -872,13 +896,13 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
         h1 = probe_slot(P, k1);
         St.s1 = reinterpret_cast<const uint4*>(P.table)[h1];
     }
-    if (L.v == kPendUdp) St.s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+    if (L.v == kPendUdp) udp_local_issue<kUb>(P, L.ports >> 16, St.s1);
     St.h1 = h1;
     if (L.need) L.lsum = fast ? seg_sum_fast(C, W, lane, f, (int)L.E, resum) : MemAcc{f}.sum_le16(L.S, L.E);
     DK_SUB_STAMP(1);
 }
 
-template <bool kStage, bool kOpt = true, bool kNtRes = false, bool kTcpStaged = false>
+template <bool kStage, bool kOpt = true, bool kNtRes = false, bool kTcpStaged = false, bool kUb = false>
 __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live, uint32_t lane, uint32_t off,
                                         FinState& St, uint32_t& v_out, uint32_t& fid_out, Rec& rec,
                                         uint32_t stamp_base = ~0u) {
@@ -923,7 +947,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
             L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
         } else if (L.v == kPendUdp) {
             // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
-            fid = s1.x;  // (local_ip, port)
+            fid = udp_local_finish<kUb>(dport, s1);  // (local_ip, port)
             if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortUdpAny, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
         }
@@ -973,13 +997,14 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
     fid_out = fid;
 }
 
-template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false, bool kTcpStaged = false>
+template <bool kShift, bool kStage, class WL, bool kOpt = true, bool kNtRes = false, bool kTcpStaged = false,
+          bool kUb = false>
 __device__ __forceinline__ void rx_finish(const RxParams& P, uint32_t i, bool live, uint32_t lane, WL& W,
                                           uint32_t off, uint32_t len, const Chunk& C, uint32_t& v_out,
                                           uint32_t& fid_out, Rec& rec, uint32_t stamp_base = ~0u) {
     FinState St;
-    rx_front<kShift>(P, live, lane, W, off, len, C, St, stamp_base);
-    rx_back<kStage, kOpt, kNtRes, kTcpStaged>(P, i, live, lane, off, St, v_out, fid_out, rec, stamp_base);
+    rx_front<kShift, WL, kUb>(P, live, lane, W, off, len, C, St, stamp_base);
+    rx_back<kStage, kOpt, kNtRes, kTcpStaged, kUb>(P, i, live, lane, off, St, v_out, fid_out, rec, stamp_base);
 }
 
 // Schedule of one wave (host-chosen per launch, measured in DESIGN.md "Tuning log"). Chunk k of a wave holds the
@@ -1319,9 +1344,20 @@ void dk_rx_kernel(RxParams P) {
 // reads its frame's 64 bytes back; scattered frames (e.g. one per 2 KiB mbuf) keep the per-lane loads.
 constexpr uint32_t kWinGran = 288;                    // 4.5 KiB: 64 packed 64-byte frames at any even offset
 constexpr uint32_t kWinLoads = (kWinGran + 63) / 64;  // DMA loads for a full window
+// kUb: the last granules share the window's LDS (the general pass runs after the main loop's last window), leaving
+// room for the LDS bind table at three workgroups per CU; measured 3 % slower at C3 with the port table, so the
+// instantiation without the table keeps them apart (session r05zo).
+template <bool kUb>
 struct SmallLds {
-    uint4 tail[64];              // the last granule of each big frame (seg_sum_fast)
-    uint4 win[kWinLoads * 64];   // the chunk's frame window (whole 1 KiB DMA pieces)
+    uint4 tail[64];             // the general pass: the last granule of each big frame (seg_sum_fast)
+    uint4 win[kWinLoads * 64];  // the main loop: the chunk's frame window (whole 1 KiB DMA pieces)
+};
+template <>
+struct SmallLds<true> {
+    union {
+        uint4 win[kWinLoads * 64];
+        uint4 tail[64];
+    };
 };
 #ifndef DK_MIN_WAVES_SMALL
 #define DK_MIN_WAVES_SMALL 6  // 80 VGPRs, no spills since round 5 (lane id re-materialised per chunk, uniform wave
@@ -1473,7 +1509,7 @@ __device__ __forceinline__ bool small_fast_eligible(const FrameDesc<kShift>& F, 
     const bool topt = R.b8(23) == 6u && (R.b8(46) >> 4) > 5u;
     return F.vec && !F.big && len >= 34 && ihl5 && !arp && !topt;
 }
-template <bool kOpt>
+template <bool kOpt, bool kUb>
 __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool live, uint32_t lane, const RegAcc& R,
                                            uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
     Lane L;
@@ -1490,7 +1526,7 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
         h1 = probe_slot(P, k1);
         s1 = reinterpret_cast<const uint4*>(P.table)[h1];
     }
-    if (L.v == kPendUdp) s1.x = P.port_tab[kPortUdpLocal + (L.ports >> 16)];
+    if (L.v == kPendUdp) udp_local_issue<kUb>(P, L.ports >> 16, s1);
     uint32_t lsum = 0;
     if (L.need) {  // LE-half sum of frame bytes [34, E), E <= 64: the window (seg_sum_fast's small-frame forms)
         if (!__ballot(L.E != 64u)) {
@@ -1529,7 +1565,7 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
             if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortTcpPassive, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_TCP_NOSOCK : DK_V_OK_TCP;
         } else if (L.v == kPendUdp) {  // (local_ip, dport), then (0.0.0.0, dport) (udp/peer.rs:147-165)
-            fid = s1.x;
+            fid = udp_local_finish<kUb>(dport, s1);
             if (fid == DK_FLOW_NONE) fid = port_lookup(P, kPortUdpAny, dport);
             L.v = fid == DK_FLOW_NONE ? DK_V_UDP_NOSOCK : DK_V_OK_UDP;
         }
@@ -1560,9 +1596,9 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
     fid_out = fid;
 }
 
-template <bool kShift, bool kOpt>
+template <bool kShift, bool kOpt, bool kUb = false>
 __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
-    __shared__ SmallLds s_wave[kSmallWaves];
+    __shared__ SmallLds<kUb> s_wave[kSmallWaves];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
 
@@ -1589,6 +1625,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     for (uint32_t k = tid; k < DK_V_COUNT; k += kSmallBlock) s_vh[k] = 0;
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
+    if (kUb) ub_load(P, tid, kSmallBlock);
     __syncthreads();
     DK_STAMP(11);
     // The grid is one generation of waves and the chunks do not divide evenly: the waves with one chunk more than the
@@ -1599,7 +1636,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         if (r.chunk(P.small_kmin, cc, ll)) __builtin_amdgcn_s_setprio(DK_SMALL_PRIO);  // (host: chunks / waves)
     }
     const Blob B(P.frames, P.frames_bytes);
-    SmallLds& W = s_wave[wv];
+    SmallLds<kUb>& W = s_wave[wv];
     // Pipeline: descriptors are loaded two chunks ahead. Chunk k + 2's descriptor loads are issued before chunk k's
     // window DMA, so the window's wait covers them, and chunk k's deferral mask is stored after its result stores and
     // only when the chunk left frames (`had`), so it sits behind the next window's wait. (Issued after the window,
@@ -1636,7 +1673,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         const bool take = live && small_fast_eligible(F, len, C.R);
         const uint64_t dm = __ballot(live && !take);
         deferred = deferred || dm != 0;
-        small_fast<kOpt>(P, i, take, lane, C.R, len, v, fid);
+        small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid);
         if (k < 3) DK_STAMP(3 + 3 * k);
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
@@ -1673,7 +1710,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
             uint32_t v, fid;
             Rec rec;
             rec.meta = kNoRec;
-            rx_finish<kShift, false, SmallLds, kOpt, true>(P, i, mine, lane, W, o, ln, C, v, fid, rec);
+            rx_finish<kShift, false, SmallLds<kUb>, kOpt, true, false, kUb>(P, i, mine, lane, W, o, ln, C, v, fid, rec);
             count_chunk(P, mine, lane, v, fid, lds_flows, s_flow, s_vh);
         }
     }
@@ -2160,6 +2197,9 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     else if (family == dk::kFamilySmall)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kSmallBlock,
                                                           dyn_lds_bytes);
+    else if (family == dk::kFamilySmallUb)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true, true>,
+                                                          dk::kSmallBlock, dyn_lds_bytes);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &blocks, family == dk::kFamilyStaged ? dk::dk_rx_kernel<true, true> : dk::dk_rx_kernel<true, false>,
@@ -2171,12 +2211,21 @@ uint32_t dk_rx_small_block_waves() { return dk::kSmallWaves; }
 
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
-    const size_t dyn = p.lt_words ? (size_t)(p.lt_off + p.lt_words) * 4
-                       : p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
+    size_t dyn = p.lt_words ? (size_t)(p.lt_off + p.lt_words) * 4
+                 : p.flow_mode == dk::kFlowLds ? (size_t)p.flow_words * 4 : 0;
+    if (p.ub) dyn = std::max(dyn, (size_t)(p.ub_off + p.ub_words) * 4);
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
     const bool tcp = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win;  // the split kernel stages the TCP fields
-    if (p.small && p.aligned16 && opt)
+    if (p.small && p.ub && p.aligned16 && opt)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small && p.ub && p.aligned16)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small && p.ub && opt)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small && p.ub)
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+    else if (p.small && p.aligned16 && opt)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
     else if (p.small && p.aligned16)
         hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);

@@ -310,7 +310,7 @@ class RxEngine:
     def set_tuning(self, **knobs) -> None:
         """Diagnostics (dk_diag.h): override the engine's kernel family / schedule / grid choices (-1 = its rule);
         unnamed knobs go back to the rule. Names: N.DK_DIAG_RX_KNOBS (stage, split, small, sched, grid, grid_per_cu, debug,
-        lds_table)."""
+        lds_table, tail, udp_table)."""
         bad = set(knobs) - set(N.DK_DIAG_RX_KNOBS)
         assert not bad, bad
         arr = (ctypes.c_int32 * len(N.DK_DIAG_RX_KNOBS))(*[int(knobs.get(k, -1)) for k in N.DK_DIAG_RX_KNOBS])

@@ -29,13 +29,15 @@ int dk_diag_path_stats_read(struct dk_rx_ctx* ctx, uint64_t out[4]); /* synchron
 
 /* Tuning overrides for A/B measurements and tests (-1 = the engine's own rule). A receive context reads them once from
  * the environment when it is created (DK_RX_STAGE, DK_RX_SPLIT, DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID,
- * DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE, DK_RX_TAIL), never on the launch path; this call replaces them.
- * knobs[] = {stage, split, small, sched, grid, grid_per_cu, debug, lds_table, tail}: stage/split/small force a kernel
- * family on (1) or off (0), sched picks the wave schedule (0 round-robin tiles, 1 one contiguous share per wave),
- * grid / grid_per_cu fix the persistent grid, debug > 0 prints each launch's choice to stderr, lds_table 0 keeps Active
- * lookups on the global socket table (no LDS copy), tail sets the staged kernel's dynamic tail (0 off, d > 0: the
- * last ~d rounds of chunks handed out by per-XCD counters instead of round-robin). */
-#define DK_DIAG_RX_KNOBS 9
+ * DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE, DK_RX_TAIL, DK_RX_UDP_TABLE), never on the launch path; this call
+ * replaces them. knobs[] = {stage, split, small, sched, grid, grid_per_cu, debug, lds_table, tail, udp_table}:
+ * stage/split/small force a kernel family on (1) or off (0), sched picks the wave schedule (0 round-robin tiles, 1 one
+ * contiguous share per wave), grid / grid_per_cu fix the persistent grid, debug > 0 prints each launch's choice to
+ * stderr, lds_table 0 keeps Active lookups on the global socket table (no LDS copy), tail sets the staged kernel's
+ * dynamic tail (0 off, d > 0: the last ~d rounds of chunks handed out by per-XCD counters instead of round-robin),
+ * udp_table 0 / 1: the small-frame kernel looks local UDP binds up in the port table / in its LDS bind table whenever
+ * that fits (the rule: when the binds are scattered over the port table). */
+#define DK_DIAG_RX_KNOBS 10
 /* knobs[0 .. nknobs): the caller says how many it passes (knobs past nknobs are -1, the rule), so a caller built
  * against an older, shorter list never has its array read past its end. 0 or EINVAL. */
 int dk_diag_rx_set_tuning(struct dk_rx_ctx* ctx, const int32_t* knobs, uint32_t nknobs);

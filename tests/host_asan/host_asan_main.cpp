@@ -186,11 +186,25 @@ int do_ltable() {
     if (ok) wr(words.data(), words.size());
     return 0;
 }
+// utable: 65,536 port-table words (kPortUdpLocal) -> ok, mask, seed, direct lines, then the table's slots.
+int do_utable() {
+    std::vector<uint32_t> local(65536);
+    rd(local.data(), local.size());
+    std::vector<uint32_t> words;
+    uint32_t mask = 0, seed = 0, lines = 0;
+    const bool ok = dk::build_udp_table(local.data(), words, mask, seed, lines);
+    wr1<int32_t>(ok ? 1 : 0);
+    wr1<uint32_t>(ok ? mask : 0);
+    wr1<uint32_t>(ok ? seed : 0);
+    wr1<uint32_t>(lines);
+    if (ok) wr(words.data(), words.size());
+    return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
     if (argc != 4) {
-        fprintf(stderr, "usage: %s ring|release|udp|tcp|plan|ltable in out\n", argv[0]);
+        fprintf(stderr, "usage: %s ring|release|udp|tcp|plan|ltable|utable in out\n", argv[0]);
         return 2;
     }
     g_in = fopen(argv[2], "rb");
@@ -198,7 +212,7 @@ int main(int argc, char** argv) {
     if (!g_in || !g_out) return 2;
     const char* m = argv[1];
     int rc = !strcmp(m, "ring") ? do_ring(false) : !strcmp(m, "release") ? do_ring(true) : !strcmp(m, "udp") ? do_udp()
-             : !strcmp(m, "tcp") ? do_tcp() : !strcmp(m, "plan") ? do_plan() : !strcmp(m, "ltable") ? do_ltable() : 2;
+             : !strcmp(m, "tcp") ? do_tcp() : !strcmp(m, "plan") ? do_plan() : !strcmp(m, "ltable") ? do_ltable() : !strcmp(m, "utable") ? do_utable() : 2;
     fclose(g_out);
     fclose(g_in);
     return rc;

@@ -417,6 +417,43 @@ def test_port_table_lookups(torch_cuda, local):
     assert {"OK_UDP", "UDP_NOSOCK", "OK_TCP", "TCP_NOSOCK"} <= seen, seen
 
 
+@pytest.mark.parametrize("family", ["small", "staged", "split", "unstaged"])
+@pytest.mark.parametrize("udp_table", ["0", "1", "-1"])
+def test_udp_bind_table(torch_cuda, monkeypatch, capfd, family, udp_table):
+    """Local UDP binds looked up in the small-frame kernel's LDS bind table (rx_common.h: a two-choice cuckoo table
+    built from the port table; its window and the general pass's last granules then share LDS) or in the port table:
+    forced off (0), whenever it fits (1) and by the host's rule (1,024 binds on random ports: the table), in every
+    kernel family (the others always read the port table): the binds (port 65535 among them), binds on 0.0.0.0 and on
+    another address, a duplicate (the last wins), unbound ports and a TCP share, 3 % corrupted, 64-byte frames for the
+    small-frame kernel and IMIX sizes for the others; bit-exact vs the oracle. The debug line shows the host's choice."""
+    from demikernel_amd._native import DK_FLOW_UDP as UDP
+
+    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
+    monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
+    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
+    monkeypatch.setenv("DK_RX_UDP_TABLE", udp_table)
+    monkeypatch.setenv("DK_RX_DEBUG", "1")
+    lip = ipv4(LOCAL)
+    binds = synth.make_flows(1024, kind="udp_random_ports", seed=31)
+    binds["local_port"][7] = 65535
+    extra = np.array([(UDP, 0, 0, int(binds["local_port"][3]), 0), (UDP, 0, 0, 999, 0),
+                      (UDP, ipv4("10.9.9.9"), 0, 1000, 0), (UDP, lip, 0, int(binds["local_port"][5]), 0)],
+                     dtype=FLOW_DTYPE)
+    flows = np.concatenate([binds, extra, synth.make_flows(50)])
+    unbound = np.array([(UDP, lip, 0, p, 0) for p in (999, 1000, 1001, 2, 64000)], dtype=FLOW_DTYPE)
+    targets = np.concatenate([flows, unbound])
+    n = 30000
+    ip_len = 50 if family == "small" else synth.imix_ip_lengths(n, seed=32)
+    tr = synth.traffic(n, ip_len, targets, seed=33)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
+    got = check(blob, off, lens, flows, ctx=f"udp table {family} {udp_table}")
+    seen = {VERDICTS[m & 0xFF] for m in got["meta"]}
+    assert {"OK_UDP", "UDP_NOSOCK", "OK_TCP"} <= seen, seen
+    modes = {int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("udp_table=")}
+    assert modes == {1 if family == "small" and udp_table != "0" else 0}, modes
+
+
 def tx_check(blob, off, lens, ctx=""):
     """dk_tx_checksum on the GPU vs the oracle's serialize_and_attach restatement, frame by frame, whole blob."""
     import torch

@@ -376,3 +376,61 @@ def test_lds_table_builder(driver, tmp_path):
         ok, *_ = _ltable(driver, tmp_path, extra + [(r1, p1, 1), (r2, p2, 2)], cfg)
         assert ok == 0 and time.perf_counter() - t < 20
     assert _ltable(driver, tmp_path, [(r1, p1, 1), (r1, p1, 2)], cfg)[0] == 0  # duplicated key
+
+
+def _ub_hash(port, seed):
+    h = (port * 0x9E3779B1 + seed) & 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
+def _ub_lookup(words, mask, seed, port):
+    """rx_common.h ub_pick over the words of the port's two buckets."""
+    h = _ub_hash(port, seed)
+    b1, b2 = h & mask, (h >> 16) & mask
+    for e in (int(words[2 * b1]), int(words[2 * b1 + 1]), int(words[2 * b2]), int(words[2 * b2 + 1])):
+        if (e ^ port) & 0xFFFF == 0 and e >> 16 != 0xFFFF:
+            return e >> 16
+    return None
+
+
+def test_udp_bind_table_builder(driver, tmp_path):
+    """The compact UDP bind table (rx_common.h, lds_table.h build_udp_table: two-word buckets, load <= 1/2) from
+    port-table words: 1..32,768 binds on consecutive and random ports (ports 0 and 65535 included), every bind found at
+    its flow id and no unbound port found; the line count that picks it; refused for no binds, 32,769 binds and a flow
+    id >= 0xFFFF."""
+    rng = np.random.default_rng(7)
+    none = 0xFFFFFFFF
+
+    def build(local):
+        out = run(driver, "utable", np.asarray(local, np.uint32).tobytes(), tmp_path)
+        ok, mask, seed, lines = np.frombuffer(out[:16], np.uint32)
+        return int(ok), int(mask), int(seed), int(lines), np.frombuffer(out[16:], np.uint32)
+
+    for nb, spread in ((1, False), (3, True), (1024, False), (1024, True), (5000, True), (32768, True)):
+        local = np.full(65536, none, np.uint32)
+        ports = (rng.permutation(65536)[:nb] if spread else 5000 + np.arange(nb)).astype(np.int64)
+        if spread and nb > 2:
+            ports[0], ports[1] = 65535, 0
+            ports = np.unique(ports)
+        fids = rng.permutation(0xFFFF)[:len(ports)]
+        local[ports] = fids
+        ok, mask, seed, lines, words = build(local)
+        assert ok and len(words) == 2 * (mask + 1) and mask + 1 >= len(ports) and (mask + 1) & mask == 0, (nb, ok, mask)
+        assert lines == len(set(int(p) >> 5 for p in ports)), (nb, lines)
+        for p, f in zip(ports, fids):
+            assert _ub_lookup(words, mask, seed, int(p)) == int(f), (nb, p)
+        bound = set(int(p) for p in ports)
+        for p in rng.integers(0, 65536, 300):
+            if int(p) not in bound:
+                assert _ub_lookup(words, mask, seed, int(p)) is None
+    assert build(np.full(65536, none, np.uint32))[0] == 0
+    local = np.full(65536, none, np.uint32)
+    local[:32769] = np.arange(32769)
+    assert build(local)[0] == 0
+    local = np.full(65536, none, np.uint32)
+    local[80] = 0xFFFF
+    assert build(local)[0] == 0

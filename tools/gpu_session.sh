@@ -16,8 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zk: the small-frame kernel's first window DMA issued before the LDS init and the barrier (ew1: the compiler's
-# barrier, which then waits for the DMA; ew2: a barrier that waits for LDS writes only)
-step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --check --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/ew1.so build/variants/ew2.so
-step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --check --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/ew1.so build/variants/ew2.so
+# r05zp: the LDS bind table as its own small-frame kernel instantiation (the port-table one as HEAD's): the parity
+# file, then C3 / C3 on random ports, HEAD's library vs this build (rule, table forced off)
+step parity 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py
+step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --knob DK_RX_UDP_TABLE=-1,0 --check --iters 20 --reps 11 build/variants/head.so demikernel_amd/libdk_rx.so
+step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --knob DK_RX_UDP_TABLE=-1,0 --check --iters 20 --reps 11 build/variants/head.so demikernel_amd/libdk_rx.so
 echo done
