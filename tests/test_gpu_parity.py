@@ -454,6 +454,23 @@ def test_udp_bind_table(torch_cuda, monkeypatch, capfd, family, udp_table):
     assert modes == {1 if family == "small" and udp_table != "0" else 0}, modes
 
 
+@pytest.mark.parametrize("nbinds,want", [(16, 1), (512, 1), (2048, 0)])
+def test_udp_bind_table_fit(torch_cuda, monkeypatch, capfd, nbinds, want):
+    """The host's rule for the small-frame kernel's LDS bind table: binds on random ports take it while it fits at the
+    occupancy the kernel has without it (16 and 512 binds: 128 B and 4 KiB), and not when it would cost a workgroup per
+    CU (2,048 binds: 16 KiB beside the flow histogram); bit-exact vs the oracle either way."""
+    monkeypatch.setenv("DK_RX_SMALL", "1")
+    monkeypatch.setenv("DK_RX_DEBUG", "1")
+    flows = synth.make_flows(nbinds, kind="udp_random_ports", seed=nbinds)
+    n = 20000
+    tr = synth.traffic(n, 50, flows, seed=nbinds + 1)
+    blob, off, lens = synth.build_numpy(tr)
+    synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr))
+    check(blob, off, lens, flows, ctx=f"udp bind table fit {nbinds}")
+    modes = {int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("udp_table=")}
+    assert modes == {want}, modes
+
+
 def tx_check(blob, off, lens, ctx=""):
     """dk_tx_checksum on the GPU vs the oracle's serialize_and_attach restatement, frame by frame, whole blob."""
     import torch

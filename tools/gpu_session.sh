@@ -16,9 +16,12 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zp: the LDS bind table as its own small-frame kernel instantiation (the port-table one as HEAD's): the parity
-# file, then C3 / C3 on random ports, HEAD's library vs this build (rule, table forced off)
-step parity 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py
-step ab_c3 300 python tools/abtest.py --workload c3_udp64 --rotate 8 --defer --grids 0 --knob DK_RX_UDP_TABLE=-1,0 --check --iters 20 --reps 11 build/variants/head.so demikernel_amd/libdk_rx.so
-step ab_c3r 300 python tools/abtest.py --workload c3_udp64_random_ports --rotate 8 --defer --grids 0 --knob DK_RX_UDP_TABLE=-1,0 --check --iters 20 --reps 11 build/variants/head.so demikernel_amd/libdk_rx.so
+# r05zq: evidence at the current build (small-frame kernel's LDS bind table for scattered binds): the GPU suite,
+# smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r05zq
+step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r05zq_c3 --rotate 8 --defer
+step pmc4 400 bash tools/pmc_kernel.sh c4_imix r05zq_c4 --rotate 2 --defer
 echo done
