@@ -717,14 +717,48 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
 // the baton's state (the store moving between LDS and lane registers) before the baton moves on. 1 connection, 1M
 // in-order segments: 4.2 ms against 12.7 ms for the one-wave walk (session r05r).
 constexpr uint32_t kRelayWavesMax = 16;  // waves per connection (DK_TCP_RELAY_WAVES = 4 | 8 | 16)
-struct Baton {
-    uint32_t state, rn, nooo, front;  // front: the store's first entry's start (nooo > 0)
-    uint32_t fin_pending, fin_seq, n, open_until;  // n: deliveries so far
-    uint32_t turn;                                 // the window whose owner holds the baton
+struct alignas(16) Baton {
+    uint32_t turn;   // the window whose owner holds the baton
     uint32_t epoch;  // bumped by every window that went through the state machine (state, store, FIN may change)
+    uint32_t rn, n;  // n: deliveries so far
+    uint32_t state, nooo, front;  // front: the store's first entry's start (nooo > 0)
+    uint32_t fin_pending, fin_seq, open_until;
 };
 __device__ __forceinline__ uint32_t lds_relaxed(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// The fast hand-off relies on the LDS executing one wave's LDS instructions in issue order (the same order the
+// LGKM counter retires them in): a holder that writes {rn, n} and then turn, as two back-to-back instructions, cannot
+// have turn seen before {rn, n}; a waiter that reads turn and then {epoch, rn, n} in one poll gets, once turn shows
+// its window, values at least as new as the holder's. One LDS round trip each way instead of a wait for the stores
+// before a release store and a read after an acquire poll.
+__device__ __forceinline__ void baton_poll(const Baton* bt, uint32_t& turn, uint32_t& epoch, uint32_t& rn,
+                                           uint32_t& n) {
+    const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(bt);
+    uint32_t t, e;
+    uint2 rv;
+    asm volatile(
+        "ds_read_b32 %0, %3\n\t"
+        "ds_read_b32 %1, %3 offset:4\n\t"
+        "ds_read_b64 %2, %3 offset:8\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(t), "=v"(e), "=v"(rv)
+        : "v"(a)
+        : "memory");
+    turn = DK_U(t);
+    epoch = DK_U(e);
+    rn = DK_U(rv.x);
+    n = DK_U(rv.y);
+}
+__device__ __forceinline__ void baton_pass(Baton* bt, uint32_t turn, uint32_t rn, uint32_t n) {  // one lane
+    const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(bt);
+    const uint2 rv = make_uint2(rn, n);
+    asm volatile(
+        "ds_write_b64 %0, %1 offset:8\n\t"
+        "ds_write_b32 %0, %2"
+        :
+        : "v"(a), "v"(rv), "v"(turn)
+        : "memory");
 }
 
 template <uint32_t kRelayWaves>
@@ -749,8 +783,8 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
             sto[3][lane] = e.len;
         }
         if (lane == 0)
-            bt = Baton{state, rn0, nooo, nooo ? t->ooo_start[0] : 0u, t->fin_pending, t->fin_seq, 0u,
-                       state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u, 0u, 0u};
+            bt = Baton{0u, 0u, rn0, 0u, state, nooo, nooo ? t->ooo_start[0] : 0u, t->fin_pending, t->fin_seq,
+                       state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u};
     }
     __syncthreads();
     const uint32_t nwin = (uint32_t)(((uint64_t)cnt + kWave - 1) / kWave), last = cnt ? cnt - 1 : 0u;
@@ -825,18 +859,18 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
         const int E = synd ? er + 1 : dr;  // a candidate's end
         const bool deliv0 = (cand || synd) && pmi < E;
         // wait for the baton: the next wave in line spins, the others sleep between polls
-        for (uint32_t tv; (tv = __hip_atomic_load(&bt.turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != v;)
+        uint32_t tv, ep, rn_now, n_now;
+        for (;;) {
+            baton_poll(&bt, tv, ep, rn_now, n_now);
+            if (tv == v) break;
             if (v - tv > 1) __builtin_amdgcn_s_sleep(2);
+        }
         {
-            const uint32_t rn_now = DK_U(bt.rn), n_now = DK_U(bt.n), ep = DK_U(bt.epoch);
             const int Rq = (int)(rn_now - rn0);
             if (transparent && ep == e0 && Rq >= A && Rq <= Umin) {
                 const uint64_t pk = __ballot(deliv0 && Rq < E);
-                if (lane == 0) {
-                    bt.rn = rn0 + (uint32_t)max(Rq, (int)wmax);
-                    bt.n = n_now + (uint32_t)__builtin_popcountll(pk);
-                    __hip_atomic_store(&bt.turn, v + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+                if (lane == 0)
+                    baton_pass(&bt, v + 1, rn0 + (uint32_t)max(Rq, (int)wmax), n_now + (uint32_t)__builtin_popcountll(pk));
                 const uint32_t i2 = idx(v + 2 * kRelayWaves);
                 const uint4 g1 = P.rec[i1];
                 const Verdict r =
@@ -855,8 +889,8 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
                 continue;
             }
         }
-        const Baton b{DK_U(bt.state), DK_U(bt.rn), DK_U(bt.nooo), DK_U(bt.front), DK_U(bt.fin_pending),
-                      DK_U(bt.fin_seq), DK_U(bt.n), DK_U(bt.open_until), v, 0u};
+        const Baton b{v, 0u, DK_U(bt.rn), DK_U(bt.n), DK_U(bt.state), DK_U(bt.nooo), DK_U(bt.front),
+                      DK_U(bt.fin_pending), DK_U(bt.fin_seq), DK_U(bt.open_until)};
         // lanes below f are decided by the check against the baton's state (all of them in the common case)
         const bool plain_state = b.state == DK_TCP_ESTABLISHED && b.nooo < DK_TCP_OOO_MAX;
         const uint32_t R = b.rn - rn0;
@@ -868,11 +902,7 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
             const uint64_t bad = __ballot(q.have && !r.ok);
             f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
             pmk = __ballot(q.have && lane < f && r.act == DK_TCP_DELIVERED);
-            if (!bad && lane == 0) {
-                bt.rn = rn0 + max(R, wmax);
-                bt.n = b.n + (uint32_t)__builtin_popcountll(pmk);
-                __hip_atomic_store(&bt.turn, v + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
+            if (!bad && lane == 0) baton_pass(&bt, v + 1, rn0 + max(R, wmax), b.n + (uint32_t)__builtin_popcountll(pmk));
         }
         const uint32_t i2 = idx(v + 2 * kRelayWaves);
         const uint4 g1 = P.rec[i1];

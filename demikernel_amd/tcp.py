@@ -68,8 +68,8 @@ class TcpOut:
 class TcpReceiver:
     """Per-GPU TCP receive processing over a device connection table (the ControlBlock receive halves)."""
 
-    def __init__(self, device: int = 0):
-        self.lib = N.load_library()
+    def __init__(self, device: int = 0, lib_path: str | None = None):
+        self.lib = N.load_library(lib_path) if lib_path else N.load_library()
         self.device = device
         h = ctypes.c_void_p()
         _check(self.lib.dk_tcp_ctx_create(device, ctypes.byref(h)), "dk_tcp_ctx_create")

@@ -16,12 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zq: evidence at the current build (small-frame kernel's LDS bind table for scattered binds): the GPU suite,
-# smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r05zq
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r05zq_c3 --rotate 8 --defer
-step pmc4 400 bash tools/pmc_kernel.sh c4_imix r05zq_c4 --rotate 2 --defer
+# r05zr: the TCP relay walk's hand-off as in-order LDS instructions (holder: {rn, n} then turn; waiter: turn, then
+# {epoch, rn, n} in one poll) instead of a release store / acquire poll: the TCP GPU tests, then the walk probe against
+# the previous relay (build/variants/headtcp.so) on 1 and 64 connections
+step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 64 --walks relay --relay-waves 8 --iters 7 --libs build/variants/headtcp.so demikernel_amd/libdk_rx.so
 echo done

@@ -20,6 +20,7 @@ ap.add_argument("--nconns", type=int, nargs="+", default=[1])
 ap.add_argument("--walks", nargs="+", default=["relay", "wave"])
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--relay-waves", type=int, nargs="+", default=[16])
+ap.add_argument("--libs", nargs="+", default=[None], help="libdk_rx builds to compare (default: the package's)")
 a = ap.parse_args()
 torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
@@ -37,12 +38,12 @@ for nconns in a.nconns:
         for k, v in rx.items():
             r.t[k].copy_(torch.from_numpy(v.view(np.int32)))
         ref = None
-        for walk in [w + (f":{k}" if w == "relay" else "") for w in a.walks
-                     for k in (a.relay_waves if w == "relay" else [0])]:
+        for walk, lib in [(w + (f":{k}" if w == "relay" else ""), lib) for w in a.walks
+                          for k in (a.relay_waves if w == "relay" else [0]) for lib in a.libs]:
             os.environ["DK_TCP_WALK"] = walk.split(":")[0]
             if walk.startswith("relay"):
                 os.environ["DK_TCP_RELAY_WAVES"] = walk.split(":")[1]
-            tcp = TcpReceiver(0)
+            tcp = TcpReceiver(0, lib_path=os.path.abspath(lib) if lib else None)
             pristine = tcp.conns_to_device(table)
             conns = pristine.clone()
             out = TcpOut(a.nseg, len(table), 0)
@@ -61,6 +62,7 @@ for nconns in a.nconns:
             same = None if ref is None else bool(np.array_equal(ref, got["action"]))
             ref = got["action"] if ref is None else ref
             tcp.close()
-            print(json.dumps({"stream": name, "nconns": nconns, "walk": walk, "ms": round(float(np.median(times)), 4),
+            print(json.dumps({"stream": name, "nconns": nconns, "walk": walk, "lib": lib or "package",
+                              "ms": round(float(np.median(times)), 4),
                               "mseg_s": round(a.nseg / float(np.median(times)) / 1e3, 1),
                               "hist": [int(x) for x in hist], "same_actions_as_first": same}), flush=True)
