@@ -413,12 +413,12 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0, bu
             "delivered_frac": round(float(hist[1]) / nseg, 3),
             "actions": {name: int(c) for name, c in zip(TCP_ACTION_NAMES, hist) if c},
             "cpu_baseline": {"mseg_s": round(nseg / tc / 1e6, 2), "cores": 1, "kind": "port", "reps": reps},
-            "walk": os.environ.get("DK_TCP_WALK") or ("relay" if nseg >= 1024 * nconns and nconns <= 4096 else
+            "walk": os.environ.get("DK_TCP_WALK") or ("scan" if nseg >= 1024 * nconns and nconns <= 256 else
                                                        "wave" if nseg >= 8 * nconns else "lane"),
             "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (lanes = connections, "
                         "store in LDS; one wave per connection with a parallel 64-segment check at >= 8 "
-                        "segments per connection; 8 waves per connection relaying its state through LDS at "
-                        ">= 1,024)"}
+                        "segments per connection; at >= 1,024 and <= 256 connections the scan walk: windows "
+                        "precomputed across the chip, 64 windows per wave scan, decided windows written in parallel)"}
 
 
 def rx_kernel_name(frame_bytes, n):

@@ -70,6 +70,12 @@ struct Params {
                        // [range[2c], range[2c + 1]) are walked and the rest were classified (sort key 2c + 1)
     uint32_t* cls;     // [n]: the connection of a segment classified in the key kernel (never walked), else kNoConn
     uint32_t* open_until;  // [nconns]: frames of the connection from this index on come after its close
+    // the scan walk's per-window scratch (window v of connection c at ws = range[2c] / 64 + c + v: disjoint per c)
+    uint4* scan_sum;   // [ws]: {A, U, window maximum, 1} against the connection's state at the call's start
+    int* scan_ends;    // [ws / 64][lane][ws % 64]: each lane's candidate end if it delivers at R below it, else INT_MIN
+    uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
+    uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
+                          // fin_pending, fin_seq}, saved by the scan kernel for the post kernel
     dk_tcp_out out;
 };
 constexpr uint32_t kNoConn = 0xFFFFFFFFu;
@@ -981,15 +987,302 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
         }
     }
 }
+
+// ---------------- The scan walk (round 5): few connections with many segments each ----------------
+// The relay walk's per-window work splits into what does not depend on RCV.NXT at the window start (R) and a serial
+// hand-off, and on one connection the relay runs both on one CU. The scan walk spreads the first part over the chip
+// and turns the hand-off into wave scans:
+//   dk_tcp_scan_pre_kernel (every window of every connection in parallel, against the connection's state at the
+//     call's start): the relay's precompute (candidates' running maximum, the thresholds A <= R <= U under which
+//     classify() decides the whole window, the window's maximum) and each lane's candidate end if it delivers;
+//   dk_tcp_scan_kernel (one wave per connection, 64 windows at a time): R of each window = max(R at the batch start,
+//     the maxima of the windows before it in the batch) while every window is decided (an exclusive max scan and one
+//     compare per window), the deliveries each window makes at its R (its lanes' ends against R) and before it (a
+//     sum scan); the first undecided window runs here as in the relay (the state machine for its undecided lanes) and
+//     the scan resumes after it; once a window changes the state other than RCV.NXT (store, FIN, connection state)
+//     the precomputed windows after it are stale and the wave walks the rest of the connection as the wave walk does;
+//   dk_tcp_scan_post_kernel (every window in parallel): the decided windows' segments classified at their R, their
+//     outputs and deliveries written.
+// Same outputs as the other walks (every GPU TCP test runs it).
+struct Pre {  // a window's candidates against rn0 (the relay's precompute)
+    uint32_t pm, key, wmax;
+    bool cand, syn_r, synd;
+};
+__device__ __forceinline__ Pre pre_window(const Seg& q, uint32_t rn0, uint32_t wend, WaveScan::storage_type& scan) {
+    Pre r;
+    r.cand = q.cand(false, wend);
+    const uint32_t key1 = r.cand && lt(rn0, q.dend) ? q.dend - rn0 : 0u;
+    uint32_t pm1;
+    WaveScan().exclusive_scan(key1, pm1, 0u, scan, rocprim::maximum<uint32_t>());
+    r.syn_r = q.syn && !ge(q.seg_end, wend) && (int)(q.x - rn0) < (int)pm1;
+    r.synd = r.syn_r && q.ack_ok;
+    r.key = r.synd && lt(rn0, q.seg_end + 1u) ? max(key1, q.seg_end + 1u - rn0) : key1;
+    WaveScan().exclusive_scan(r.key, r.pm, 0u, scan, rocprim::maximum<uint32_t>());
+    r.wmax = (uint32_t)__builtin_amdgcn_readlane(max(r.pm, r.key), kWave - 1);
+    return r;
+}
+// The connection's state at the call's start, as the scan walk's kernels read it (wave-uniform).
+struct ConnHead {
+    uint32_t state, rn0, reader, bufsz, snd, wend, nooo, front, finp, fins;
+    __device__ __forceinline__ explicit ConnHead(const dk_tcp_conn* t) {
+        state = DK_U(t->state);
+        rn0 = DK_U(t->receive_next);
+        reader = DK_U(t->reader_next);
+        bufsz = DK_U(t->buffer_size);
+        snd = DK_U(t->send_next);
+        wend = reader + bufsz;
+        nooo = DK_U(min(t->ooo_count, DK_TCP_OOO_MAX));
+        front = nooo ? DK_U(t->ooo_start[0]) : 0u;
+        finp = DK_U(t->fin_pending);
+        fins = DK_U(t->fin_seq);
+    }
+};
+__device__ __forceinline__ uint32_t scan_ws(const Params& P, uint32_t c) { return P.range[2 * c] / kWave + c; }
+__device__ __forceinline__ int* scan_end_slot(const Params& P, uint32_t w, uint32_t lane) {
+    return P.scan_ends + (size_t)(w / kWave) * kWave * kWave + lane * kWave + (w % kWave);
+}
+
+constexpr uint32_t kScanBlock = 256, kScanWaves = kScanBlock / kWave;
+__global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
+    __shared__ WaveScan::storage_type scan_tmp[kScanWaves];
+    const uint32_t c = blockIdx.y, lane = threadIdx.x & (kWave - 1), wv = DK_U(threadIdx.x / kWave);
+    const dk_tcp_conn* t = P.conns + c;
+    const uint32_t k0 = P.range[2 * c], cnt = P.range[2 * c + 1] - k0;
+    const uint32_t nwin = (uint32_t)(((uint64_t)cnt + kWave - 1) / kWave), last = cnt ? cnt - 1 : 0u;
+    if (blockIdx.x * kScanWaves >= nwin) return;
+    const ConnHead h(t);
+    const uint32_t ws0 = scan_ws(P, c);
+    for (uint32_t v = blockIdx.x * kScanWaves + wv; v < nwin; v += gridDim.x * kScanWaves) {
+        const uint32_t base = v * kWave, lim = min(cnt - base, kWave);
+        const uint32_t i = P.svals[k0 + min(base + lane, last)];
+        const Seg q(P.rec[i], lane < lim, h.snd);
+        const Pre pr = pre_window(q, h.rn0, h.wend, scan_tmp[wv]);
+        // lane j is decided by classify() iff max(R, pm_j) >= T_j, or for a SYN at or past RCV.NXT iff R <= U_j
+        // (the relay walk's thresholds, against the state at the call's start)
+        const int xr = (int)(q.x - h.rn0), er = (int)(q.seg_end - h.rn0), dr = (int)(q.dend - h.rn0), pmi = (int)pr.pm;
+        int T = INT_MIN, U = INT_MAX;
+        if (q.have) {
+            const bool drains =
+                q.ack_ok && q.len > 0 && ((h.nooo && q.dend == h.front) || (h.finp && q.dend == h.fins));
+            if (ge(q.x, h.wend))
+                T = q.x == h.wend ? INT_MAX : INT_MIN;
+            else if (q.syn) {
+                const bool send_drains = (h.nooo && q.seg_end + 1u == h.front) || (h.finp && q.seg_end + 1u == h.fins);
+                if (pmi > er) {
+                } else if (pr.synd) {
+                    if (send_drains) T = er + 1;
+                } else if (pr.syn_r) {
+                } else if (ge(q.seg_end, h.wend) || pmi > xr) {
+                    T = er + 1;
+                } else {
+                    U = xr;
+                }
+            } else if (!q.simple)
+                T = er + 1;
+            else if (pr.cand)
+                T = drains ? dr : xr;
+            else
+                T = q.len == 0 || !ge(q.dend - 1u, h.wend) ? xr : er + 1;
+            if (pmi >= T) T = INT_MIN;
+        }
+        uint32_t tm, um;
+        WaveScan().inclusive_scan((uint32_t)T ^ 0x80000000u, tm, scan_tmp[wv], rocprim::maximum<uint32_t>());
+        WaveScan().inclusive_scan(~((uint32_t)U ^ 0x80000000u), um, scan_tmp[wv], rocprim::maximum<uint32_t>());
+        const int A = (int)((uint32_t)__builtin_amdgcn_readlane(tm, kWave - 1) ^ 0x80000000u);
+        const int Umin = (int)(~(uint32_t)__builtin_amdgcn_readlane(um, kWave - 1) ^ 0x80000000u);
+        const int E = pr.synd ? er + 1 : dr;
+        const bool deliv0 = (pr.cand || pr.synd) && pmi < E;
+        *scan_end_slot(P, ws0 + v, lane) = deliv0 ? E : INT_MIN;
+        if (lane == 0) P.scan_sum[ws0 + v] = make_uint4((uint32_t)A, (uint32_t)Umin, pr.wmax, 1u);
+    }
+}
+
+__global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
+    __shared__ WaveScan::storage_type scan_tmp[1];
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    dk_tcp_conn* t = P.conns + c;
+    const ConnHead h(t);
+    const uint32_t k0 = P.range[2 * c], cnt = P.range[2 * c + 1] - k0, all = P.range[2 * c + 2] - k0;
+    const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c, cap = all + DK_TCP_DELIV_EXTRA;
+    dk_tcp_view* const dv = P.out.deliv + d0;
+    const uint32_t nwin = (uint32_t)(((uint64_t)cnt + kWave - 1) / kWave), last = cnt ? cnt - 1 : 0u;
+    const uint32_t ws0 = scan_ws(P, c);
+    const auto idx = [&](uint32_t v) { return P.svals[k0 + min(v * kWave + lane, last)]; };
+    // the walk's state: scalars wave-uniform, the store in lane registers (entry k in lane k)
+    Walk w{h.state, h.rn0, h.reader, h.bufsz, h.snd, h.finp, h.fins, h.nooo};
+    RegStore s{0u, 0u, 0u, 0u, lane};
+    if (lane < h.nooo) {
+        const dk_tcp_view e = t->ooo[lane];
+        s = RegStore{t->ooo_start[lane], e.ref, e.off, e.len, lane};
+    }
+    if (lane < 7) {  // the post kernel runs after this one has written the connection back
+        const uint32_t hv[7] = {h.rn0, h.wend, h.snd, h.nooo, h.front, h.finp, h.fins};
+        uint32_t x = hv[0];
+#pragma unroll
+        for (uint32_t k = 1; k < 7; k++) x = lane == k ? hv[k] : x;
+        P.scan_head[8 * c + lane] = x;
+    }
+    uint32_t n = 0, open_until = h.state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u;
+    const bool transparent = h.state == DK_TCP_ESTABLISHED && h.nooo < DK_TCP_OOO_MAX;
+    bool stale = !transparent;  // the precomputed windows no longer describe the state
+    uint32_t v = 0;
+    while (v < nwin && !stale) {
+        // 64 windows: R of window v + k if every window before it in the batch is decided
+        const uint32_t R0 = w.rn - h.rn0;
+        const bool have = v + lane < nwin;
+        const uint4 sm = have ? P.scan_sum[ws0 + v + lane] : make_uint4(0x80000000u, 0x7FFFFFFFu, 0u, 0u);
+        int ends[kWave];
+#pragma unroll
+        for (uint32_t j = 0; j < kWave; j++) ends[j] = have ? *scan_end_slot(P, ws0 + v + lane, j) : INT_MIN;
+        uint32_t wx;
+        WaveScan().exclusive_scan(sm.z, wx, 0u, scan_tmp[0], rocprim::maximum<uint32_t>());
+        const uint32_t Rk = max(R0, wx);
+        const bool ok = have && (int)Rk >= (int)sm.x && (int)Rk <= (int)sm.y;
+        const uint64_t bad = __ballot(!ok);
+        const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
+        uint32_t cntk = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kWave; j++) cntk += (int)Rk < ends[j] ? 1u : 0u;
+        uint32_t nx;
+        WaveScan().exclusive_scan(cntk, nx, 0u, scan_tmp[0], rocprim::plus<uint32_t>());
+        if (lane < f) P.scan_post[ws0 + v + lane] = make_uint4(Rk, n + nx, 1u, 0u);
+        if (f > 0) {
+            w.rn = h.rn0 + (uint32_t)__builtin_amdgcn_readlane(max(Rk, sm.z), f - 1);
+            n += (uint32_t)__builtin_amdgcn_readlane(nx + cntk, f - 1);
+        }
+        v += f;
+        if (f == kWave || v >= nwin) continue;
+        // window v is not decided by the thresholds: the relay's slow path on the walk's state
+        if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t base = v * kWave, lim = min(cnt - base, kWave), i = idx(v);
+        const uint4 g = P.rec[i];
+        const Seg q(g, lane < lim, h.snd);
+        const Pre pr = pre_window(q, h.rn0, h.wend, scan_tmp[0]);
+        const uint32_t R = w.rn - h.rn0;
+        const Verdict r = classify(q, h.rn0 + max(R, pr.pm), h.wend, false, w.nooo, w.nooo ? s.start(0) : 0u,
+                                   w.fin_pending, w.fin_seq, pr.syn_r);
+        const uint64_t bl = __ballot(q.have && !r.ok);
+        const uint32_t fl = bl ? (uint32_t)__builtin_ctzll(bl) : kWave;
+        const uint64_t pmk = __ballot(q.have && lane < fl && r.act == DK_TCP_DELIVERED);
+        if (q.have && lane < fl) {
+            const uint32_t before =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(pmk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pmk, 0u));
+            const dk_tcp_view view{i, r.voff, r.vlen};
+            P.out.action[i] = r.act;
+            P.out.view[i] = view;
+            if (r.act == DK_TCP_DELIVERED && n + before < cap) dv[n + before] = view;
+        }
+        n += (uint32_t)__builtin_popcountll(pmk);
+        if (fl == kWave) {
+            w.rn = h.rn0 + max(R, pr.wmax);
+        } else {  // lane fl needs the state machine, then the one-wave walk resumes after it
+            w.rn = h.rn0 + max(R, (uint32_t)__builtin_amdgcn_readlane(pr.pm, fl));
+            WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};
+            const uint4 gf = make_uint4(__builtin_amdgcn_readlane(g.x, fl), __builtin_amdgcn_readlane(g.y, fl),
+                                        __builtin_amdgcn_readlane(g.z, fl), __builtin_amdgcn_readlane(g.w, fl));
+            const uint32_t i_f = __builtin_amdgcn_readlane(i, fl);
+            dk_tcp_view vf;
+            const uint32_t a_f = process(W.s, W.w, gf, i_f, W.o, vf);
+            if (lane == 0) {
+                P.out.action[i_f] = (uint8_t)a_f;
+                P.out.view[i_f] = vf;
+            }
+            if (W.w.state != DK_TCP_ESTABLISHED) W.open_until = i_f + 1;
+            W.window(base, i, g, fl + 1);
+            w = W.w;
+            s = W.s;
+            n = W.o.n;
+            open_until = W.open_until;
+        }
+        v++;
+        const uint32_t front = w.nooo ? s.start(0) : 0u;
+        stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
+                w.fin_seq != h.fins;
+    }
+    if (v < nwin) {  // the rest as the wave walk does (records one window ahead)
+        WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};
+        uint32_t i = idx(v);
+        uint4 g = P.rec[i];
+        for (; v < nwin; v++) {
+            if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t i1 = idx(v + 1);
+            const uint4 g1 = P.rec[i1];
+            W.window(v * kWave, i, g);
+            i = i1;
+            g = g1;
+        }
+        w = W.w;
+        s = W.s;
+        n = W.o.n;
+        open_until = W.open_until;
+    }
+    if (lane == 0) {
+        P.out.deliv_start[c] = d0;
+        P.open_until[c] = open_until;
+        t->state = w.state;
+        t->receive_next = w.rn;
+        t->fin_pending = w.fin_pending;
+        t->fin_seq = w.fin_seq;
+        t->ooo_count = w.nooo;
+        P.out.deliv_count[c] = n;
+    }
+    if (lane < DK_TCP_OOO_MAX) {
+        const bool live = lane < w.nooo;
+        t->ooo_start[lane] = live ? s.st : 0u;
+        t->ooo[lane] = live ? dk_tcp_view{s.rf, s.of, s.ln} : dk_tcp_view{0, 0, 0};
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_post_kernel(Params P) {
+    __shared__ WaveScan::storage_type scan_tmp[kScanWaves];
+    const uint32_t c = blockIdx.y, lane = threadIdx.x & (kWave - 1), wv = DK_U(threadIdx.x / kWave);
+    const uint32_t k0 = P.range[2 * c], cnt = P.range[2 * c + 1] - k0, all = P.range[2 * c + 2] - k0;
+    const uint32_t nwin = (uint32_t)(((uint64_t)cnt + kWave - 1) / kWave), last = cnt ? cnt - 1 : 0u;
+    if (blockIdx.x * kScanWaves >= nwin) return;
+    const uint32_t d0 = k0 + DK_TCP_DELIV_EXTRA * c, cap = all + DK_TCP_DELIV_EXTRA;
+    dk_tcp_view* const dv = P.out.deliv + d0;
+    const uint32_t ws0 = scan_ws(P, c);
+    // the state at the call's start (the scan kernel has written the connection's final state back by now): decided
+    // windows only exist while the state other than RCV.NXT equals it
+    const uint32_t* hd = P.scan_head + 8 * c;
+    const uint32_t rn0 = DK_U(hd[0]), wend = DK_U(hd[1]), snd = DK_U(hd[2]), nooo = DK_U(hd[3]), front = DK_U(hd[4]),
+                   finp = DK_U(hd[5]), fins = DK_U(hd[6]);
+    for (uint32_t v = blockIdx.x * kScanWaves + wv; v < nwin; v += gridDim.x * kScanWaves) {
+        const uint4 po = P.scan_post[ws0 + v];
+        if (DK_U(po.z) != 1u) continue;
+        const uint32_t base = v * kWave, lim = min(cnt - base, kWave);
+        const uint32_t i = P.svals[k0 + min(base + lane, last)];
+        const Seg q(P.rec[i], lane < lim, snd);
+        const Pre pr = pre_window(q, rn0, wend, scan_tmp[wv]);
+        const int Rq = (int)DK_U(po.x), pmi = (int)pr.pm;
+        const int er = (int)(q.seg_end - rn0), dr = (int)(q.dend - rn0);
+        const int E = pr.synd ? er + 1 : dr;
+        const bool deliv0 = (pr.cand || pr.synd) && pmi < E;
+        const uint64_t pk = __ballot(deliv0 && Rq < E);
+        const uint32_t n0 = DK_U(po.y);
+        const Verdict r = classify(q, rn0 + (uint32_t)max(Rq, pmi), wend, false, nooo, front, finp, fins, pr.syn_r);
+        const uint32_t before =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(pk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pk, 0u));
+        if (q.have) {
+            const dk_tcp_view view{i, r.voff, r.vlen};
+            P.out.action[i] = r.act;
+            P.out.view[i] = view;
+            if (r.act == DK_TCP_DELIVERED && n0 + before < cap) dv[n0 + before] = view;
+        }
+    }
+}
 #undef DK_U
 
-// Which walk runs: `force` (DK_TCP_WALK=lane|wave|relay, read once at dk_tcp_ctx_create: 0 lane, 1 wave, 2 relay,
-// -1 the rule); otherwise one lane per connection below kWaveWalkMinSegs segments per connection, the relay walk from
-// kRelayMinSegs (every relay wave gets a window) for up to kRelayMaxConns connections, else one wave per connection.
+// Which walk runs: `force` (DK_TCP_WALK=lane|wave|relay|scan, read once at dk_tcp_ctx_create: 0 lane, 1 wave, 2
+// relay, 3 scan, -1 the rule); otherwise one lane per connection below kWaveWalkMinSegs segments per connection, the
+// scan walk from kScanMinSegs (16 windows) for up to DK_TCP_SCAN_MAX_CONNS connections, else one wave per connection.
+// 1M segments (sessions r05zt-r05zv, profiles/r05_tcp_walks.jsonl): 1 connection scan 0.87 ms, relay 3.8, wave 12.7;
+// 16: scan 0.29, wave 0.94; 64: scan 0.22, relay 0.23, wave 0.31; 256: scan 0.19, wave 0.18; 1,024: wave 0.14, relay
+// 0.16, scan 0.18 (a wave per connection fills the chip). The relay walk stays selectable.
 constexpr uint32_t kWaveWalkMinSegs = 8;
-constexpr uint32_t kRelayMinSegs = kRelayWavesMax * kWave;
-#ifndef DK_TCP_RELAY_MAX_CONNS
-#define DK_TCP_RELAY_MAX_CONNS 4096
+constexpr uint32_t kScanMinSegs = 16 * kWave;
+#ifndef DK_TCP_SCAN_MAX_CONNS
+#define DK_TCP_SCAN_MAX_CONNS 256
 #endif
 // Up to this many connections (waves) the wave walk streams through LDS rings (kRing): 8 waves per CU at most on
 // 256 CUs, 12 KiB of LDS each.
@@ -997,12 +1290,13 @@ constexpr uint32_t kRelayMinSegs = kRelayWavesMax * kWave;
 #define DK_TCP_DEEP_MAX_CONNS 2048
 #endif
 constexpr uint32_t kDeepAheadMaxConns = DK_TCP_DEEP_MAX_CONNS;
-enum Walker { kLaneWalk = 0, kWaveWalk = 1, kRelayWalk = 2 };
+enum Walker { kLaneWalk = 0, kWaveWalk = 1, kRelayWalk = 2, kScanWalk = 3 };
 Walker pick_walk(uint32_t n, uint32_t nconns, int force) {
     if (nconns > (1u << 24)) return kLaneWalk;  // grid of nconns workgroups
-    if (force >= 0 && force <= 2) return (Walker)force;
+    if (force == 3 && nconns > 65535) return kRelayWalk;  // the scan walk's grids have one row per connection
+    if (force >= 0 && force <= 3) return (Walker)force;
     if ((uint64_t)n < (uint64_t)kWaveWalkMinSegs * nconns) return kLaneWalk;
-    if ((uint64_t)n >= (uint64_t)kRelayMinSegs * nconns && nconns <= DK_TCP_RELAY_MAX_CONNS) return kRelayWalk;
+    if ((uint64_t)n >= (uint64_t)kScanMinSegs * nconns && nconns <= DK_TCP_SCAN_MAX_CONNS) return kScanWalk;
     return kWaveWalk;
 }
 
@@ -1036,7 +1330,7 @@ int grow(T*& p, size_t& cap, size_t n) {
 // two streams never overlap on the scratch, and growing it waits for that work before freeing.
 struct dk_tcp_ctx {
     int device = 0;
-    int walk = -1;  // DK_TCP_WALK at creation: 0 lane, 1 wave, 2 relay, -1 the engine's rule
+    int walk = -1;  // DK_TCP_WALK at creation: 0 lane, 1 wave, 2 relay, 3 scan, -1 the engine's rule
     int relay_waves = 8;  // DK_TCP_RELAY_WAVES at creation (4 / 8 / 16; 8 measured best, session r05r)
     hipEvent_t last = nullptr;
     hipStream_t last_stream = nullptr;
@@ -1047,6 +1341,10 @@ struct dk_tcp_ctx {
     size_t rec_cap = 0;
     uint8_t* temp = nullptr;
     size_t temp_cap = 0;
+    uint4 *scan_sum = nullptr, *scan_post = nullptr;  // the scan walk's per-window scratch (dk_tcp::Params)
+    int* scan_ends = nullptr;
+    uint32_t* scan_head = nullptr;
+    size_t scan_sum_cap = 0, scan_post_cap = 0, scan_ends_cap = 0, scan_head_cap = 0;
 };
 
 extern "C" {
@@ -1060,7 +1358,7 @@ int dk_tcp_ctx_create(int32_t device, dk_tcp_ctx** out) {
     dk_tcp_ctx* t = new dk_tcp_ctx();
     t->device = device;
     if (const char* e = getenv("DK_TCP_WALK"))
-        t->walk = !strcmp(e, "relay") ? 2 : !strcmp(e, "wave") ? 1 : !strcmp(e, "lane") ? 0 : -1;
+        t->walk = !strcmp(e, "scan") ? 3 : !strcmp(e, "relay") ? 2 : !strcmp(e, "wave") ? 1 : !strcmp(e, "lane") ? 0 : -1;
     if (const char* e = getenv("DK_TCP_RELAY_WAVES")) t->relay_waves = atoi(e);
     if (hipEventCreateWithFlags(&t->last, hipEventDisableTiming) != hipSuccess) {
         delete t;
@@ -1075,7 +1373,8 @@ void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     dk_tcp::DeviceGuard g(t->device);
     if (t->used) (void)hipEventSynchronize(t->last);
     for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp,
-                    (void*)t->cls, (void*)t->open_until})
+                    (void*)t->cls, (void*)t->open_until, (void*)t->scan_sum, (void*)t->scan_post, (void*)t->scan_ends,
+                    (void*)t->scan_head})
         if (p) (void)hipFree(p);
     (void)hipEventDestroy(t->last);
     delete t;
@@ -1105,6 +1404,17 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
         (rc = grow(t->range, t->range_cap, 2 * (size_t)nconns + 1)) || (rc = grow(t->cls, t->cls_cap, n)) ||
         (rc = grow(t->open_until, t->open_cap, nconns)))
         return rc;
+    const dk_tcp::Walker walker = nconns ? dk_tcp::pick_walk(n, nconns, t->walk) : dk_tcp::kLaneWalk;
+    if (walker == dk_tcp::kScanWalk) {  // windows: ws = range[2c] / 64 + c + v < n / 64 + nconns + 1
+        const size_t nw = (size_t)n / 64 + nconns + 1;
+        if (t->used && (t->scan_sum_cap < nw || t->scan_ends_cap < (nw / 64 + 1) * 4096 || t->scan_head_cap < 8ull * nconns) &&
+            hipEventSynchronize(t->last) != hipSuccess)
+            return EINVAL;
+        if ((rc = grow(t->scan_sum, t->scan_sum_cap, nw)) || (rc = grow(t->scan_post, t->scan_post_cap, nw)) ||
+            (rc = grow(t->scan_ends, t->scan_ends_cap, (nw / 64 + 1) * 4096)) ||
+            (rc = grow(t->scan_head, t->scan_head_cap, 8 * (size_t)nconns)))
+            return rc;
+    }
     int bits = 1;
     while (bits < 32 && (1ull << bits) <= 2ull * nconns) bits++;  // keys are 0 .. 2 nconns
     const rocprim::counting_iterator<uint32_t> index(0);
@@ -1131,6 +1441,10 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     P.range = t->range;
     P.cls = t->cls;
     P.open_until = t->open_until;
+    P.scan_sum = t->scan_sum;
+    P.scan_post = t->scan_post;
+    P.scan_ends = t->scan_ends;
+    P.scan_head = t->scan_head;
     P.out = *out;
     const dim3 gn((n + kBlock - 1) / kBlock), gr((2 * nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
     if (n) {
@@ -1142,7 +1456,15 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     }
     if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
     if (nconns) {
-        switch (pick_walk(n, nconns, t->walk)) {
+        switch (walker) {
+            case kScanWalk: {
+                const uint32_t per = (uint32_t)(((uint64_t)n / kWave / nconns + kScanWaves) / kScanWaves);
+                const dim3 gs(std::min<uint32_t>(std::max<uint32_t>(per, 1u), 65535u), nconns);
+                hipLaunchKernelGGL(dk_tcp_scan_pre_kernel, gs, dim3(kScanBlock), 0, s, P);
+                hipLaunchKernelGGL(dk_tcp_scan_kernel, dim3(nconns), dim3(kWave), 0, s, P);
+                hipLaunchKernelGGL(dk_tcp_scan_post_kernel, gs, dim3(kScanBlock), 0, s, P);
+                break;
+            }
             case kRelayWalk:
                 if (t->relay_waves == 4)
                     hipLaunchKernelGGL(dk_tcp_relay_walk_kernel<4>, dim3(nconns), dim3(4 * kWave), 0, s, P);

@@ -17,11 +17,12 @@ from oracle.oracle import OraclePeer
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["lane", "wave", "relay"])
+@pytest.fixture(scope="module", params=["lane", "wave", "relay", "scan"])
 def tcp(request):
     """Every test runs through every walk: lanes = connections, one wave per connection with the parallel in-order
-    check, and 8 waves per connection relaying its state window to window (DK_TCP_WALK forces the choice the engine
-    otherwise makes from segments per connection)."""
+    check, 8 waves per connection relaying its state window to window, and the scan walk (windows precomputed across
+    the chip, 64 windows per wave scan, the undecided ones through the state machine) (DK_TCP_WALK forces the choice
+    the engine otherwise makes from segments per connection)."""
     import os
 
     import torch

@@ -16,9 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zr: the TCP relay walk's hand-off as in-order LDS instructions (holder: {rn, n} then turn; waiter: turn, then
-# {epoch, rn, n} in one poll) instead of a release store / acquire poll: the TCP GPU tests, then the walk probe against
-# the previous relay (build/variants/headtcp.so) on 1 and 64 connections
-step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 64 --walks relay --relay-waves 8 --iters 7 --libs build/variants/headtcp.so demikernel_amd/libdk_rx.so
+# r05zw: the bench's TCP lines' shapes (reordered streams, 16 MiB windows) per walk: 64 and 16 connections
+step w64 300 env DK_TCP_WALK=wave python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
+step r64 300 env DK_TCP_WALK=relay python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
+step s64 300 env DK_TCP_WALK=scan python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
 echo done

@@ -1,4 +1,4 @@
-"""dk_tcp_rx_process time per walk (DK_TCP_WALK=lane|wave|relay) on one connection's stream, with and without the
+"""dk_tcp_rx_process time per walk (DK_TCP_WALK=lane|wave|relay|scan) on one connection's stream, with and without the
 segments that need the state machine (synth.tcp_streams dup / oow / rare fractions), to separate the walks' per-window
 cost from their process() calls. One JSON line per (stream, walk): ms per call (HIP events, median)."""
 import argparse
