@@ -72,7 +72,7 @@ struct Params {
     uint32_t* open_until;  // [nconns]: frames of the connection from this index on come after its close
     // the scan walk's per-window scratch (window v of connection c at ws = range[2c] / 64 + c + v: disjoint per c)
     uint4* scan_sum;   // [ws]: {A, U, window maximum, 1} against the connection's state at the call's start
-    int* scan_ends;    // [ws / 64][lane][ws % 64]: each lane's candidate end if it delivers at R below it, else INT_MIN
+    int* scan_ends;    // [ws][lane]: each lane's candidate end if it delivers at R below it, else INT_MIN
     uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
     uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
                           // fin_pending, fin_seq}, saved by the scan kernel for the post kernel
@@ -1038,9 +1038,6 @@ struct ConnHead {
     }
 };
 __device__ __forceinline__ uint32_t scan_ws(const Params& P, uint32_t c) { return P.range[2 * c] / kWave + c; }
-__device__ __forceinline__ int* scan_end_slot(const Params& P, uint32_t w, uint32_t lane) {
-    return P.scan_ends + (size_t)(w / kWave) * kWave * kWave + lane * kWave + (w % kWave);
-}
 
 constexpr uint32_t kScanBlock = 256, kScanWaves = kScanBlock / kWave;
 __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
@@ -1092,7 +1089,7 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
         const int Umin = (int)(~(uint32_t)__builtin_amdgcn_readlane(um, kWave - 1) ^ 0x80000000u);
         const int E = pr.synd ? er + 1 : dr;
         const bool deliv0 = (pr.cand || pr.synd) && pmi < E;
-        *scan_end_slot(P, ws0 + v, lane) = deliv0 ? E : INT_MIN;
+        P.scan_ends[(size_t)(ws0 + v) * kWave + lane] = deliv0 ? E : INT_MIN;
         if (lane == 0) P.scan_sum[ws0 + v] = make_uint4((uint32_t)A, (uint32_t)Umin, pr.wmax, 1u);
     }
 }
@@ -1125,15 +1122,31 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
     uint32_t n = 0, open_until = h.state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u;
     const bool transparent = h.state == DK_TCP_ESTABLISHED && h.nooo < DK_TCP_OOO_MAX;
     bool stale = !transparent;  // the precomputed windows no longer describe the state
+    // lane k of a batch at v: window v + k's summary and its 64 lanes' ends (unconditional loads, clamped to the last
+    // window; a lane past it fails the check). The next batch (v + 64, the common case) is loaded before this one is
+    // resolved, so its latency hides behind the scans and stores.
+    struct Batch {
+        uint4 sm;
+        int4 ends[kWave / 4];
+    };
+    const auto load_batch = [&](uint32_t v0, Batch& b) {
+        const uint32_t wk = ws0 + min(v0 + lane, nwin - 1);
+        b.sm = P.scan_sum[wk];
+        const int4* er = reinterpret_cast<const int4*>(P.scan_ends + (size_t)wk * kWave);
+#pragma unroll
+        for (uint32_t m = 0; m < kWave / 4; m++) b.ends[m] = er[m];
+    };
     uint32_t v = 0;
-    while (v < nwin && !stale) {
+    Batch cur;
+    if (!stale && nwin) load_batch(0, cur);
+    while (v < nwin && !stale) {  // (nwin >= 1 here)
         // 64 windows: R of window v + k if every window before it in the batch is decided
         const uint32_t R0 = w.rn - h.rn0;
         const bool have = v + lane < nwin;
-        const uint4 sm = have ? P.scan_sum[ws0 + v + lane] : make_uint4(0x80000000u, 0x7FFFFFFFu, 0u, 0u);
-        int ends[kWave];
-#pragma unroll
-        for (uint32_t j = 0; j < kWave; j++) ends[j] = have ? *scan_end_slot(P, ws0 + v + lane, j) : INT_MIN;
+        Batch nxt;
+        load_batch(v + kWave, nxt);
+        const uint4 sm = cur.sm;
+        const int4(&ends)[kWave / 4] = cur.ends;
         uint32_t wx;
         WaveScan().exclusive_scan(sm.z, wx, 0u, scan_tmp[0], rocprim::maximum<uint32_t>());
         const uint32_t Rk = max(R0, wx);
@@ -1142,7 +1155,9 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
         uint32_t cntk = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < kWave; j++) cntk += (int)Rk < ends[j] ? 1u : 0u;
+        for (uint32_t m = 0; m < kWave / 4; m++)
+            cntk += ((int)Rk < ends[m].x ? 1u : 0u) + ((int)Rk < ends[m].y ? 1u : 0u) + ((int)Rk < ends[m].z ? 1u : 0u) +
+                    ((int)Rk < ends[m].w ? 1u : 0u);
         uint32_t nx;
         WaveScan().exclusive_scan(cntk, nx, 0u, scan_tmp[0], rocprim::plus<uint32_t>());
         if (lane < f) P.scan_post[ws0 + v + lane] = make_uint4(Rk, n + nx, 1u, 0u);
@@ -1151,7 +1166,11 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
             n += (uint32_t)__builtin_amdgcn_readlane(nx + cntk, f - 1);
         }
         v += f;
-        if (f == kWave || v >= nwin) continue;
+        if (f == kWave) {
+            cur = nxt;
+            continue;
+        }
+        if (v >= nwin) continue;
         // window v is not decided by the thresholds: the relay's slow path on the walk's state
         if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t base = v * kWave, lim = min(cnt - base, kWave), i = idx(v);
@@ -1198,6 +1217,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         const uint32_t front = w.nooo ? s.start(0) : 0u;
         stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
                 w.fin_seq != h.fins;
+        if (!stale && v < nwin) load_batch(v, cur);
     }
     if (v < nwin) {  // the rest as the wave walk does (records one window ahead)
         WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};
@@ -1407,11 +1427,11 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     const dk_tcp::Walker walker = nconns ? dk_tcp::pick_walk(n, nconns, t->walk) : dk_tcp::kLaneWalk;
     if (walker == dk_tcp::kScanWalk) {  // windows: ws = range[2c] / 64 + c + v < n / 64 + nconns + 1
         const size_t nw = (size_t)n / 64 + nconns + 1;
-        if (t->used && (t->scan_sum_cap < nw || t->scan_ends_cap < (nw / 64 + 1) * 4096 || t->scan_head_cap < 8ull * nconns) &&
+        if (t->used && (t->scan_sum_cap < nw || t->scan_ends_cap < nw * 64 || t->scan_head_cap < 8ull * nconns) &&
             hipEventSynchronize(t->last) != hipSuccess)
             return EINVAL;
         if ((rc = grow(t->scan_sum, t->scan_sum_cap, nw)) || (rc = grow(t->scan_post, t->scan_post_cap, nw)) ||
-            (rc = grow(t->scan_ends, t->scan_ends_cap, (nw / 64 + 1) * 4096)) ||
+            (rc = grow(t->scan_ends, t->scan_ends_cap, nw * 64)) ||
             (rc = grow(t->scan_head, t->scan_head_cap, 8 * (size_t)nconns)))
             return rc;
     }

@@ -16,8 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zw: the bench's TCP lines' shapes (reordered streams, 16 MiB windows) per walk: 64 and 16 connections
-step w64 300 env DK_TCP_WALK=wave python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
-step r64 300 env DK_TCP_WALK=relay python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
-step s64 300 env DK_TCP_WALK=scan python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
+# r05zz: scan walk, next batch loaded before the current one is resolved: the TCP GPU tests, the probe
+step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 --walks scan --iters 7
 echo done
