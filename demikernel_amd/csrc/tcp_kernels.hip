@@ -722,7 +722,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
 // after; otherwise the lanes before the first undecided one are taken and the one-wave walk continues from there on
 // the baton's state (the store moving between LDS and lane registers) before the baton moves on. 1 connection, 1M
 // in-order segments: 4.2 ms against 12.7 ms for the one-wave walk (session r05r).
-constexpr uint32_t kRelayWavesMax = 16;  // waves per connection (DK_TCP_RELAY_WAVES = 4 | 8 | 16)
+// waves per connection: DK_TCP_RELAY_WAVES = 4 | 8 | 16
 struct alignas(16) Baton {
     uint32_t turn;   // the window whose owner holds the baton
     uint32_t epoch;  // bumped by every window that went through the state machine (state, store, FIN may change)

@@ -16,7 +16,10 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r05zz: scan walk, next batch loaded before the current one is resolved: the TCP GPU tests, the probe
+# r06a: scan walk in one loop: batches resume once the state is the call-start one again; the slow window's next
+# batch loading behind it. TCP GPU tests, the probe, the bench's reordered shapes (scan vs wave)
 step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 --walks scan --iters 7
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan --iters 7
+step s64 300 env DK_TCP_WALK=scan python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
+step w64 300 env DK_TCP_WALK=wave python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
 echo done
