@@ -16,10 +16,12 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06a: scan walk in one loop: batches resume once the state is the call-start one again; the slow window's next
-# batch loading behind it. TCP GPU tests, the probe, the bench's reordered shapes (scan vs wave)
-step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan --iters 7
-step s64 300 env DK_TCP_WALK=scan python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
-step w64 300 env DK_TCP_WALK=wave python tools/tcpbench.py --nconns 64 16 --cpu-seconds 0.2
+# r06b: evidence at the current build (TCP relay hand-off, scan walk): the GPU suite, smoke(), the default bench
+# line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r06b
+step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r06b_c3 --rotate 8 --defer
+step pmc4 400 bash tools/pmc_kernel.sh c4_imix r06b_c4 --rotate 2 --defer
 echo done
