@@ -16,12 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06b: evidence at the current build (TCP relay hand-off, scan walk): the GPU suite, smoke(), the default bench
-# line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r06b
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r06b_c3 --rotate 8 --defer
-step pmc4 400 bash tools/pmc_kernel.sh c4_imix r06b_c4 --rotate 2 --defer
+# r06c: staging kernel with the first chunk's descriptors loaded before the LDS init / table copy / barrier (ed.so)
+step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --check --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/ed.so
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --check --iters 10 --reps 9 demikernel_amd/libdk_rx.so build/variants/ed.so
 echo done
