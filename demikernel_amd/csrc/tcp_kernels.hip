@@ -1123,8 +1123,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
     const bool transparent = h.state == DK_TCP_ESTABLISHED && h.nooo < DK_TCP_OOO_MAX;
     bool stale = !transparent;  // the precomputed windows no longer describe the state
     // lane k of a batch at v: window v + k's summary and its 64 lanes' ends (unconditional loads, clamped to the last
-    // window; a lane past it fails the check). The next batch (v + 64, the common case) is loaded before this one is
-    // resolved, so its latency hides behind the scans and stores.
+    // window; a lane past it fails the check)
     struct Batch {
         uint4 sm;
         int4 ends[kWave / 4];
@@ -1137,40 +1136,48 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         for (uint32_t m = 0; m < kWave / 4; m++) b.ends[m] = er[m];
     };
     uint32_t v = 0;
-    Batch cur;
-    if (!stale && nwin) load_batch(0, cur);
-    while (v < nwin && !stale) {  // (nwin >= 1 here)
-        // 64 windows: R of window v + k if every window before it in the batch is decided
+    // One batch at v from b (loaded for v): the decided windows' R and deliveries; returns how many windows it took
+    // (64: all; fewer: window v + f is undecided, or the connection ends).
+    const auto batch_step = [&](const Batch& b) -> uint32_t {
         const uint32_t R0 = w.rn - h.rn0;
         const bool have = v + lane < nwin;
-        Batch nxt;
-        load_batch(v + kWave, nxt);
-        const uint4 sm = cur.sm;
-        const int4(&ends)[kWave / 4] = cur.ends;
         uint32_t wx;
-        WaveScan().exclusive_scan(sm.z, wx, 0u, scan_tmp[0], rocprim::maximum<uint32_t>());
+        WaveScan().exclusive_scan(b.sm.z, wx, 0u, scan_tmp[0], rocprim::maximum<uint32_t>());
         const uint32_t Rk = max(R0, wx);
-        const bool ok = have && (int)Rk >= (int)sm.x && (int)Rk <= (int)sm.y;
+        const bool ok = have && (int)Rk >= (int)b.sm.x && (int)Rk <= (int)b.sm.y;
         const uint64_t bad = __ballot(!ok);
         const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
         uint32_t cntk = 0;
 #pragma unroll
         for (uint32_t m = 0; m < kWave / 4; m++)
-            cntk += ((int)Rk < ends[m].x ? 1u : 0u) + ((int)Rk < ends[m].y ? 1u : 0u) + ((int)Rk < ends[m].z ? 1u : 0u) +
-                    ((int)Rk < ends[m].w ? 1u : 0u);
+            cntk += ((int)Rk < b.ends[m].x ? 1u : 0u) + ((int)Rk < b.ends[m].y ? 1u : 0u) +
+                    ((int)Rk < b.ends[m].z ? 1u : 0u) + ((int)Rk < b.ends[m].w ? 1u : 0u);
         uint32_t nx;
         WaveScan().exclusive_scan(cntk, nx, 0u, scan_tmp[0], rocprim::plus<uint32_t>());
         if (lane < f) P.scan_post[ws0 + v + lane] = make_uint4(Rk, n + nx, 1u, 0u);
         if (f > 0) {
-            w.rn = h.rn0 + (uint32_t)__builtin_amdgcn_readlane(max(Rk, sm.z), f - 1);
+            w.rn = h.rn0 + (uint32_t)__builtin_amdgcn_readlane(max(Rk, b.sm.z), f - 1);
             n += (uint32_t)__builtin_amdgcn_readlane(nx + cntk, f - 1);
         }
         v += f;
-        if (f == kWave) {
-            cur = nxt;
-            continue;
+        return f;
+    };
+    // Three batches in flight (b0, b1, b2 for v, v + 64, v + 128), each reloaded 128 windows ahead once used: no
+    // register copies, so no wait for a batch before its turn.
+    Batch b0, b1, b2;
+    while (v < nwin && !stale) {
+        load_batch(v, b0);
+        load_batch(v + kWave, b1);
+        load_batch(v + 2 * kWave, b2);
+        for (;;) {
+            if (batch_step(b0) < kWave) break;
+            load_batch(v + 2 * kWave, b0);
+            if (batch_step(b1) < kWave) break;
+            load_batch(v + 2 * kWave, b1);
+            if (batch_step(b2) < kWave) break;
+            load_batch(v + 2 * kWave, b2);
         }
-        if (v >= nwin) continue;
+        if (v >= nwin) break;
         // window v is not decided by the thresholds: the relay's slow path on the walk's state
         if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t base = v * kWave, lim = min(cnt - base, kWave), i = idx(v);
@@ -1217,7 +1224,6 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         const uint32_t front = w.nooo ? s.start(0) : 0u;
         stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
                 w.fin_seq != h.fins;
-        if (!stale && v < nwin) load_batch(v, cur);
     }
     if (v < nwin) {  // the rest as the wave walk does (records one window ahead)
         WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};

@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06c: staging kernel with the first chunk's descriptors loaded before the LDS init / table copy / barrier (ed.so)
-step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --check --iters 20 --reps 11 demikernel_amd/libdk_rx.so build/variants/ed.so
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --check --iters 10 --reps 9 demikernel_amd/libdk_rx.so build/variants/ed.so
+# r06e: scan kernel, the batches after a slow window loading while it runs: TCP GPU tests, the probe
+step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 --walks scan --iters 7
 echo done
