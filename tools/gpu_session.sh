@@ -16,7 +16,6 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06e: scan kernel, the batches after a slow window loading while it runs: TCP GPU tests, the probe
-step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 --walks scan --iters 7
+# r06f: rocPRIM onesweep configs for the TCP sort (s8b: 8 bits/pass 256x24; s6a: 6 bits/pass 512x16) vs the default
+step probe 300 python tools/tcp_walk_probe.py --nconns 16384 1 --walks wave scan --iters 7 --libs demikernel_amd/libdk_rx.so build/variants/s8b.so build/variants/s6a.so
 echo done
