@@ -16,6 +16,12 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06f: rocPRIM onesweep configs for the TCP sort (s8b: 8 bits/pass 256x24; s6a: 6 bits/pass 512x16) vs the default
-step probe 300 python tools/tcp_walk_probe.py --nconns 16384 1 --walks wave scan --iters 7 --libs demikernel_amd/libdk_rx.so build/variants/s8b.so build/variants/s6a.so
+# r06g: evidence at the final build (scan kernel with three batches in flight): the GPU suite, smoke(), the default
+# bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r06g
+step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r06g_c3 --rotate 8 --defer
+step pmc4 400 bash tools/pmc_kernel.sh c4_imix r06g_c4 --rotate 2 --defer
 echo done
