@@ -14,8 +14,10 @@
 //      (latency-bound, lanes = connections); everything else is a pass over the batch.
 //   4'. dk_tcp_wave_walk_kernel instead, at >= kWaveWalkMinSegs segments per connection: one wave per connection,
 //      64 segments classified in parallel per step, the state machine only for the segments that need it;
-//   4''. dk_tcp_relay_walk_kernel for few connections with many segments each: 8 waves per connection take its
-//      windows in turn and pass its state from window to window through LDS.
+//   4''. the scan walk for few connections with many segments each (dk_tcp_scan_pre_kernel, dk_tcp_scan_kernel,
+//      dk_tcp_scan_post_kernel): windows precomputed across the chip, 64 windows resolved per wave scan, the decided
+//      windows written in parallel (below); dk_tcp_relay_walk_kernel (DK_TCP_WALK=relay): 8 waves per connection
+//      take its windows in turn and pass its state from window to window through LDS.
 // Segments whose outcome cannot depend on their place in the connection's order are classified in step 1 and never
 // walked: RCV.NXT only moves forward, from its value at the start of the batch up to the window end (reader_next +
 // buffer size, fixed during the batch), so a segment starting past the window end is OUT_OF_WINDOW whenever it is
