@@ -16,12 +16,10 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06g: evidence at the final build (scan kernel with three batches in flight): the GPU suite, smoke(), the default
-# bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r06g
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r06g_c3 --rotate 8 --defer
-step pmc4 400 bash tools/pmc_kernel.sh c4_imix r06g_c4 --rotate 2 --defer
+# r06h: medium frames of <= 640 B streamed by 8 lanes, 8 per step (med8.so) vs 16 lanes, 4 per step
+step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --check --iters 10 --reps 9 demikernel_amd/libdk_rx.so build/variants/med8.so
+step ab_imix1 300 python tools/abtest.py --workload c4_imix --rotate 1 --defer --grids 0 --iters 10 --reps 7 demikernel_amd/libdk_rx.so build/variants/med8.so
+step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --check --iters 20 --reps 9 demikernel_amd/libdk_rx.so build/variants/med8.so
+step ab_c2 300 python tools/abtest.py --workload c2_tcp1500 --defer --grids 0 --check --iters 10 --reps 7 demikernel_amd/libdk_rx.so build/variants/med8.so
+step ab_tx 300 python tools/abtest.py --workload c2_tcp1500 --tx --grids 0 --iters 10 --reps 7 demikernel_amd/libdk_rx.so build/variants/med8.so
 echo done
