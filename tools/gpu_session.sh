@@ -16,10 +16,9 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06h: medium frames of <= 640 B streamed by 8 lanes, 8 per step (med8.so) vs 16 lanes, 4 per step
-step ab_imix 300 python tools/abtest.py --workload c4_imix --rotate 2 --defer --grids 0 --check --iters 10 --reps 9 demikernel_amd/libdk_rx.so build/variants/med8.so
-step ab_imix1 300 python tools/abtest.py --workload c4_imix --rotate 1 --defer --grids 0 --iters 10 --reps 7 demikernel_amd/libdk_rx.so build/variants/med8.so
-step ab_c1 300 python tools/abtest.py --workload c1_tcp1078 --rotate 3 --defer --grids 0 --check --iters 20 --reps 9 demikernel_amd/libdk_rx.so build/variants/med8.so
-step ab_c2 300 python tools/abtest.py --workload c2_tcp1500 --defer --grids 0 --check --iters 10 --reps 7 demikernel_amd/libdk_rx.so build/variants/med8.so
-step ab_tx 300 python tools/abtest.py --workload c2_tcp1500 --tx --grids 0 --iters 10 --reps 7 demikernel_amd/libdk_rx.so build/variants/med8.so
+# r06i: per-wave timelines of the staging kernel at the final sources (-DDK_DIAG_STAMPS build): IMIX with 2 rotating
+# batches, the default dynamic tail and without it; C1
+step st_imix 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2
+step st_imix_t0 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail=0
+step st_c1 120 python tools/stamps_staged.py build/variants/stamps.so --workload c1_tcp1078 --rotate 3
 echo done
