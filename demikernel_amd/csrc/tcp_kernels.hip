@@ -73,7 +73,8 @@ struct Params {
     uint32_t* cls;     // [n]: the connection of a segment classified in the key kernel (never walked), else kNoConn
     uint32_t* open_until;  // [nconns]: frames of the connection from this index on come after its close
     // the scan walk's per-window scratch (window v of connection c at ws = range[2c] / 64 + c + v: disjoint per c)
-    uint4* scan_sum;   // [ws]: {A, U, window maximum, 1} against the connection's state at the call's start
+    uint4* scan_sum;   // [ws]: {A, U, window maximum, A2} against the connection's state at the call's start (decided
+                       // iff A <= R <= U or R >= A2)
     int* scan_ends;    // [ws][lane]: each lane's candidate end if it delivers at R below it, else INT_MIN
     uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
     uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
@@ -1057,9 +1058,10 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
         const Seg q(P.rec[i], lane < lim, h.snd);
         const Pre pr = pre_window(q, h.rn0, h.wend, scan_tmp[wv]);
         // lane j is decided by classify() iff max(R, pm_j) >= T_j, or for a SYN at or past RCV.NXT iff R <= U_j
-        // (the relay walk's thresholds, against the state at the call's start)
+        // (the relay walk's thresholds, against the state at the call's start) — or, for that SYN, once R is past its
+        // end (old: DUPLICATE), R >= Aalt_j; a retransmitted SYN no earlier lane reaches is decided either way
         const int xr = (int)(q.x - h.rn0), er = (int)(q.seg_end - h.rn0), dr = (int)(q.dend - h.rn0), pmi = (int)pr.pm;
-        int T = INT_MIN, U = INT_MAX;
+        int T = INT_MIN, U = INT_MAX, Aalt = INT_MIN;
         if (q.have) {
             const bool drains =
                 q.ack_ok && q.len > 0 && ((h.nooo && q.dend == h.front) || (h.finp && q.dend == h.fins));
@@ -1075,6 +1077,7 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
                     T = er + 1;
                 } else {
                     U = xr;
+                    Aalt = er + 1;
                 }
             } else if (!q.simple)
                 T = er + 1;
@@ -1089,10 +1092,13 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
         WaveScan().inclusive_scan(~((uint32_t)U ^ 0x80000000u), um, scan_tmp[wv], rocprim::maximum<uint32_t>());
         const int A = (int)((uint32_t)__builtin_amdgcn_readlane(tm, kWave - 1) ^ 0x80000000u);
         const int Umin = (int)(~(uint32_t)__builtin_amdgcn_readlane(um, kWave - 1) ^ 0x80000000u);
+        // the window is also decided at R >= A2 when its one upper bound is such a SYN's (no upper bound then)
+        const uint64_t ul = __ballot(U != INT_MAX);
+        const int A2 = __popcll(ul) == 1 ? max(A, __builtin_amdgcn_readlane(Aalt, (uint32_t)__builtin_ctzll(ul))) : INT_MAX;
         const int E = pr.synd ? er + 1 : dr;
         const bool deliv0 = (pr.cand || pr.synd) && pmi < E;
         P.scan_ends[(size_t)(ws0 + v) * kWave + lane] = deliv0 ? E : INT_MIN;
-        if (lane == 0) P.scan_sum[ws0 + v] = make_uint4((uint32_t)A, (uint32_t)Umin, pr.wmax, 1u);
+        if (lane == 0) P.scan_sum[ws0 + v] = make_uint4((uint32_t)A, (uint32_t)Umin, pr.wmax, (uint32_t)A2);
     }
 }
 
@@ -1146,7 +1152,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         uint32_t wx;
         WaveScan().exclusive_scan(b.sm.z, wx, 0u, scan_tmp[0], rocprim::maximum<uint32_t>());
         const uint32_t Rk = max(R0, wx);
-        const bool ok = have && (int)Rk >= (int)b.sm.x && (int)Rk <= (int)b.sm.y;
+        const bool ok = have && (((int)Rk >= (int)b.sm.x && (int)Rk <= (int)b.sm.y) || (int)Rk >= (int)b.sm.w);
         const uint64_t bad = __ballot(!ok);
         const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
         uint32_t cntk = 0;

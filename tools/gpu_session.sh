@@ -16,9 +16,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06i: per-wave timelines of the staging kernel at the final sources (-DDK_DIAG_STAMPS build): IMIX with 2 rotating
-# batches, the default dynamic tail and without it; C1
-step st_imix 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2
-step st_imix_t0 120 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2 --tuning tail=0
-step st_c1 120 python tools/stamps_staged.py build/variants/stamps.so --workload c1_tcp1078 --rotate 3
+# r06j: scan walk: a window whose only upper bound is a retransmitted SYN no earlier lane reaches is also decided once
+# R is past that SYN's end (DUPLICATE): the TCP GPU tests (all walks), the probe
+step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 --walks scan --iters 7
 echo done
