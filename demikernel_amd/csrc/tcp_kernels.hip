@@ -623,6 +623,43 @@ struct WaveWalk {
     }
 };
 
+// The windows v0.. of a connection's cnt segments (sorted frame indices at P.svals + k0) through W, streamed into LDS
+// rings. Window u's indices land in sidx[u % 16] (DMA issued at window u - 2H, read at u - H and u), its records in
+// srec[u % 8] (issued at window u - H, read at u). Window v issues records(v + H), then indices(v + 2H), so at least
+// 2H - 2 vector-memory operations follow indices(v + H) and 2H - 1 follow records(v): vmcnt(2H - 2) has both landed
+// whatever else (result stores) was issued in between (vmcnt retires in order).
+__device__ __forceinline__ void ring_walk(const Params& P, WaveWalk& W, uint32_t (&sidx)[kIdxSlots][kWave],
+                                          uint4 (&srec)[kRecSlots][kWave], uint32_t k0, uint32_t cnt, uint32_t v0) {
+    const uint32_t lane = W.lane, last = cnt ? cnt - 1 : 0u;
+    const auto idx_dma = [&](uint32_t u) {
+        __builtin_amdgcn_global_load_lds((const void*)(P.svals + k0 + min(u * kWave + lane, last)),
+                                         (lds_void*)&sidx[u % kIdxSlots][0], 4, 0, 0);
+    };
+    const auto rec_dma = [&](uint32_t u, uint32_t fi) {
+        __builtin_amdgcn_global_load_lds((const void*)(P.rec + fi), (lds_void*)&srec[u % kRecSlots][0], 16, 0, 0);
+    };
+    // The ring is read by inline-asm LDS loads: the compiler cannot tell ring slots apart and would wait for every
+    // LDS-DMA load (vmcnt(0)) before each LDS read.
+    const auto idx_at = [&](uint32_t u) { return lds_addr(&sidx[u % kIdxSlots][lane]); };
+    if (v0 * kWave >= cnt) return;  // (k0 may be n then)
+    for (uint32_t u = v0; u < v0 + kRingH; u++) idx_dma(u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t u = v0; u < v0 + kRingH; u++) {
+        rec_dma(u, lds_read_u32(idx_at(u)));
+        idx_dma(u + kRingH);
+    }
+    for (uint32_t v = v0; v * kWave < cnt; v++) {
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        uint32_t i, fi;
+        uint4 g;
+        lds_read_window(idx_at(v), lds_addr(&srec[v % kRecSlots][lane]), idx_at(v + kRingH), i, g, fi);
+        rec_dma(v + kRingH, fi);
+        idx_dma(v + 2 * kRingH);
+        W.window(v * kWave, i, g);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write outlives the workgroup
+}
+
 #define DK_U(x) (uint32_t) __builtin_amdgcn_readfirstlane((int)(x))
 
 template <bool kRing>
@@ -647,38 +684,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     // Loads are unconditional: positions past the connection's last segment read its last one again (unused).
     const uint32_t last = cnt ? cnt - 1 : 0u;
     if constexpr (kRing) {
-        // Window u's indices land in sidx[u % 16] (DMA issued at window u - 2H, read at u - H and u), its records in
-        // srec[u % 8] (issued at window u - H, read at u). Window v issues records(v + H), then indices(v + 2H), so
-        // at least 2H - 2 vector-memory operations follow indices(v + H) and 2H - 1 follow records(v): vmcnt(2H - 2)
-        // has both landed whatever else (result stores) was issued in between (vmcnt retires in order).
-        const auto idx_dma = [&](uint32_t u) {
-            __builtin_amdgcn_global_load_lds((const void*)(P.svals + k0 + min(u * kWave + lane, last)),
-                                             (lds_void*)&sidx[u % kIdxSlots][0], 4, 0, 0);
-        };
-        const auto rec_dma = [&](uint32_t u, uint32_t fi) {
-            __builtin_amdgcn_global_load_lds((const void*)(P.rec + fi), (lds_void*)&srec[u % kRecSlots][0], 16, 0, 0);
-        };
-        // The ring is read by inline-asm LDS loads: the compiler cannot tell ring slots apart and would wait for every
-        // LDS-DMA load (vmcnt(0)) before each LDS read.
-        const auto idx_at = [&](uint32_t u) { return lds_addr(&sidx[u % kIdxSlots][lane]); };
-        if (cnt) {  // (k0 may be n then)
-            for (uint32_t u = 0; u < kRingH; u++) idx_dma(u);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            for (uint32_t u = 0; u < kRingH; u++) {
-                rec_dma(u, lds_read_u32(idx_at(u)));
-                idx_dma(u + kRingH);
-            }
-        }
-        for (uint32_t v = 0; v * kWave < cnt; v++) {
-            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-            uint32_t i, fi;
-            uint4 g;
-            lds_read_window(idx_at(v), lds_addr(&srec[v % kRecSlots][lane]), idx_at(v + kRingH), i, g, fi);
-            rec_dma(v + kRingH, fi);
-            idx_dma(v + 2 * kRingH);
-            W.window(v * kWave, i, g);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write outlives the workgroup
+        ring_walk(P, W, sidx, srec, k0, cnt, 0u);
     } else {
         // frame indices two windows ahead, records one
         const auto idx = [&](uint32_t u) { return P.svals[k0 + min(u * kWave + lane, last)]; };
@@ -1104,6 +1110,8 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
 
 __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
     __shared__ WaveScan::storage_type scan_tmp[1];
+    __shared__ uint32_t sidx[kIdxSlots][kWave];
+    __shared__ uint4 srec[kRecSlots][kWave];
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     dk_tcp_conn* t = P.conns + c;
     const ConnHead h(t);
@@ -1233,18 +1241,10 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
                 w.fin_seq != h.fins;
     }
-    if (v < nwin) {  // the rest as the wave walk does (records one window ahead)
+    if (v < nwin) {  // the rest as the wave walk does (the LDS rings)
+        for (uint32_t u = v + lane; u < nwin; u += kWave) P.scan_post[ws0 + u] = make_uint4(0u, 0u, 0u, 0u);
         WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};
-        uint32_t i = idx(v);
-        uint4 g = P.rec[i];
-        for (; v < nwin; v++) {
-            if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
-            const uint32_t i1 = idx(v + 1);
-            const uint4 g1 = P.rec[i1];
-            W.window(v * kWave, i, g);
-            i = i1;
-            g = g1;
-        }
+        ring_walk(P, W, sidx, srec, k0, cnt, v);
         w = W.w;
         s = W.s;
         n = W.o.n;

@@ -16,8 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06j: scan walk: a window whose only upper bound is a retransmitted SYN no earlier lane reaches is also decided once
-# R is past that SYN's end (DUPLICATE): the TCP GPU tests (all walks), the probe
+# r06l: scan walk: resume inside the batch holding the next window after an undecided one (was: reload all three)
 step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 --walks scan --iters 7
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan --streams clean dups default bench --iters 7
 echo done

@@ -20,6 +20,8 @@ ap.add_argument("--nconns", type=int, nargs="+", default=[1])
 ap.add_argument("--walks", nargs="+", default=["relay", "wave"])
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--relay-waves", type=int, nargs="+", default=[16])
+ap.add_argument("--streams", nargs="+", default=["clean", "dups", "default"],
+                help="clean | dups | default (in order, 1 GB buffer) | bench (bench.py's 64-connection line: reorder 3, 16 MB)")
 ap.add_argument("--libs", nargs="+", default=[None], help="libdk_rx builds to compare (default: the package's)")
 a = ap.parse_args()
 torch.cuda.set_device(0)
@@ -27,10 +29,12 @@ dev = torch.device("cuda", 0)
 s = torch.cuda.current_stream(0)
 STREAMS = {"clean": dict(dup=0.0, oow=0.0, rare=0.0, fin=0.0, rst=0.0),
            "dups": dict(dup=0.02, oow=0.0, rare=0.0, fin=0.0, rst=0.0),
-           "default": dict()}
+           "default": dict(),
+           "bench": dict(buffer_size=1 << 24, reorder=3.0)}
 for nconns in a.nconns:
-    for name, kw in STREAMS.items():
-        _, tr, table = synth.tcp_streams(a.nseg, nconns, 1500, buffer_size=1 << 30, reorder=0.0, **kw)
+    for name in a.streams:
+        kw = {"buffer_size": 1 << 30, "reorder": 0.0, **STREAMS[name]}
+        _, tr, table = synth.tcp_streams(a.nseg, nconns, 1500, **kw)
         rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
               "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
               "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
