@@ -623,13 +623,14 @@ struct WaveWalk {
     }
 };
 
-// The windows v0.. of a connection's cnt segments (sorted frame indices at P.svals + k0) through W, streamed into LDS
+// The windows v0 .. v1 - 1 of a connection's cnt segments (sorted frame indices at P.svals + k0) through W, streamed into LDS
 // rings. Window u's indices land in sidx[u % 16] (DMA issued at window u - 2H, read at u - H and u), its records in
 // srec[u % 8] (issued at window u - H, read at u). Window v issues records(v + H), then indices(v + 2H), so at least
 // 2H - 2 vector-memory operations follow indices(v + H) and 2H - 1 follow records(v): vmcnt(2H - 2) has both landed
 // whatever else (result stores) was issued in between (vmcnt retires in order).
 __device__ __forceinline__ void ring_walk(const Params& P, WaveWalk& W, uint32_t (&sidx)[kIdxSlots][kWave],
-                                          uint4 (&srec)[kRecSlots][kWave], uint32_t k0, uint32_t cnt, uint32_t v0) {
+                                          uint4 (&srec)[kRecSlots][kWave], uint32_t k0, uint32_t cnt, uint32_t v0,
+                                          uint32_t v1) {
     const uint32_t lane = W.lane, last = cnt ? cnt - 1 : 0u;
     const auto idx_dma = [&](uint32_t u) {
         __builtin_amdgcn_global_load_lds((const void*)(P.svals + k0 + min(u * kWave + lane, last)),
@@ -641,14 +642,14 @@ __device__ __forceinline__ void ring_walk(const Params& P, WaveWalk& W, uint32_t
     // The ring is read by inline-asm LDS loads: the compiler cannot tell ring slots apart and would wait for every
     // LDS-DMA load (vmcnt(0)) before each LDS read.
     const auto idx_at = [&](uint32_t u) { return lds_addr(&sidx[u % kIdxSlots][lane]); };
-    if (v0 * kWave >= cnt) return;  // (k0 may be n then)
+    if (v0 >= v1) return;  // (k0 may be n when cnt is 0)
     for (uint32_t u = v0; u < v0 + kRingH; u++) idx_dma(u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (uint32_t u = v0; u < v0 + kRingH; u++) {
         rec_dma(u, lds_read_u32(idx_at(u)));
         idx_dma(u + kRingH);
     }
-    for (uint32_t v = v0; v * kWave < cnt; v++) {
+    for (uint32_t v = v0; v < v1; v++) {
         asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
         uint32_t i, fi;
         uint4 g;
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_wave_walk_kernel(Params P) {
     // Loads are unconditional: positions past the connection's last segment read its last one again (unused).
     const uint32_t last = cnt ? cnt - 1 : 0u;
     if constexpr (kRing) {
-        ring_walk(P, W, sidx, srec, k0, cnt, 0u);
+        ring_walk(P, W, sidx, srec, k0, cnt, 0u, (uint32_t)(((uint64_t)cnt + kWave - 1) / kWave));
     } else {
         // frame indices two windows ahead, records one
         const auto idx = [&](uint32_t u) { return P.svals[k0 + min(u * kWave + lane, last)]; };
@@ -1049,6 +1050,9 @@ struct ConnHead {
 __device__ __forceinline__ uint32_t scan_ws(const Params& P, uint32_t c) { return P.range[2 * c] / kWave + c; }
 
 constexpr uint32_t kScanBlock = 256, kScanWaves = kScanBlock / kWave;
+// windows the scan kernel walks in the rings after two undecided in a row: kScanRingRun, doubled while that repeats
+// (up to kScanRingRunMax), back to kScanRingRun once the scan took more than a batch again
+constexpr uint32_t kScanRingRun = 8, kScanRingRunMax = 512;
 __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
     __shared__ WaveScan::storage_type scan_tmp[kScanWaves];
     const uint32_t c = blockIdx.y, lane = threadIdx.x & (kWave - 1), wv = DK_U(threadIdx.x / kWave);
@@ -1178,23 +1182,8 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         v += f;
         return f;
     };
-    // Three batches in flight (b0, b1, b2 for v, v + 64, v + 128), each reloaded 128 windows ahead once used: no
-    // register copies, so no wait for a batch before its turn.
-    Batch b0, b1, b2;
-    while (v < nwin && !stale) {
-        load_batch(v, b0);
-        load_batch(v + kWave, b1);
-        load_batch(v + 2 * kWave, b2);
-        for (;;) {
-            if (batch_step(b0) < kWave) break;
-            load_batch(v + 2 * kWave, b0);
-            if (batch_step(b1) < kWave) break;
-            load_batch(v + 2 * kWave, b1);
-            if (batch_step(b2) < kWave) break;
-            load_batch(v + 2 * kWave, b2);
-        }
-        if (v >= nwin) break;
-        // window v is not decided by the thresholds: the relay's slow path on the walk's state
+    // window v is not decided by the thresholds: the relay's slow path on the walk's state
+    const auto slow_window = [&]() {
         if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t base = v * kWave, lim = min(cnt - base, kWave), i = idx(v);
         const uint4 g = P.rec[i];
@@ -1237,19 +1226,49 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
             open_until = W.open_until;
         }
         v++;
-        const uint32_t front = w.nooo ? s.start(0) : 0u;
-        stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
-                w.fin_seq != h.fins;
-    }
-    if (v < nwin) {  // the rest as the wave walk does (the LDS rings)
-        for (uint32_t u = v + lane; u < nwin; u += kWave) P.scan_post[ws0 + u] = make_uint4(0u, 0u, 0u, 0u);
+    };
+    // windows v .. v1 - 1 as the wave walk does (the LDS rings)
+    const auto ring_run = [&](uint32_t v1) {
+        for (uint32_t u = v + lane; u < v1; u += kWave) P.scan_post[ws0 + u] = make_uint4(0u, 0u, 0u, 0u);
         WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};
-        ring_walk(P, W, sidx, srec, k0, cnt, v);
+        ring_walk(P, W, sidx, srec, k0, cnt, v, v1);
         w = W.w;
         s = W.s;
         n = W.o.n;
         open_until = W.open_until;
+        v = v1;
+    };
+    // Three batches in flight (b0, b1, b2 for v, v + 64, v + 128), each reloaded 128 windows ahead once used: no
+    // register copies, so no wait for a batch before its turn.
+    Batch b0, b1, b2;
+    uint32_t last_slow = 0xFFFFFFFEu, run = kScanRingRun;  // the last window the slow path took, the next ring run
+    while (v < nwin && !stale) {
+        load_batch(v, b0);
+        load_batch(v + kWave, b1);
+        load_batch(v + 2 * kWave, b2);
+        for (;;) {
+            if (batch_step(b0) < kWave) break;
+            load_batch(v + 2 * kWave, b0);
+            if (batch_step(b1) < kWave) break;
+            load_batch(v + 2 * kWave, b1);
+            if (batch_step(b2) < kWave) break;
+            load_batch(v + 2 * kWave, b2);
+        }
+        if (v >= nwin) break;
+        if (v == last_slow + 1) {  // two undecided windows in a row (reordering): the next ones in the rings
+            ring_run(v + min(run, nwin - v));
+            last_slow = v - 1;
+            run = min(2 * run, kScanRingRunMax);
+        } else {
+            if (v - last_slow > kWave) run = kScanRingRun;
+            last_slow = v;
+            slow_window();
+        }
+        const uint32_t front = w.nooo ? s.start(0) : 0u;
+        stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
+                w.fin_seq != h.fins;
     }
+    if (v < nwin) ring_run(nwin);  // stale: the rest as the wave walk does
     if (lane == 0) {
         P.out.deliv_start[c] = d0;
         P.open_until[c] = open_until;

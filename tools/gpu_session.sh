@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06l: scan walk: resume inside the batch holding the next window after an undecided one (was: reload all three)
+# r06q: scan walk: ring runs of 8 windows doubling while undecided windows keep coming in pairs (up to 512)
 step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
 step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan --streams clean dups default bench --iters 7
 echo done
