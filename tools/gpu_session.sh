@@ -16,12 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06r: evidence at the final build (scan walk with the SYN threshold, ring tail and ring runs): the GPU suite,
-# smoke(), the default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes, C3 and IMIX SQ counters
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r06r
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r06r_c3 --rotate 8 --defer
-step pmc4 400 bash tools/pmc_kernel.sh c4_imix r06r_c4 --rotate 2 --defer
+# r06s: reordered runs resolved from the arrival order (chain_run) in the one-wave walk's window loop
+step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
+step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan wave --streams clean default bench --iters 7
 echo done
