@@ -182,6 +182,7 @@ struct Store {
 
 // The wave walk's store: entry k in lane k's registers (lanes >= DK_TCP_OOO_MAX unused). Reads are lane reads of a
 // wave-uniform index, remove and insert one cross-lane shift each instead of an entry-by-entry copy loop.
+static_assert(DK_TCP_OOO_MAX <= 16, "RegStore keeps the store in row 0 (lanes 0..15)");
 struct RegStore {
     uint32_t st, rf, of, ln, lane;
     __device__ __forceinline__ uint32_t start(uint32_t k) const { return __builtin_amdgcn_readlane(st, k); }
@@ -190,9 +191,16 @@ struct RegStore {
         return dk_tcp_view{(uint32_t)__builtin_amdgcn_readlane(rf, k), (uint32_t)__builtin_amdgcn_readlane(of, k),
                            (uint32_t)__builtin_amdgcn_readlane(ln, k)};
     }
+    // Entries live in lanes 0..DK_TCP_OOO_MAX - 1 = row 0: the shifts are DPP row shifts (a VALU operand
+    // modifier) rather than LDS-unit permutes.
+    static __device__ __forceinline__ uint32_t from_next(uint32_t x) {  // lane l gets lane l + 1 (row_shl:1)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x101, 0xF, 0xF, false);
+    }
+    static __device__ __forceinline__ uint32_t from_prev(uint32_t x) {  // lane l gets lane l - 1 (row_shr:1)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x111, 0xF, 0xF, false);
+    }
     __device__ __forceinline__ void remove(uint32_t at, uint32_t) {
-        const uint32_t a = __shfl_down(st, 1, 64), b = __shfl_down(rf, 1, 64), c = __shfl_down(of, 1, 64),
-                       d = __shfl_down(ln, 1, 64);
+        const uint32_t a = from_next(st), b = from_next(rf), c = from_next(of), d = from_next(ln);
         if (lane >= at) {
             st = a;
             rf = b;
@@ -201,8 +209,7 @@ struct RegStore {
         }
     }
     __device__ __forceinline__ void insert(uint32_t at, uint32_t, uint32_t s, dk_tcp_view v) {
-        const uint32_t a = __shfl_up(st, 1, 64), b = __shfl_up(rf, 1, 64), c = __shfl_up(of, 1, 64),
-                       d = __shfl_up(ln, 1, 64);
+        const uint32_t a = from_prev(st), b = from_prev(rf), c = from_prev(of), d = from_prev(ln);
         if (lane > at) {
             st = a;
             rf = b;

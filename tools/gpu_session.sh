@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06s: reordered runs resolved from the arrival order (chain_run) in the one-wave walk's window loop
+# r06u: reordered runs resolved from the arrival order (chain_run) with a DPP / swizzle bitonic sort
 step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
 step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan wave --streams clean default bench --iters 7
 echo done
