@@ -16,7 +16,10 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06u: reordered runs resolved from the arrival order (chain_run) with a DPP / swizzle bitonic sort
-step tcptest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_tcp.py
-step probe 300 python tools/tcp_walk_probe.py --nconns 1 16 64 256 --walks scan wave --streams clean default bench --iters 7
+# r06v: evidence at the final build (the register store's DPP shifts on top of r06r): the GPU suite, smoke(), the
+# default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r06v
 echo done
