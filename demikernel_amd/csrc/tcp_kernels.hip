@@ -1017,7 +1017,8 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
 //     compare per window), the deliveries each window makes at its R (its lanes' ends against R) and before it (a
 //     sum scan); the first undecided window runs here as in the relay (the state machine for its undecided lanes) and
 //     the scan resumes after it; once a window changes the state other than RCV.NXT (store, FIN, connection state)
-//     the precomputed windows after it are stale and the wave walks the rest of the connection as the wave walk does;
+//     the precomputed windows after it are stale and the wave walks the rest of the connection as the wave walk does
+//     (LDS rings); after two undecided windows in a row the next ones go through the rings too (ring runs);
 //   dk_tcp_scan_post_kernel (every window in parallel): the decided windows' segments classified at their R, their
 //     outputs and deliveries written.
 // Same outputs as the other walks (every GPU TCP test runs it).
