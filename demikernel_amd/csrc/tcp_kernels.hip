@@ -543,8 +543,11 @@ __device__ __forceinline__ Verdict classify(const Seg& q, uint32_t rn, uint32_t 
     const uint32_t send1 = q.seg_end + 1u;
     const bool syn_part_ok = syn_reach && q.syn && before && !dup && !ge(q.seg_end, wend) &&
                              !(q.ack_ok && ((nooo && send1 == front) || (fin_pending && send1 == fin_seq)));
+    // plain segments past rn that carry no deliverable data (no ACK, ACK of unsent data, or no payload) change nothing
+    // in process_packet either (ctrlblk.rs:403-440): NO_ACK / ACK_UNSENT / NO_DATA at any place in the window
     const bool ok = dup || oow || syn_ok || syn_part_ok || (at && plain && (q.len == 0 || data_in)) ||
-                    (before && plain && data_in) || (past && beyond);
+                    (before && plain && data_in) || (past && beyond) ||
+                    (past && q.simple && q.fast_action != DK_TCP_DELIVERED);
     Verdict r;
     r.ok = ok && q.have;
     r.act = dup ? (uint8_t)DK_TCP_DUPLICATE
@@ -870,7 +873,7 @@ __global__ __launch_bounds__(kRelayWaves * kWave) void dk_tcp_relay_walk_kernel(
             else if (cand)
                 T = drains ? dr : xr;
             else
-                T = q.len == 0 || !ge(q.dend - 1u, wend) ? xr : er + 1;
+                T = q.len == 0 || !ge(q.dend - 1u, wend) ? INT_MIN : er + 1;  // (decided at any R: classify())
             if (pmi >= T) T = INT_MIN;
         }
         // wave max of T and min of U (order-preserving unsigned maps through the max scan)
@@ -1102,7 +1105,7 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
             else if (pr.cand)
                 T = drains ? dr : xr;
             else
-                T = q.len == 0 || !ge(q.dend - 1u, h.wend) ? xr : er + 1;
+                T = q.len == 0 || !ge(q.dend - 1u, h.wend) ? INT_MIN : er + 1;  // (decided at any R: classify())
             if (pmi >= T) T = INT_MIN;
         }
         uint32_t tm, um;

@@ -16,7 +16,10 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06w: SQ counters of the C3 and IMIX kernels at the final tree
-step pmc3 400 bash tools/pmc_kernel.sh c3_udp64 r06w_c3 --rotate 8 --defer
-step pmc4 400 bash tools/pmc_kernel.sh c4_imix r06w_c4 --rotate 2 --defer
+# r06y: evidence at the final tree (classify() decides no-data segments past RCV.NXT): the GPU suite, smoke(), the
+# default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 1100 bash tools/profile_bench.sh r06y
 echo done
