@@ -544,6 +544,26 @@ def device_identity(dev) -> dict:
     return ident
 
 
+class CommSizeError(SystemExit):
+    """A scaling line whose RCCL communicator does not hold every rank is refused (exit status 4)."""
+
+    def __init__(self, nranks, world):
+        super().__init__(4)
+        self.nranks, self.world = nranks, world
+
+    def __str__(self):
+        return f"bench: the RCCL communicator holds {self.nranks} ranks, the job {self.world}: no scaling line"
+
+
+def check_comm_size(nranks, world):
+    """in RCCL mode the communicator's own rank count (dk_comm_count) must equal the job's world
+    size, or the run exits non-zero before any line is printed."""
+    if nranks != world:
+        e = CommSizeError(nranks, world)
+        print(str(e), file=sys.stderr, flush=True)
+        raise e
+
+
 def scale_fields(world, comm, per_rank, coll_s, gather_every):
     """The fields by which a multi-GPU line proves itself: how many ranks the product's RCCL
     communicator holds (dk_comm_count; None when the counters went through the test-only torch stand-in or there is
@@ -554,6 +574,7 @@ def scale_fields(world, comm, per_rank, coll_s, gather_every):
     if comm is not None and hasattr(comm, "count"):  # demikernel_amd.Comm: the include/dk_comm.h communicator
         nranks = int(comm.count())
         kind = "rccl (dk_rx_flow_counts_allreduce_to over dk_comm.h)"
+        check_comm_size(nranks, world)
     elif comm is not None:
         kind = "TEST ONLY: torch.distributed all_reduce (--counts-via-torch-gloo-test)"
     rows = sorted(per_rank, key=lambda r: r["rank"])
@@ -630,6 +651,7 @@ def main():
             print(f"bench: rank {rank}: dk_comm_init_rank failed ({e}); the packet-sharded path needs the RCCL "
                   f"communicator of include/dk_comm.h", file=sys.stderr, flush=True)
             sys.exit(3)
+        check_comm_size(comm.count(), world)  # before any timing: a mis-sized communicator prints no line
         collective = (f"dk_rx_flow_counts_allreduce_to (RCCL all-reduce of accumulating u64 flow + verdict counters) "
                       f"every {GATHER_EVERY} batches and after the last, on the launch stream (RCCL's kernel does not "
                       f"run beside the receive kernels: profiles/r04_overlap.json), double-buffered counter sets "

@@ -12,9 +12,7 @@ from ctypes import POINTER, c_char_p, c_int, c_int32, c_uint8, c_uint16, c_uint3
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libdk_rx.so")
-# Tuning builds only (tools/variants.sh): load an alternative build of the same sources.
-LIB_PATH = os.environ.get("DK_RX_LIB_VARIANT", LIB_PATH)
+LIB_PATH = os.path.join(PKG_DIR, "libdk_rx.so")  # tuning builds (tools/variants.sh) are passed as lib_path explicitly
 
 DK_FLOW_NONE = 0xFFFFFFFF
 DK_RX_BATCH_ALIGNED16 = 1  # dk_rx_batch.flags
@@ -187,8 +185,11 @@ DIAG_FUNCTIONS = [
     ("dk_diag_path_stats_read", c_int, [c_void_p, c_void_p]),
     ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p, c_uint32]),
     ("dk_diag_tx_set_tuning", c_int, [c_int32, c_int32, c_int32]),
+    ("dk_diag_tcp_set_walk", c_int, [c_void_p, c_int32, c_int32]),
 ]
-DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table", "tail", "udp_table"]
+DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table", "tail", "udp_table",
+                    "host_zc"]
+DK_TCP_WALKS = {"lane": 0, "wave": 1, "relay": 2, "scan": 3}
 
 ALL_FUNCTIONS = FUNCTIONS + RING_FUNCTIONS + TCP_FUNCTIONS + DIAG_FUNCTIONS + DEMI_FUNCTIONS + COMM_FUNCTIONS
 

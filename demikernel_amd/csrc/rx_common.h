@@ -130,6 +130,7 @@ struct RowCombine {
 // needed, so its latency is hidden. A launch zeroes the counter set the stream's next tail launch will use (two sets
 // per stream slot, alternating).
 constexpr uint32_t kTailXcds = 8;
+constexpr uint32_t kStagedWaves = 4;  // waves per workgroup of the staged kernel (the host's tail boundary uses it too)
 constexpr uint32_t kTailStride = 64;  // words between counters
 constexpr uint32_t kTailSetWords = kTailXcds * kTailStride;
 

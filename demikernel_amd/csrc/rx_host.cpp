@@ -69,15 +69,14 @@ struct Stage {  // device staging for one pipeline stream
     uint32_t opts_cap = 0;
 };
 
-// Tuning overrides (-1 = the host rule). Read once from the environment at dk_rx_ctx_create (DK_RX_STAGE, DK_RX_SPLIT,
-// DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID, DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE, DK_RX_TAIL, DK_RX_UDP_TABLE)
-// or set by dk_diag_rx_set_tuning; never read on the launch path.
+// Tuning overrides (-1 = the host rule). A context starts on the built-in rule; only dk_diag_rx_set_tuning changes
+// them (dk_diag.h). The process environment is never read: a LibOS process cannot inherit a different kernel family.
 struct Tuning {
     int32_t stage = -1, split = -1, small = -1, sched = -1, grid = -1, grid_per_cu = -1, debug = 0;
-    int32_t lds_table = -1;  // 0: Active lookups never use the LDS table (DK_RX_LDS_TABLE)
-    int32_t tail = -1;       // staged kernel's dynamic tail rounds (DK_RX_TAIL; 0 off)
+    int32_t lds_table = -1;  // 0: Active lookups never use the LDS table
+    int32_t tail = -1;       // staged kernel's dynamic tail rounds (0 off)
     int32_t udp_table = -1;  // small-frame kernel, local UDP binds: 0 the port table, 1 the LDS bind table whenever it
-                             // fits (DK_RX_UDP_TABLE)
+                             // fits
     int32_t host_zc = -1;  // dk_rx_process_host: read mapped pinned frames in place (-1/1 when mapped, 0 never)
 };
 
@@ -128,11 +127,6 @@ uint32_t next_pow2(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
     return p;
-}
-
-int32_t env_knob(const char* name) {
-    const char* e = getenv(name);
-    return e ? (int32_t)atoi(e) : -1;
 }
 
 int upload_table(dk_rx_ctx* c, const std::vector<uint32_t>& slots, uint32_t mask) {
@@ -363,7 +357,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     p.tail_ctr = p.tail_next = nullptr;
     const int32_t tail_d = T.tail >= 0 ? T.tail : 2;
     if (family == dk::kFamilyStaged && p.sched == 0 && tail_d > 0) {
-        const uint32_t nwaves = grid * 4u, nchunk = (p.n + 63) / 64;
+        const uint32_t nwaves = grid * dk::kStagedWaves, nchunk = (p.n + 63) / 64;
         const uint32_t per = nchunk / nwaves;
         if (per + 1 >= (uint32_t)tail_d + 2) p.tail_ks = per + 1 - (uint32_t)tail_d;
         p.tail_pools = grid % 8 == 0 ? 8u : grid % 4 == 0 ? 4u : grid % 2 == 0 ? 2u : 1u;
@@ -472,11 +466,9 @@ int ensure_stage(Stage& s, uint32_t cap, uint64_t bytes, bool opts) {
     return 0;
 }
 
-// TX tuning overrides (-1 = host rule): DK_TX_SPLIT, DK_RX_SCHED, DK_RX_GRID_PER_CU read once per process, or set by
-// dk_diag_tx_set_tuning; never read from the environment on the launch path.
+// TX tuning overrides (-1 = host rule), set only by dk_diag_tx_set_tuning (never from the environment).
 struct TxTuning {
     std::atomic<int32_t> split{-1}, sched{-1}, grid_per_cu{-1};
-    TxTuning() : split(env_knob("DK_TX_SPLIT")), sched(env_knob("DK_RX_SCHED")), grid_per_cu(env_knob("DK_RX_GRID_PER_CU")) {}
 };
 TxTuning& tx_tuning() {
     static TxTuning t;
@@ -536,18 +528,7 @@ int dk_rx_ctx_create(const dk_rx_cfg* cfg, dk_rx_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || cus <= 0)
         cus = 256;
     c->cu_count = (uint32_t)cus;
-    Tuning& t = c->tune;  // tuning overrides: read once here, never on the launch path
-    t.stage = env_knob("DK_RX_STAGE");
-    t.split = env_knob("DK_RX_SPLIT");
-    t.small = env_knob("DK_RX_SMALL");
-    t.sched = env_knob("DK_RX_SCHED");
-    t.grid = env_knob("DK_RX_GRID");
-    t.grid_per_cu = env_knob("DK_RX_GRID_PER_CU");
-    t.debug = env_knob("DK_RX_DEBUG");
-    t.host_zc = env_knob("DK_RX_HOST_ZC");
-    t.lds_table = env_knob("DK_RX_LDS_TABLE");
-    t.tail = env_knob("DK_RX_TAIL");
-    t.udp_table = env_knob("DK_RX_UDP_TABLE");
+    // c->tune: the built-in rule (every override -1) until dk_diag_rx_set_tuning
     // Empty socket table: every probe misses.
     std::vector<uint32_t> slots(dk::kMinTableSlots * 4 + dk::kPortTabWords, 0u);
     std::fill(slots.begin() + dk::kMinTableSlots * 4, slots.end(), DK_FLOW_NONE);
@@ -877,7 +858,6 @@ int dk_diag_path_stats_read(dk_rx_ctx* c, uint64_t out[4]) {
 
 int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t* knobs, uint32_t nknobs) {
     if (!c || (nknobs && !knobs)) return EINVAL;
-    const int32_t zc = c->tune.host_zc;  // not a diag knob: kept from DK_RX_HOST_ZC
     int32_t k[DK_DIAG_RX_KNOBS];
     for (uint32_t i = 0; i < DK_DIAG_RX_KNOBS; i++) k[i] = i < nknobs ? knobs[i] : -1;
     Tuning t;
@@ -891,7 +871,7 @@ int dk_diag_rx_set_tuning(dk_rx_ctx* c, const int32_t* knobs, uint32_t nknobs) {
     t.lds_table = k[7];
     t.tail = k[8];
     t.udp_table = k[9];
-    t.host_zc = zc;
+    t.host_zc = k[10];
     c->tune = t;
     c->occ_family = ~0u;
     c->lt_occ_family = ~0u;

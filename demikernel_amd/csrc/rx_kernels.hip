@@ -57,6 +57,7 @@ constexpr uint32_t kIcmpTypes = (1u << 0) | (1u << 3) | (1u << 4) | (1u << 5) | 
 #endif
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
+static_assert(kWaves == (int)kStagedWaves, "the host computes the dynamic tail's boundary with kStagedWaves");
 constexpr uint32_t kCoopU = DK_COOP_U; // dwordx4 loads per lane per phase-B round
 constexpr uint32_t kCoopSpan = 16 * kCoopU;  // 16-byte blocks one quarter-wave covers per round
 #ifndef DK_ROUNDS_PER_STEP

@@ -16,7 +16,7 @@
 //      64 segments classified in parallel per step, the state machine only for the segments that need it;
 //   4''. the scan walk for few connections with many segments each (dk_tcp_scan_pre_kernel, dk_tcp_scan_kernel,
 //      dk_tcp_scan_post_kernel): windows precomputed across the chip, 64 windows resolved per wave scan, the decided
-//      windows written in parallel (below); dk_tcp_relay_walk_kernel (DK_TCP_WALK=relay): 8 waves per connection
+//      windows written in parallel (below); dk_tcp_relay_walk_kernel (dk_diag_tcp_set_walk): 8 waves per connection
 //      take its windows in turn and pass its state from window to window through LDS.
 // Segments whose outcome cannot depend on their place in the connection's order are classified in step 1 and never
 // walked: RCV.NXT only moves forward, from its value at the start of the batch up to the window end (reader_next +
@@ -38,6 +38,7 @@
 #include <cstddef>
 #include <cstring>
 
+#include "../../include/dk_diag.h"
 #include "../../include/dk_tcp.h"
 
 namespace dk_tcp {
@@ -1337,8 +1338,7 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_post_kernel(Params P) 
 }
 #undef DK_U
 
-// Which walk runs: `force` (DK_TCP_WALK=lane|wave|relay|scan, read once at dk_tcp_ctx_create: 0 lane, 1 wave, 2
-// relay, 3 scan, -1 the rule); otherwise one lane per connection below kWaveWalkMinSegs segments per connection, the
+// Which walk runs: `force` (dk_diag_tcp_set_walk: 0 lane, 1 wave, 2 relay, 3 scan, -1 the rule); otherwise one lane per connection below kWaveWalkMinSegs segments per connection, the
 // scan walk from kScanMinSegs (16 windows) for up to DK_TCP_SCAN_MAX_CONNS connections, else one wave per connection.
 // 1M segments (sessions r05zt-r05zv, profiles/r05_tcp_walks.jsonl): 1 connection scan 0.87 ms, relay 3.8, wave 12.7;
 // 16: scan 0.29, wave 0.94; 64: scan 0.22, relay 0.23, wave 0.31; 256: scan 0.19, wave 0.18; 1,024: wave 0.14, relay
@@ -1394,8 +1394,8 @@ int grow(T*& p, size_t& cap, size_t n) {
 // two streams never overlap on the scratch, and growing it waits for that work before freeing.
 struct dk_tcp_ctx {
     int device = 0;
-    int walk = -1;  // DK_TCP_WALK at creation: 0 lane, 1 wave, 2 relay, 3 scan, -1 the engine's rule
-    int relay_waves = 8;  // DK_TCP_RELAY_WAVES at creation (4 / 8 / 16; 8 measured best, session r05r)
+    int walk = -1;  // dk_diag_tcp_set_walk: 0 lane, 1 wave, 2 relay, 3 scan, -1 the engine's rule
+    int relay_waves = 8;  // dk_diag_tcp_set_walk (4 / 8 / 16; 8 measured best, session r05r)
     hipEvent_t last = nullptr;
     hipStream_t last_stream = nullptr;
     bool used = false;
@@ -1421,14 +1421,18 @@ int dk_tcp_ctx_create(int32_t device, dk_tcp_ctx** out) {
     dk_tcp::DeviceGuard g(device);
     dk_tcp_ctx* t = new dk_tcp_ctx();
     t->device = device;
-    if (const char* e = getenv("DK_TCP_WALK"))
-        t->walk = !strcmp(e, "scan") ? 3 : !strcmp(e, "relay") ? 2 : !strcmp(e, "wave") ? 1 : !strcmp(e, "lane") ? 0 : -1;
-    if (const char* e = getenv("DK_TCP_RELAY_WAVES")) t->relay_waves = atoi(e);
     if (hipEventCreateWithFlags(&t->last, hipEventDisableTiming) != hipSuccess) {
         delete t;
         return EINVAL;
     }
     *out = t;
+    return 0;
+}
+
+int dk_diag_tcp_set_walk(dk_tcp_ctx* t, int32_t walk, int32_t relay_waves) {
+    if (!t || walk < -1 || walk > 3) return EINVAL;
+    t->walk = walk;
+    t->relay_waves = relay_waves == 4 || relay_waves == 16 ? relay_waves : 8;
     return 0;
 }
 

@@ -164,8 +164,9 @@ class RxResults:
             self.t["tcp_opts"] = torch.zeros(max(n, 1) * N.TCP_OPTS_DTYPE.itemsize, dtype=torch.uint8, **kw)
 
     def c_struct(self) -> N.DkRxResults:
-        """The ABI struct, rebuilt when an array was replaced (the arrays are fixed at construction)."""
-        key = tuple(map(id, self.t.values()))
+        """The ABI struct, rebuilt when an array was replaced: keyed on each array's name and device address (an id()
+        could be reused by a replacement tensor after the old one is freed)."""
+        key = tuple((k, _ptr(v)) for k, v in self.t.items())
         c = self.__dict__.get("_cs")
         if c is None or c[0] != key:
             c = (key, N.DkRxResults(*[_ptr(self.t.get(name)) for name in N.RESULT_FIELDS]))
@@ -191,7 +192,10 @@ class RxResults:
 class RxEngine:
     """Batch receive path on one GPU (the drop-in for layer2..layer4 receive + demux, see module docstring)."""
 
-    def __init__(self, config: Config, device: int = 0, lib_path: Optional[str] = None):
+    def __init__(self, config: Config, device: int = 0, lib_path: Optional[str] = None,
+                 tuning: Optional[dict] = None):
+        """tuning: diagnostic overrides passed to set_tuning right after the context is created (tests and A/B tools;
+        the engine's own rule otherwise — the process environment is never consulted)."""
         self.lib = N.load_library() if lib_path is None else N.load_library(lib_path)
         self.config = config
         self.device = device
@@ -205,6 +209,8 @@ class RxEngine:
         # to the counter arrays (dk_rx.h DK_RX_BATCH_DEFER_COUNTS), so the arrays are kept alive until the next launch
         # on the stream, a flush, forget_stream or close
         self._pending = {}
+        if tuning:
+            self.set_tuning(**tuning)
 
     @property
     def flow_counts_deferred(self) -> bool:
@@ -310,7 +316,7 @@ class RxEngine:
     def set_tuning(self, **knobs) -> None:
         """Diagnostics (dk_diag.h): override the engine's kernel family / schedule / grid choices (-1 = its rule);
         unnamed knobs go back to the rule. Names: N.DK_DIAG_RX_KNOBS (stage, split, small, sched, grid, grid_per_cu, debug,
-        lds_table, tail, udp_table)."""
+        lds_table, tail, udp_table, host_zc)."""
         bad = set(knobs) - set(N.DK_DIAG_RX_KNOBS)
         assert not bad, bad
         arr = (ctypes.c_int32 * len(N.DK_DIAG_RX_KNOBS))(*[int(knobs.get(k, -1)) for k in N.DK_DIAG_RX_KNOBS])

@@ -68,12 +68,17 @@ class TcpOut:
 class TcpReceiver:
     """Per-GPU TCP receive processing over a device connection table (the ControlBlock receive halves)."""
 
-    def __init__(self, device: int = 0, lib_path: str | None = None):
+    def __init__(self, device: int = 0, lib_path: str | None = None, walk: str | None = None, relay_waves: int = 8):
+        """walk: a diagnostic override of the engine's walk choice ("lane", "wave", "relay", "scan"; None = the rule),
+        set through dk_diag_tcp_set_walk."""
         self.lib = N.load_library(lib_path) if lib_path else N.load_library()
         self.device = device
         h = ctypes.c_void_p()
         _check(self.lib.dk_tcp_ctx_create(device, ctypes.byref(h)), "dk_tcp_ctx_create")
         self._ctx = h
+        if walk is not None or relay_waves != 8:
+            _check(self.lib.dk_diag_tcp_set_walk(self._ctx, N.DK_TCP_WALKS[walk] if walk else -1, relay_waves),
+                   "dk_diag_tcp_set_walk")
 
     def close(self) -> None:
         if self._ctx:

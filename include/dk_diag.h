@@ -27,22 +27,29 @@ struct dk_rx_ctx;
 int dk_diag_path_stats_enable(struct dk_rx_ctx* ctx, int on);       /* 0, EINVAL or ENOMEM; on: counters reset */
 int dk_diag_path_stats_read(struct dk_rx_ctx* ctx, uint64_t out[4]); /* synchronous; 0 or EINVAL */
 
-/* Tuning overrides for A/B measurements and tests (-1 = the engine's own rule). A receive context reads them once from
- * the environment when it is created (DK_RX_STAGE, DK_RX_SPLIT, DK_RX_SMALL, DK_RX_SCHED, DK_RX_GRID,
- * DK_RX_GRID_PER_CU, DK_RX_DEBUG, DK_RX_LDS_TABLE, DK_RX_TAIL, DK_RX_UDP_TABLE), never on the launch path; this call
- * replaces them. knobs[] = {stage, split, small, sched, grid, grid_per_cu, debug, lds_table, tail, udp_table}:
+/* Tuning overrides for A/B measurements and tests (-1 = the engine's own rule). A receive context starts on the
+ * built-in rule and nothing but this call changes it: the process environment is never read (a LibOS process that
+ * inherits an environment gets the same kernels as any other). knobs[] = {stage, split, small, sched, grid,
+ * grid_per_cu, debug, lds_table, tail, udp_table, host_zc}:
  * stage/split/small force a kernel family on (1) or off (0), sched picks the wave schedule (0 round-robin tiles, 1 one
  * contiguous share per wave), grid / grid_per_cu fix the persistent grid, debug > 0 prints each launch's choice to
  * stderr, lds_table 0 keeps Active lookups on the global socket table (no LDS copy), tail sets the staged kernel's
- * dynamic tail (0 off, d > 0: the last ~d rounds of chunks handed out by per-XCD counters instead of round-robin),
+ * dynamic tail (0 off, d > 0: the last ~d rounds of chunks handed out by per-pool counters instead of round-robin),
  * udp_table 0 / 1: the small-frame kernel looks local UDP binds up in the port table / in its LDS bind table whenever
- * that fits (the rule: when the binds are scattered over the port table). */
-#define DK_DIAG_RX_KNOBS 10
+ * that fits (the rule: when the binds are scattered over the port table), host_zc 0: dk_rx_process_host stages
+ * frames through HBM copies even when they are in mapped page-locked memory (the rule reads them in place). */
+#define DK_DIAG_RX_KNOBS 11
 /* knobs[0 .. nknobs): the caller says how many it passes (knobs past nknobs are -1, the rule), so a caller built
  * against an older, shorter list never has its array read past its end. 0 or EINVAL. */
 int dk_diag_rx_set_tuning(struct dk_rx_ctx* ctx, const int32_t* knobs, uint32_t nknobs);
-/* The same for dk_tx_checksum (process-wide; first read from DK_TX_SPLIT, DK_RX_SCHED, DK_RX_GRID_PER_CU). */
-int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu); /* 0 */
+/* The same for dk_tx_checksum / dk_tx_checksum_fields (process-wide, -1 = the rule). 0. */
+int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu);
+
+/* Which walk dk_tcp_rx_process runs (dk_tcp.h): walk -1 the engine's rule, 0 one lane per connection, 1 one wave per
+ * connection, 2 the relay walk (relay_waves 4 / 8 / 16 waves per connection, else 8), 3 the scan walk. A TCP context
+ * starts on the rule; the environment is never read. 0 or EINVAL. */
+struct dk_tcp_ctx;
+int dk_diag_tcp_set_walk(struct dk_tcp_ctx* ctx, int32_t walk, int32_t relay_waves);
 
 #ifdef __cplusplus
 }

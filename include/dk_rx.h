@@ -33,8 +33,8 @@
  *     different streams of one context may run concurrently; counters they share are added atomically. A stream
  *     handed to dk_rx_process must stay valid while the context lives, or be released with dk_rx_stream_forget
  *     before it is destroyed (a later stream may reuse its handle value).
- *   - Tuning: the engine's choices (kernel family, grid) follow the batch; overrides are diagnostics (dk_diag.h),
- *     read from the environment once, when the context is created.
+ *   - Tuning: the engine's choices (kernel family, grid) follow the batch; overrides are diagnostics set only by an
+ *     explicit dk_diag_rx_set_tuning call (dk_diag.h). The process environment is never read.
  *   - No torch / HIP types in signatures: streams are passed as void* (a hipStream_t, NULL = default stream).
  */
 #ifndef DK_RX_H

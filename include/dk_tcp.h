@@ -23,9 +23,9 @@
  * first waits (on the device) for the previous call's work — so use one context per stream for concurrent batches.
  * The engine picks its per-connection walk from the batch (one lane per connection; one wave per connection at
  * >= 8 segments per connection; at >= 1,024 segments per connection and <= 256 connections the scan walk: windows
- * precomputed across the chip, 64 windows per wave scan per connection, the rest in parallel); the environment
- * variable DK_TCP_WALK=lane|wave|relay|scan, read when the context is created, forces one (relay: 8 waves per
- * connection passing its state window to window). Results are identical.
+ * precomputed across the chip, 64 windows per wave scan per connection, the rest in parallel); the diagnostic
+ * dk_diag_tcp_set_walk (dk_diag.h) forces one (relay: 8 waves per connection passing its state window to window).
+ * The environment is never read. Results are identical.
  */
 #ifndef DK_TCP_H
 #define DK_TCP_H

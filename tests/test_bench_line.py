@@ -47,3 +47,14 @@ def test_single_gpu_line():
     f = bench.scale_fields(1, None, rows(1), [], 8)
     assert f["rccl_nranks"] is None and f["collective_kind"] == "none" and f["gather_every"] is None
     assert f["collective_ms_avg"] is None and len(f["per_rank"]) == 1
+
+
+def test_missized_communicator_is_refused():
+    """an RCCL communicator that does not hold every rank exits non-zero (status 4), never a line."""
+    import pytest
+
+    for nranks, world in ((1, 8), (4, 8), (8, 4)):
+        with pytest.raises(SystemExit) as e:
+            bench.scale_fields(world, FakeRccl(nranks), rows(world), [0.008], 8)
+        assert e.value.code == 4
+    bench.check_comm_size(2, 2)  # the right size passes

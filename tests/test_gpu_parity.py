@@ -23,10 +23,17 @@ def torch_cuda():
     return torch
 
 
-def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None, aligned16=None, dst_ip=True):
+def family(name: str) -> dict:
+    """dk_diag_rx_set_tuning knobs that force one kernel family (tests pass them explicitly: the engine never reads the
+    process environment)."""
+    return {"small": int(name == "small"), "stage": int(name != "unstaged"), "split": int(name == "split")}
+
+
+def run_gpu(blob, off, lens, flows, cfg=None, tcp_fields=True, frames_bytes=None, aligned16=None, dst_ip=True,
+            tuning=None):
     import torch
 
-    eng = RxEngine(cfg or Config(LOCAL), device=0)
+    eng = RxEngine(cfg or Config(LOCAL), device=0, tuning=tuning)
     eng.set_sockets(flows)
     b = FrameBatch.from_numpy(blob, off, lens, device=0)
     if aligned16 is not None:  # override the hint: both kernel instantiations see the same inputs
@@ -60,9 +67,10 @@ def assert_same(got, exp, ctx=""):
             raise AssertionError(f"{ctx}: '{k}' differs at {bad}: got {v[bad]} exp {e[bad]}{extra}")
 
 
-def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None, dst_ip=True, tcp_fields=True):
+def check(blob, off, lens, flows, cfg=None, ctx="", frames_bytes=None, aligned16=None, dst_ip=True, tcp_fields=True,
+          tuning=None):
     got = run_gpu(blob, off, lens, flows, cfg, frames_bytes=frames_bytes, aligned16=aligned16, dst_ip=dst_ip,
-                  tcp_fields=tcp_fields)
+                  tcp_fields=tcp_fields, tuning=tuning)
     exp = run_oracle(blob, off, lens, flows, cfg, frames_bytes=frames_bytes)
     assert_same(got, exp, ctx)
     return got
@@ -105,34 +113,29 @@ def test_random_batches(torch_cuda, mix, hint):
 @pytest.mark.parametrize("record", ["libos", "headline"])
 @pytest.mark.parametrize("grid", [None, "7"])
 @pytest.mark.parametrize("sched", ["0", "1"])
-@pytest.mark.parametrize("family", ["unstaged", "staged", "split", "small"])
-def test_kernel_variants(torch_cuda, monkeypatch, family, sched, grid, record):
+@pytest.mark.parametrize("fam", ["unstaged", "staged", "split", "small"])
+def test_kernel_variants(torch_cuda, fam, sched, grid, record):
     """Every shipped kernel family (results stored per chunk / staged in registers / split stream+finish waves /
     small-frame kernel, whose frames past the 64-byte window are summed wave-wide) under both wave schedules, with a
     grid small enough that each wave walks many chunks (staged results flushed mid-loop and at exit) and with the
     default grid. The split kernel always walks sched 0. Under sched 1 every family writes the 20-byte layout (no
     dst_ip, ABI 3). Both records: with the TCP fields (the LibOS record) and without (the 24-byte record bench.py
     times), i.e. every instantiation of every family."""
-    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
-    monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
-    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
-    monkeypatch.setenv("DK_RX_SCHED", sched)
-    if grid is not None:
-        monkeypatch.setenv("DK_RX_GRID", grid)
+    tune = {**family(fam), "sched": int(sched), "grid": int(grid) if grid else -1}
     n = 12345
     flows = np.concatenate([synth.make_flows(300), synth.make_flows(20, kind="udp")])
     tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=4), flows, seed=6)
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.05, tr))
     perm = np.random.default_rng(8).permutation(n)
-    got = check(blob, off[perm], lens[perm], flows, ctx=f"{family} sched={sched} grid={grid} {record}",
-                dst_ip=sched != "1", tcp_fields=record == "libos")
+    got = check(blob, off[perm], lens[perm], flows, ctx=f"{fam} sched={sched} grid={grid} {record}",
+                dst_ip=sched != "1", tcp_fields=record == "libos", tuning=tune)
     assert ("dst_ip" in got) == (sched != "1") and ("tcp_seq" in got) == (record == "libos")
 
 
-@pytest.mark.parametrize("grid", ["7", "40"])
+@pytest.mark.parametrize("grid", ["7", "10", "12", "40"])
 @pytest.mark.parametrize("tail", ["0", "1", "2", "4", "12"])
-def test_staged_dynamic_tail(torch_cuda, monkeypatch, capfd, tail, grid):
+def test_staged_dynamic_tail(torch_cuda, capfd, tail, grid):
     """The staged kernel's dynamic tail (rx_common.h kTailXcds): the last rounds of chunks handed out by per-pool
     counters (pools keyed by workgroup index). Every depth from off (0) to most of the batch grabbed (12), on grids of
     7 (one pool) and 40 workgroups (8 pools; many chunks per wave), IMIX with a corrupted tail, 16-byte aligned and at
@@ -141,12 +144,7 @@ def test_staged_dynamic_tail(torch_cuda, monkeypatch, capfd, tail, grid):
     the oracle. The debug line shows the round-robin rounds the host chose."""
     import torch
 
-    monkeypatch.setenv("DK_RX_SMALL", "0")
-    monkeypatch.setenv("DK_RX_STAGE", "1")
-    monkeypatch.setenv("DK_RX_SPLIT", "0")
-    monkeypatch.setenv("DK_RX_TAIL", tail)
-    monkeypatch.setenv("DK_RX_GRID", grid)
-    monkeypatch.setenv("DK_RX_DEBUG", "1")
+    tune = {**family("staged"), "tail": int(tail), "grid": int(grid), "debug": 1}
     n = 60000
     flows = np.concatenate([synth.make_flows(300), synth.make_flows(20, kind="udp")])
     tr = synth.traffic(n, synth.imix_ip_lengths(n, seed=44), flows, seed=45)
@@ -157,7 +155,7 @@ def test_staged_dynamic_tail(torch_cuda, monkeypatch, capfd, tail, grid):
             off = off + 2
         synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
         exp = run_oracle(blob, off, lens, flows)
-        eng = RxEngine(Config(LOCAL), device=0)
+        eng = RxEngine(Config(LOCAL), device=0, tuning=tune)
         eng.set_sockets(flows)
         b = FrameBatch.from_numpy(blob, off, lens, device=0)
         rs = [eng.results(n) for _ in range(4)]
@@ -177,17 +175,14 @@ def test_staged_dynamic_tail(torch_cuda, monkeypatch, capfd, tail, grid):
         assert want > 0
 
 
-@pytest.mark.parametrize("family", ["staged", "unstaged"])
+@pytest.mark.parametrize("fam", ["staged", "unstaged"])
 @pytest.mark.parametrize("align", [64, 16, 4, 2])
-def test_packed_layouts(torch_cuda, monkeypatch, family, align):
+def test_packed_layouts(torch_cuda, fam, align):
     """Frames packed back to back in the blob at several slot alignments (64-byte slots with padding between frames;
     16; 4 and 2, where a frame often ends inside the granule the next one starts in), IMIX and random lengths, with a
     corrupted tail and, in the second batch, a shuffled stretch of descriptors and one frame at an odd address, against
     the oracle. (Round 3 ran it against a window-stream build, which read packed chunks lane-contiguously: 75 GPU parity
     tests green, IMIX 33 % slower, not kept: DESIGN.md §8.)"""
-    monkeypatch.setenv("DK_RX_SMALL", "0")
-    monkeypatch.setenv("DK_RX_SPLIT", "0")
-    monkeypatch.setenv("DK_RX_STAGE", "1" if family == "staged" else "0")
     flows = np.concatenate([synth.make_flows(200), synth.make_flows(16, kind="udp")])
     rng = np.random.default_rng(align)
     for trial, n in enumerate((9000, 7000)):
@@ -204,14 +199,14 @@ def test_packed_layouts(torch_cuda, monkeypatch, family, align):
             odd = int(blob.size - 3000) | 1
             blob[odd: odd + int(lens[5000])] = blob[int(off[5000]): int(off[5000]) + int(lens[5000])]
             off[5000] = odd
-        check(blob, off, lens, flows, ctx=f"{family} align={align} trial={trial}")
+        check(blob, off, lens, flows, ctx=f"{fam} align={align} trial={trial}", tuning=family(fam))
 
 
 @pytest.mark.parametrize("sizes", ["imix", "1500"])
 @pytest.mark.parametrize("nact", [1, 7, 1024, 2600, 4096, 5000])
-def test_lds_active_table(torch_cuda, monkeypatch, capfd, nact, sizes):
+def test_lds_active_table(torch_cuda, capfd, nact, sizes):
     """The LDS copy of the Active table (rx_common.h: minimal perfect hash, staged and split kernels) against the
-    oracle, and against the global table (DK_RX_LDS_TABLE=0): 20 % of the TCP segments come from remote endpoints that
+    oracle, and against the global table (lds_table=0): 20 % of the TCP segments come from remote endpoints that
     are not in the table (they land on another key's slot and must fail its compare, then take the Passive listener),
     plus a duplicated Active key (the last one wins) and Active entries on another local address (never found). 5,000
     keys exceed kLtMaxKeys (global table only); the debug line says which path ran."""
@@ -231,10 +226,8 @@ def test_lds_active_table(torch_cuda, monkeypatch, capfd, nact, sizes):
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr))
     exp = run_oracle(blob, off, lens, flows)
-    monkeypatch.setenv("DK_RX_DEBUG", "1")
     for lt in ("-1", "0"):
-        monkeypatch.setenv("DK_RX_LDS_TABLE", lt)
-        got = run_gpu(blob, off, lens, flows)
+        got = run_gpu(blob, off, lens, flows, tuning={"debug": 1, "lds_table": int(lt)})
         assert_same(got, exp, f"nact={nact} {sizes} lds_table={lt}")
         used = [int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("lds_table=")]
         assert used, "no debug line"
@@ -263,11 +256,11 @@ def test_misaligned_and_offsets(torch_cuda):
     check(blob, off[perm], lens2[perm], flows, ctx="misaligned, aligned16 hint", aligned16=True)
 
 
-def test_small_kernel_mixed(torch_cuda, monkeypatch):
+def test_small_kernel_mixed(torch_cuda):
     """The small-frame kernel on what it is chosen for (minimum-size frames) with a few large frames mixed in, at
     every even and odd offset mod 16: the wave-wide sum of frames past the register window, the realigned header
     window and the last granule in LDS must give the oracle's result."""
-    monkeypatch.setenv("DK_RX_SMALL", "1")
+    T = {"small": 1}
     flows = np.concatenate([synth.make_flows(64, kind="udp"), synth.make_flows(64)])
     n = 4000
     rng = np.random.default_rng(12)
@@ -279,13 +272,13 @@ def test_small_kernel_mixed(torch_cuda, monkeypatch):
     synth.corrupt_numpy(blob0, off0, synth.corruption_plan(n, 0.05, tr))
     frames = [blob0[o:o + L].tobytes() for o, L in zip(off0, lens)]
     blob, off, lens2 = F.pack(frames, align=64, misalign=list(range(16)))
-    check(blob, off, lens2, flows, ctx="small kernel, misaligned")
+    check(blob, off, lens2, flows, ctx="small kernel, misaligned", tuning=T)
     # no optional outputs requested: the instantiation without the TCP-field / path-stats stores
-    got = run_gpu(blob, off, lens2, flows, tcp_fields=False)
+    got = run_gpu(blob, off, lens2, flows, tcp_fields=False, tuning=T)
     assert "tcp_seq" not in got
     assert_same(got, run_oracle(blob, off, lens2, flows), "small kernel, no optional outputs")
     blob, off, lens2 = F.pack(frames, align=64)
-    check(blob, off, lens2, flows, ctx="small kernel, aligned16 hint", aligned16=True)
+    check(blob, off, lens2, flows, ctx="small kernel, aligned16 hint", aligned16=True, tuning=T)
 
 
 def test_fuzz_headers(torch_cuda):
@@ -417,9 +410,9 @@ def test_port_table_lookups(torch_cuda, local):
     assert {"OK_UDP", "UDP_NOSOCK", "OK_TCP", "TCP_NOSOCK"} <= seen, seen
 
 
-@pytest.mark.parametrize("family", ["small", "staged", "split", "unstaged"])
+@pytest.mark.parametrize("fam", ["small", "staged", "split", "unstaged"])
 @pytest.mark.parametrize("udp_table", ["0", "1", "-1"])
-def test_udp_bind_table(torch_cuda, monkeypatch, capfd, family, udp_table):
+def test_udp_bind_table(torch_cuda, capfd, fam, udp_table):
     """Local UDP binds looked up in the small-frame kernel's LDS bind table (rx_common.h: a two-choice cuckoo table
     built from the port table; its window and the general pass's last granules then share LDS) or in the port table:
     forced off (0), whenever it fits (1) and by the host's rule (1,024 binds on random ports: the table), in every
@@ -428,11 +421,7 @@ def test_udp_bind_table(torch_cuda, monkeypatch, capfd, family, udp_table):
     small-frame kernel and IMIX sizes for the others; bit-exact vs the oracle. The debug line shows the host's choice."""
     from demikernel_amd._native import DK_FLOW_UDP as UDP
 
-    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
-    monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
-    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
-    monkeypatch.setenv("DK_RX_UDP_TABLE", udp_table)
-    monkeypatch.setenv("DK_RX_DEBUG", "1")
+    tune = {**family(fam), "udp_table": int(udp_table), "debug": 1}
     lip = ipv4(LOCAL)
     binds = synth.make_flows(1024, kind="udp_random_ports", seed=31)
     binds["local_port"][7] = 65535
@@ -443,30 +432,28 @@ def test_udp_bind_table(torch_cuda, monkeypatch, capfd, family, udp_table):
     unbound = np.array([(UDP, lip, 0, p, 0) for p in (999, 1000, 1001, 2, 64000)], dtype=FLOW_DTYPE)
     targets = np.concatenate([flows, unbound])
     n = 30000
-    ip_len = 50 if family == "small" else synth.imix_ip_lengths(n, seed=32)
+    ip_len = 50 if fam == "small" else synth.imix_ip_lengths(n, seed=32)
     tr = synth.traffic(n, ip_len, targets, seed=33)
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
-    got = check(blob, off, lens, flows, ctx=f"udp table {family} {udp_table}")
+    got = check(blob, off, lens, flows, ctx=f"udp table {fam} {udp_table}", tuning=tune)
     seen = {VERDICTS[m & 0xFF] for m in got["meta"]}
     assert {"OK_UDP", "UDP_NOSOCK", "OK_TCP"} <= seen, seen
     modes = {int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("udp_table=")}
-    assert modes == {1 if family == "small" and udp_table != "0" else 0}, modes
+    assert modes == {1 if fam == "small" and udp_table != "0" else 0}, modes
 
 
 @pytest.mark.parametrize("nbinds,want", [(16, 1), (512, 1), (2048, 0)])
-def test_udp_bind_table_fit(torch_cuda, monkeypatch, capfd, nbinds, want):
+def test_udp_bind_table_fit(torch_cuda, capfd, nbinds, want):
     """The host's rule for the small-frame kernel's LDS bind table: binds on random ports take it while it fits at the
     occupancy the kernel has without it (16 and 512 binds: 128 B and 4 KiB), and not when it would cost a workgroup per
     CU (2,048 binds: 16 KiB beside the flow histogram); bit-exact vs the oracle either way."""
-    monkeypatch.setenv("DK_RX_SMALL", "1")
-    monkeypatch.setenv("DK_RX_DEBUG", "1")
     flows = synth.make_flows(nbinds, kind="udp_random_ports", seed=nbinds)
     n = 20000
     tr = synth.traffic(n, 50, flows, seed=nbinds + 1)
     blob, off, lens = synth.build_numpy(tr)
     synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.02, tr))
-    check(blob, off, lens, flows, ctx=f"udp bind table fit {nbinds}")
+    check(blob, off, lens, flows, ctx=f"udp bind table fit {nbinds}", tuning={"small": 1, "debug": 1})
     modes = {int(w.split("=")[1]) for w in capfd.readouterr().err.split() if w.startswith("udp_table=")}
     assert modes == {want}, modes
 
@@ -563,7 +550,7 @@ def test_tx_checksum_large_frames_schedule(torch_cuda):
 
 @pytest.mark.parametrize("sizes", ["imix", "min64"])
 @pytest.mark.parametrize("mem", ["pageable", "pinned_staged", "pinned_zero_copy"])
-def test_host_pipeline_matches_device_path(torch_cuda, monkeypatch, mem, sizes):
+def test_host_pipeline_matches_device_path(torch_cuda, mem, sizes):
     """dk_rx_process_host gives the oracle's results from pageable memory (staged copies), from pinned memory with
     staging forced (DK_RX_HOST_ZC=0), and from pinned, GPU-mapped memory read in place (the default there); IMIX
     sizes (staged kernel) and 64-byte frames (small-frame kernel with its deferred general pass, per chunk)."""
@@ -580,9 +567,7 @@ def test_host_pipeline_matches_device_path(torch_cuda, monkeypatch, mem, sizes):
     exp = run_oracle(blob, off, lens, flows)
     if mem != "pageable":
         blob = torch.from_numpy(blob).pin_memory().numpy()
-    if mem == "pinned_staged":
-        monkeypatch.setenv("DK_RX_HOST_ZC", "0")
-    eng = RxEngine(Config(LOCAL))
+    eng = RxEngine(Config(LOCAL), tuning={"host_zc": 0} if mem == "pinned_staged" else None)
     eng.set_sockets(flows)
     r = RxResults(n, len(flows), tcp_fields=True, host=True)
     eng.receive_batch_host(blob, off, lens, r, chunk_frames=7000)
@@ -1032,7 +1017,7 @@ def test_reference_udp_kat_through_hip(torch_cuda, offload):
         assert got["src_ip"][k] == int(g["src"]) and got["flow_id"][k] == 0
 
 
-def test_flow_counter_modes_and_wrap_guard(torch_cuda, monkeypatch):
+def test_flow_counter_modes_and_wrap_guard(torch_cuda):
     """Per-flow counts on both counter paths (LDS histogram up to 32768 flows, global atomics above) and the packed-u16
     wrap guard: one workgroup asked to count 100k frames of one flow must still count exactly."""
     for nflows in (32767, 32768, 32769):
@@ -1046,34 +1031,27 @@ def test_flow_counter_modes_and_wrap_guard(torch_cuda, monkeypatch):
     n = 100_000
     tr = synth.traffic(n, 40, flows, seed=1)
     blob, off, lens = synth.build_numpy(tr)
-    monkeypatch.setenv("DK_RX_GRID", "1")
-    got = run_gpu(blob, off, lens, flows)
+    got = run_gpu(blob, off, lens, flows, tuning={"grid": 1})
     assert int(got["flow_counts"][0]) == n and int(got["verdict_counts"][0]) == n
 
 
-@pytest.mark.parametrize("family", ["staged", "split", "small"])
-def test_counter_rows_accumulate(torch_cuda, monkeypatch, family):
+@pytest.mark.parametrize("fam", ["staged", "split", "small"])
+def test_counter_rows_accumulate(torch_cuda, fam):
     """The per-workgroup counter rows and dk_flow_reduce_kernel, per kernel family, on grids of 7 workgroups, the
     default and 1,500: three launches on one context accumulate exactly 3x the oracle's counts (rows are rewritten by
     every launch, never carried over); also with > 32,768 flows (verdict rows only) and with 300k frames on 20
     workgroups (15k frames per workgroup: the packed u16 halves near their limit)."""
     import torch
 
-    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
-    monkeypatch.setenv("DK_RX_STAGE", "1")
-    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
     cases = [(20000, 700, None), (20000, 700, "7"), (400000, 700, "1500"), (9000, 40000, None), (300000, 1, "20")]
     for n, nflows, grid in cases:
-        if grid is None:
-            monkeypatch.delenv("DK_RX_GRID", raising=False)
-        else:
-            monkeypatch.setenv("DK_RX_GRID", grid)
+        tune = {**family(fam), "grid": int(grid) if grid else -1}
         flows = np.concatenate([synth.make_flows(nflows, passive=False), synth.make_flows(8, kind="udp")])
-        ip_len = 50 if family == "small" else synth.imix_ip_lengths(n, seed=n)
+        ip_len = 50 if fam == "small" else synth.imix_ip_lengths(n, seed=n)
         tr = synth.traffic(n, ip_len, flows, seed=nflows)
         blob, off, lens = synth.build_numpy(tr)
         synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
-        eng = RxEngine(Config(LOCAL), device=0)
+        eng = RxEngine(Config(LOCAL), device=0, tuning=tune)
         eng.set_sockets(flows)
         b = FrameBatch.from_numpy(blob, off, lens, device=0)
         r = eng.results(n)
@@ -1083,14 +1061,14 @@ def test_counter_rows_accumulate(torch_cuda, monkeypatch, family):
         got = r.to_numpy()
         eng.close()
         exp = run_oracle(blob, off, lens, flows)
-        ctx = f"{family} n={n} flows={nflows} grid={grid}"
+        ctx = f"{fam} n={n} flows={nflows} grid={grid}"
         assert np.array_equal(got["flow_counts"], 3 * exp["flow_counts"][: len(got["flow_counts"])]), ctx
         assert np.array_equal(got["verdict_counts"], 3 * exp["verdict_counts"]), ctx
         assert np.array_equal(got["meta"], exp["meta"]) and np.array_equal(got["flow_id"], exp["flow_id"]), ctx
 
 
-@pytest.mark.parametrize("family", ["staged", "split", "small", "unstaged"])
-def test_deferred_counts(torch_cuda, monkeypatch, family):
+@pytest.mark.parametrize("fam", ["staged", "split", "small", "unstaged"])
+def test_deferred_counts(torch_cuda, fam):
     """DK_RX_BATCH_DEFER_COUNTS: a launch leaves its counter rows pending and the next launch on the stream adds them to
     the deferred launch's counters inside its own kernel (statically assigned row blocks, RowCombine), or dk_rx_counts_flush does.
     Per kernel family and grid (7 workgroups, the default, 1,500; > 32,768 flows: verdict rows only): two counter sets
@@ -1100,21 +1078,15 @@ def test_deferred_counts(torch_cuda, monkeypatch, family):
     every per-frame result is the oracle's."""
     import torch
 
-    monkeypatch.setenv("DK_RX_SMALL", "1" if family == "small" else "0")
-    monkeypatch.setenv("DK_RX_STAGE", "0" if family == "unstaged" else "1")
-    monkeypatch.setenv("DK_RX_SPLIT", "1" if family == "split" else "0")
     for n, nflows, grid in [(20000, 700, None), (20000, 700, "7"), (150000, 700, "1500"), (9000, 40000, None)]:
-        if grid is None:
-            monkeypatch.delenv("DK_RX_GRID", raising=False)
-        else:
-            monkeypatch.setenv("DK_RX_GRID", grid)
+        tune = {**family(fam), "grid": int(grid) if grid else -1}
         flows = np.concatenate([synth.make_flows(nflows, passive=False), synth.make_flows(8, kind="udp")])
-        ip_len = 50 if family == "small" else synth.imix_ip_lengths(n, seed=n)
+        ip_len = 50 if fam == "small" else synth.imix_ip_lengths(n, seed=n)
         tr = synth.traffic(n, ip_len, flows, seed=nflows + 1)
         blob, off, lens = synth.build_numpy(tr)
         synth.corrupt_numpy(blob, off, synth.corruption_plan(n, 0.03, tr))
         exp = run_oracle(blob, off, lens, flows)
-        ctx = f"{family} n={n} flows={nflows} grid={grid}"
+        ctx = f"{fam} n={n} flows={nflows} grid={grid}"
         small = FrameBatch.from_numpy(blob[: int(off[99]) + int(lens[99])], off[:100], lens[:100])
         exp_small = run_oracle(blob, off[:100], lens[:100], flows)
 
@@ -1123,7 +1095,7 @@ def test_deferred_counts(torch_cuda, monkeypatch, family):
             assert np.array_equal(got["flow_counts"], k * e["flow_counts"][: len(got["flow_counts"])]), (ctx, what)
             assert np.array_equal(got["verdict_counts"], k * e["verdict_counts"]), (ctx, what)
 
-        eng = RxEngine(Config(LOCAL), device=0)
+        eng = RxEngine(Config(LOCAL), device=0, tuning=tune)
         eng.set_sockets(flows)
         b = FrameBatch.from_numpy(blob, off, lens, device=0)
         ra, rb = eng.results(n), eng.results(n)

@@ -22,21 +22,13 @@ def tcp(request):
     """Every test runs through every walk: lanes = connections, one wave per connection with the parallel in-order
     check, 8 waves per connection relaying its state window to window, and the scan walk (windows precomputed across
     the chip, 64 windows per wave scan, the undecided ones through the state machine) (DK_TCP_WALK forces the choice
-    the engine otherwise makes from segments per connection)."""
-    import os
-
+    the engine otherwise makes from the batch; dk_diag_tcp_set_walk forces one)."""
     import torch
 
     assert torch.cuda.is_available()
-    old = os.environ.get("DK_TCP_WALK")
-    os.environ["DK_TCP_WALK"] = request.param
-    r = TcpReceiver(0)
+    r = TcpReceiver(0, walk=request.param)
     yield r
     r.close()
-    if old is None:
-        os.environ.pop("DK_TCP_WALK", None)
-    else:
-        os.environ["DK_TCP_WALK"] = old
 
 
 def rx_device(rx: dict):

@@ -22,8 +22,8 @@ def main():
     ap.add_argument("--grids", default="2,3,4")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--reps", type=int, default=7)
-    ap.add_argument("--scheds", default="", help="comma list of DK_RX_SCHED values to interleave (default: host rule)")
-    ap.add_argument("--knob", default="", help="NAME=v1,v2,...: interleave values of one more env knob (e.g. DK_RX_SPLIT=0,1)")
+    ap.add_argument("--scheds", default="", help="comma list of sched knob values to interleave (default: host rule)")
+    ap.add_argument("--knob", default="", help="NAME=v1,v2,...: interleave values of one more dk_diag_rx_set_tuning knob (e.g. DK_RX_SPLIT=0,1)")
     ap.add_argument("--tx", action="store_true", help="time dk_tx_checksum instead of the receive kernel")
     ap.add_argument("--rotate", type=int, default=1, help="distinct batches cycled per launch (C3: 8, past the MALL)")
     ap.add_argument("--frames", type=int, default=0, help="frames per batch (0: the workload's own)")
@@ -60,22 +60,13 @@ def main():
     for rep in range(args.reps):
         for g, cf in [(g, cf) for g in grids for cf in configs]:
             sc, kv = cf
-            if g > 0:  # builds that read the knobs per launch (round 1); 0 = the engine's own grid rule
-                os.environ["DK_RX_GRID_PER_CU"] = str(g)
-            else:
-                os.environ.pop("DK_RX_GRID_PER_CU", None)
-            if sc is not None:
-                os.environ["DK_RX_SCHED"] = sc
-            if kv is not None:
-                os.environ[kname] = kv
             knobs = {"grid_per_cu": g if g > 0 else -1}
             if sc is not None:
                 knobs["sched"] = int(sc)
             if kv is not None and kname.startswith("DK_RX_") and kname[6:].lower() in N.DK_DIAG_RX_KNOBS:
                 knobs[kname[6:].lower()] = int(kv)
             for k, (e, r) in engines.items():
-                if hasattr(e.lib, "dk_diag_rx_set_tuning"):  # later builds read them once per context
-                    e.set_tuning(**knobs)
+                e.set_tuning(**knobs)
                 run = ((lambda b: e.tx_checksum(b)) if args.tx else  # noqa: E731
                        (lambda b: e.receive_batch(b, r, defer_counts=args.defer)))
                 run(batch)
@@ -88,7 +79,7 @@ def main():
     if args.check and not args.tx:
         ref = None
         for k, (e, _) in engines.items():
-            os.environ.pop("DK_RX_GRID_PER_CU", None)
+            e.set_tuning()
             r = e.results(batch.n)
             e.receive_batch(batch, r)
             torch.cuda.synchronize()

@@ -5,7 +5,7 @@ of a 64-byte line (lg = 0..3), (f) in a TPACKET_V3 ring (block scan outside the 
 ring path with its scan; beside each, a host-side count of the 64-byte lines the kernel's loads touch per frame under
 the quarter-wave span plan (spans from the frame's first granule, rounds 1-4) and under line-aligned spans (round 5),
 counting a line once per load instruction that touches it (uncached host memory: no merging across instructions).
-One library per process (DK_RX_LIB_VARIANT selects a build): python tools/ring_bytes.py [--frames N]"""
+One library per process (--lib selects a build): python tools/ring_bytes.py [--frames N] [--lib path]"""
 import argparse
 import json
 import os
@@ -38,18 +38,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1 << 19)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="a variant libdk_rx.so (tools/variants.sh) instead of the in-tree one")
     args = ap.parse_args()
     import torch
 
     from demikernel_amd import Config, RxEngine, RxResults, synth
     from demikernel_amd import ring as RG
 
-    lib = os.path.basename(os.environ.get("DK_RX_LIB_VARIANT", "libdk_rx.so"))
+    lib = os.path.basename(args.lib or "libdk_rx.so")
     n = args.frames
     flows = synth.make_flows(1024)
     tr = synth.traffic(n, np.full(n, 1486, np.uint16), flows, seed=synth.SEED + 5)
     packed, poff, lens = synth.build_numpy(tr)
-    eng = RxEngine(Config(synth.BOB_IPV4), device=0)
+    eng = RxEngine(Config(synth.BOB_IPV4), device=0, lib_path=os.path.abspath(args.lib) if args.lib else None)
     eng.set_sockets(flows)
     res = RxResults(n, len(flows), host=True)
     nbytes = int(lens.astype(np.int64).sum())

@@ -1,4 +1,4 @@
-"""dk_tcp_rx_process time per walk (DK_TCP_WALK=lane|wave|relay|scan) on one connection's stream, with and without the
+"""dk_tcp_rx_process time per walk (lane|wave|relay|scan|rule, forced by dk_diag_tcp_set_walk) on one connection's stream, with and without the
 segments that need the state machine (synth.tcp_streams dup / oow / rare fractions), to separate the walks' per-window
 cost from their process() calls. One JSON line per (stream, walk): ms per call (HIP events, median)."""
 import argparse
@@ -44,10 +44,10 @@ for nconns in a.nconns:
         ref = None
         for walk, lib in [(w + (f":{k}" if w == "relay" else ""), lib) for w in a.walks
                           for k in (a.relay_waves if w == "relay" else [0]) for lib in a.libs]:
-            os.environ["DK_TCP_WALK"] = walk.split(":")[0]
-            if walk.startswith("relay"):
-                os.environ["DK_TCP_RELAY_WAVES"] = walk.split(":")[1]
-            tcp = TcpReceiver(0, lib_path=os.path.abspath(lib) if lib else None)
+            wname = walk.split(":")[0]
+            tcp = TcpReceiver(0, lib_path=os.path.abspath(lib) if lib else None,
+                              walk=None if wname == "rule" else wname,
+                              relay_waves=int(walk.split(":")[1]) if walk.startswith("relay") else 8)
             pristine = tcp.conns_to_device(table)
             conns = pristine.clone()
             out = TcpOut(a.nseg, len(table), 0)
