@@ -10,6 +10,7 @@
 //                       12 / 13 s_memrealtime at entry / exit
 //   dk_rx_small_kernel: 0 entry, 11 after the barrier, 1 first window, 2 + 3k .. 4 + 3k chunk k (k < 3), 16 + 5k + j
 //                       sub-phases j of phase C (k < 3), 14 after the combine, 15 exit, 12 / 13 realtime
+//   both, totals over every chunk (DK_ACC_*): 20.. per-phase shader-clock totals, 26 the wave's chunk count
 #pragma once
 
 #ifdef DK_DIAG_STAMPS
@@ -34,6 +35,32 @@ constexpr bool kPathStatsOn = true;
 }
 #define DK_DIAG_STAMP_AT(slot, t, wpg) do {} while (0)
 #define DK_SUB_STAMP(j) do {} while (0)
+#endif
+
+// Per-wave phase totals over ALL of a wave's chunks (stamps only cover chunks k < 3): DK_ACC_BEGIN() at a phase
+// boundary, DK_ACC_SPLIT(j) adds the shader-clock ticks since the last boundary to total j (< 6); DK_ACC_WRITE
+// stores the totals into slots 20..25 and the chunk count into slot 26. Nothing in the product build.
+#ifdef DK_DIAG_STAMPS
+#define DK_ACC_DECL uint64_t dk_acc_[6] = {0, 0, 0, 0, 0, 0}, dk_t_ = 0, dk_nch_ = 0
+#define DK_ACC_BEGIN() (dk_t_ = __builtin_amdgcn_s_memtime())
+#define DK_ACC_SPLIT(j)                                                                                             \
+    do {                                                                                                            \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                                           \
+        dk_acc_[j] += t_ - dk_t_;                                                                                   \
+        dk_t_ = t_;                                                                                                 \
+    } while (0)
+#define DK_ACC_CHUNK() (dk_nch_++)
+#define DK_ACC_WRITE(wpg)                                                                                           \
+    do {                                                                                                            \
+        for (int j_ = 0; j_ < 6; j_++) DK_DIAG_STAMP_AT(20 + j_, dk_acc_[j_], wpg);                                 \
+        DK_DIAG_STAMP_AT(26, dk_nch_, wpg);                                                                         \
+    } while (0)
+#else
+#define DK_ACC_DECL do {} while (0)
+#define DK_ACC_BEGIN() do {} while (0)
+#define DK_ACC_SPLIT(j) do {} while (0)
+#define DK_ACC_CHUNK() do {} while (0)
+#define DK_ACC_WRITE(wpg) do {} while (0)
 #endif
 
 // dk_rx_kernel / dk_rx_small_kernel shorthands: shader clock (per XCD) and the global 100 MHz clock

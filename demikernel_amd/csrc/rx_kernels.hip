@@ -1271,7 +1271,9 @@ void dk_rx_kernel(RxParams P) {
         nlen = P.len[c + r.lane_off];
     }
     WaveLds& W = s_wave[wv];
+    DK_ACC_DECL;
     for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
+        DK_ACC_BEGIN();
         // The lane id re-materialised per chunk: without this the compiler keeps ~20 lane-derived address constants
         // of phases A-C in VGPRs across the whole loop, and this kernel sits at its 168-VGPR budget (3 waves/SIMD).
         uint32_t lane = lane_id();
@@ -1303,8 +1305,10 @@ void dk_rx_kernel(RxParams P) {
         // its latency
         if (have && k + 2 >= ks) Q.issue(P, lane);
         if (k < 3) DK_STAMPW(3 + 3 * k);
+        DK_ACC_SPLIT(0);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (k < 3) DK_STAMPW(4 + 3 * k);
+        DK_ACC_SPLIT(1);
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
         // at the top of the next chunk, after a staged flush, their wait also waited for every store's write ack.
         asm volatile("" ::"v"(noff), "v"(nlen));
@@ -1316,17 +1320,24 @@ void dk_rx_kernel(RxParams P) {
                 nstg = 0;
             }
         }
+        DK_ACC_SPLIT(2);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
+        DK_ACC_SPLIT(3);
+        DK_ACC_CHUNK();
     }
 
     DK_STAMPW(11);
+    DK_ACC_BEGIN();
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, W.cb, lane);
+    DK_ACC_SPLIT(4);
     combine_pending_tail(P, lane, kWaves);  // a previous launch's deferred counter rows, in this wave's tail
+    DK_ACC_SPLIT(5);
     DK_STAMPW(14);
     __syncthreads();
     flush_counters(P, tid, kBlock, lds_flows, s_flow, s_vh);
     DK_STAMPW(15);
     DK_STAMPW_RT(13);
+    DK_ACC_WRITE(kWaves);
 }
 
 // Small-frame kernel (batches of minimum-size frames, C3): the per-chunk chain descriptor -> frame -> parse -> socket
@@ -1343,16 +1354,31 @@ void dk_rx_kernel(RxParams P) {
 // the chunk's frames lie in one window of <= kWinGran granules, ceil(G / 64) LDS-DMA loads
 // (buffer_load_dwordx4 ... lds, 1 KiB each, lane-contiguous) bring the window into the wave's LDS slot and every lane
 // reads its frame's 64 bytes back; scattered frames (e.g. one per 2 KiB mbuf) keep the per-lane loads.
-constexpr uint32_t kWinGran = 288;                    // 4.5 KiB: 64 packed 64-byte frames at any even offset
+#ifndef DK_WIN_GRAN
+#define DK_WIN_GRAN 288
+#endif
+constexpr uint32_t kWinGran = DK_WIN_GRAN;            // 4.5 KiB: 64 packed 64-byte frames at any even offset
 constexpr uint32_t kWinLoads = (kWinGran + 63) / 64;  // DMA loads for a full window
 // kUb: the last granules share the window's LDS (the general pass runs after the main loop's last window), leaving
 // room for the LDS bind table at three workgroups per CU; measured 3 % slower at C3 with the port table, so the
 // instantiation without the table keeps them apart (session r05zo).
+#ifndef DK_SMALL_LDS_UNION
+#define DK_SMALL_LDS_UNION 0  // 1: the general pass's last granules share the window's LDS in every instantiation
+#endif
 template <bool kUb>
 struct SmallLds {
     uint4 tail[64];             // the general pass: the last granule of each big frame (seg_sum_fast)
     uint4 win[kWinLoads * 64];  // the main loop: the chunk's frame window (whole 1 KiB DMA pieces)
 };
+#if DK_SMALL_LDS_UNION
+template <>
+struct SmallLds<false> {
+    union {
+        uint4 win[kWinLoads * 64];
+        uint4 tail[64];
+    };
+};
+#endif
 template <>
 struct SmallLds<true> {
     union {
@@ -1649,7 +1675,9 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     bool deferred = false;  // wave-uniform: a chunk left frames to the general pass
     // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
     uint64_t had = 0;
+    DK_ACC_DECL;
     for (uint32_t k = 0; have; k++) {
+        DK_ACC_BEGIN();
         // the lane id re-materialised per chunk (as in dk_rx_kernel): lane-derived constants are not held in VGPRs
         // across the loop
         uint32_t lane = lane_id();
@@ -1667,6 +1695,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         if (k == 0) DK_STAMP(1);
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
         if (k < 3) DK_STAMP(2 + 3 * k);
+        DK_ACC_SPLIT(0);
         if (kShift && __ballot(live && F.vec && !F.big && F.sh != 0)) {  // realign the windows of shifted frames
             uint32_t x[4] = {0, 0, 0, 0};
             if (F.vec && !F.big && F.sh != 0) realign(C.R.w, x, F.sh);
@@ -1676,12 +1705,15 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         deferred = deferred || dm != 0;
         small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid);
         if (k < 3) DK_STAMP(3 + 3 * k);
+        DK_ACC_SPLIT(1);
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
             if (lane == 0) P.defer[k * nw + gw] = dm;
             if (k < 64) had |= 1ull << k;
         }
         if (k < 3) DK_STAMP(4 + 3 * k);
+        DK_ACC_SPLIT(2);
+        DK_ACC_CHUNK();
         // rotate the pipeline
         have = have1;
         c = c1;
@@ -1695,6 +1727,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
+    DK_ACC_BEGIN();
     if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
         uint32_t cd, limd;
@@ -1715,12 +1748,16 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
             count_chunk(P, mine, lane, v, fid, lds_flows, s_flow, s_vh);
         }
     }
+    DK_ACC_SPLIT(3);
     combine_pending_tail(P, lane, kSmallWaves);  // a previous launch's deferred counter rows, in this wave's tail
+    DK_ACC_SPLIT(4);
     DK_STAMP(14);
     __syncthreads();
     flush_counters(P, tid, kSmallBlock, lds_flows, s_flow, s_vh);
     DK_STAMP(15);
     DK_STAMP_RT(13);
+    DK_ACC_SPLIT(5);
+    DK_ACC_WRITE(kSmallWaves);
 }
 
 // A wave's chunks with their descriptors loaded one chunk ahead: D.off / D.len belong to chunk D.c (0 outside the

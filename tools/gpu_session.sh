@@ -16,10 +16,13 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# r06y: evidence at the final tree (classify() decides no-data segments past RCV.NXT): the GPU suite, smoke(), the
-# default bench line, the round's rocprofv3 kernel stats + FETCH/WRITE passes
+# s1 (round 6): GPU suite at the env-free tuning; C3 / IMIX fixed-vs-per-frame sweeps and phase totals; C3 at 8
+# waves/SIMD (2 chunks per wave) as an A/B
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 1100 bash tools/profile_bench.sh r06y
+step c3_sweep 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M,8M --rotate 8 --tag base
+step c3_sweep_w8 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M,8M --rotate 8 --tag w8 --lib build/variants/w8.so
+step c3_sweep_w8b16 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M,8M --rotate 8 --tag w8b16 --lib build/variants/w8b16.so
+step c3_stamps 300 python tools/stamps.py build/variants/stamps.so --workload c3_udp64
+step imix_sweep 500 python tools/sweep.py --workload c4_imix --frames 512K,1M,2M,4M --rotate 2 --tag base
+step imix_stamps 300 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2
 echo done

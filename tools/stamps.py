@@ -83,6 +83,10 @@ def timeline(args, e, lib, rot, r, nw):
             sub = [s[:, 2 + 3 * k], s[:, b], s[:, b + 1], s[:, b + 2], s[:, b + 3]]
             row[f"c{k}"]["sub"] = {nm: q(us(sub[j + 1] - sub[j]))[2] for j, nm in
                                    enumerate(("bigframes+parse", "probe_issue+segsum", "verdict+demux", "results"))}
+        from stamps_staged import phase_totals
+
+        row["totals"] = phase_totals(st, us, ("window", "parse+table+stores", "count", "general_pass", "combine",
+                                              "barrier+rows"))
         print(json.dumps(row))
 
 

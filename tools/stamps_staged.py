@@ -70,11 +70,26 @@ def main():
                             "stream": q(us(s[:, 3 + 3 * k] - s[:, 2 + 3 * k])),
                             "phaseC": q(us(s[:, 4 + 3 * k] - s[:, 3 + 3 * k])),
                             "end_since_entry": q(us(s[:, 4 + 3 * k] - s[:, 0]))}
+        row["totals"] = phase_totals(st, us, ("to_stream_end", "phaseC", "stage+flush", "count", "last_flush",
+                                              "combine"))
         row["loop_end_to_flush"] = q(us(st[:, 14] - st[:, 11]))
         row["barrier+rows"] = q(us(st[:, 15] - st[:, 14]))
         row["entry_to_exit"] = q(us(st[:, 15] - st[:, 0]))
         print(json.dumps(row), flush=True)
     lib.dk_diag_path_stats_enable(e._ctx, 0)
+
+
+def phase_totals(st, us, names):
+    """Per-wave totals over every chunk (rx_diag.h DK_ACC_*: slots 20.., chunk count in 26): the median wave's µs per
+    phase, the same summed over the waves as a share of their summed entry-to-exit time, and per chunk."""
+    n = st[:, 26]
+    life = (st[:, 15] - st[:, 0]).astype(float)
+    out = {"chunks_per_wave": [int(n.min()), round(float(n.mean()), 2), int(n.max())]}
+    for j, nm in enumerate(names):
+        a = st[:, 20 + j].astype(float)
+        out[nm] = {"median_us": round(float(np.median(us(a))), 2), "share": round(float(a.sum() / life.sum()), 3),
+                   "us_per_chunk": round(float(us(a).sum() / max(n.sum(), 1)), 3)}
+    return out
 
 
 if __name__ == "__main__":
