@@ -430,31 +430,45 @@ def rx_kernel_name(frame_bytes, n):
 
 
 def tx_rate(eng, batch, frame_bytes, stream, iters=20):
-    """dk_tx_checksum kernel time over an HBM-resident batch: frame bytes read, 2 checksum fields written per frame."""
+    """TX checksums over an HBM-resident batch in both contracts: dk_tx_checksum (frame bytes read, the two fields
+    patched in place) and dk_tx_checksum_fields (the same read pass, the pair returned as 4 bytes per frame)."""
     import torch
 
-    for _ in range(3):
-        eng.tx_checksum(batch, stream=stream)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(iters):
-        eng.tx_checksum(batch, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / 1e3 / iters
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(iters):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / iters
+
+    t = timed(lambda: eng.tx_checksum(batch, stream=stream))
+    fields = torch.empty(batch.n, dtype=torch.int32, device=batch.off.device)
+    tf = timed(lambda: eng.tx_checksum_fields(batch, fields, stream=stream))
     # Bytes per frame: the frame read + its descriptor + the write. The fields themselves are 4 bytes (IPv4 + L4
     # checksum), but an in-place patch cannot reach HBM as less than one 64-byte write (the DRAM burst; WRITE_SIZE
-    # counts exactly 64 B per frame, profiles/pmc_traffic.json): that physical write floor is what the roofline
-    # counts; the 4-byte figure is kept beside it.
+    # counts exactly 64 B per frame, profiles/pmc_traffic.json): that physical write floor is what the in-place
+    # roofline counts; the 4-byte figure is kept beside it. The fields form writes exactly the 4 bytes.
     algo = frame_bytes + batch.n * (DESC_BYTES + 64)
     algo_fields = frame_bytes + batch.n * (DESC_BYTES + 4)
+    big = frame_bytes // max(batch.n, 1) >= 1024
     return {"gbps": round(frame_bytes / t / 1e9, 1), "kernel_ms_avg": round(t * 1e3, 4),
             "roofline_achieved_gbps": round(algo / t / 1e9, 1), "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_launch": algo,
             "bytes_counted": "frame + 6 B descriptor + 64 B written per frame (the physical write floor of an in-place "
                              "patch; the fields are 4 B)",
             "roofline_frac_field_bytes": round(algo_fields / t / 1e9 / HBM_PEAK_GBS, 4),
-            "kernel": "dk_tx_split_kernel" if frame_bytes // max(batch.n, 1) >= 1024 else "dk_tx_kernel"}
+            "kernel": "dk_tx_split_kernel" if big else "dk_tx_kernel",
+            "fields_form": {"entry": "dk_tx_checksum_fields", "gbps": round(frame_bytes / tf / 1e9, 1),
+                            "kernel_ms_avg": round(tf * 1e3, 4),
+                            "roofline_achieved_gbps": round(algo_fields / tf / 1e9, 1),
+                            "roofline_frac": round(algo_fields / tf / 1e9 / HBM_PEAK_GBS, 4),
+                            "algorithmic_bytes_per_launch": algo_fields,
+                            "bytes_counted": "frame + 6 B descriptor + 4 B of checksum pair written per frame",
+                            "kernel": "dk_tx_split_kernel<fields>" if big else "dk_tx_kernel<fields>"}}
 
 
 def read_ceiling(batch, stream, iters=10):

@@ -15,6 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libdk_rx.so")  # tuning builds (tools/variants.sh) are passed as lib_path explicitly
 
 DK_FLOW_NONE = 0xFFFFFFFF
+DK_TX_NOT_WRITTEN = 0xFFFF  # dk_tx_checksum_fields: a checksum half the in-place fill leaves untouched
 DK_RX_BATCH_ALIGNED16 = 1  # dk_rx_batch.flags
 DK_RX_BATCH_DEFER_COUNTS = 2
 DK_RX_MAX_DEFERRED_FLOWS = 32768  # flow_counts defer only for tables up to this size (dk_rx.h)
@@ -88,6 +89,7 @@ FUNCTIONS = [
     ("dk_rx_flow_counts_allreduce_to", c_int, [c_void_p, POINTER(DkRxResults), c_void_p, c_void_p, c_void_p,
                                                c_void_p]),
     ("dk_tx_checksum", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
+    ("dk_tx_checksum_fields", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
     ("dk_rx_verdict_name", c_char_p, [c_int]),
     ("dk_rx_verdict_errno", c_int, [c_int]),
     ("dk_rx_abi_version", c_uint32, []),
@@ -181,6 +183,7 @@ COMM_FUNCTIONS = [
 
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
+    ("dk_diag_rw_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p]),
     ("dk_diag_path_stats_enable", c_int, [c_void_p, c_int]),
     ("dk_diag_path_stats_read", c_int, [c_void_p, c_void_p]),
     ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p, c_uint32]),

@@ -176,7 +176,46 @@ __global__ __launch_bounds__(kBlock) void read_probe_small(const uint4* __restri
     if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
 }
 
+// The read/write mix of the small-frame kernel without the rest of it: grid-strided 4 KiB wave steps read
+// lane-contiguously (4 x 1 KiB buffer loads, nt), each followed by `nres` u32 stores per lane (nt) into nres arrays of
+// bytes / 64 entries (one u32 per 64-byte slot, as the result record's arrays are written per 64-frame chunk).
+__global__ __launch_bounds__(kBlock) void rw_probe(const uint4* __restrict__ p, uint64_t n16, uint32_t* __restrict__ dst,
+                                                   uint32_t nres, uint32_t* out) {
+    uint32_t acc = 0;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nslots = n16 / 4;  // 64-byte slots: entries per result array
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0xFFFFFFFF, 0x00020000);
+    for (uint64_t base = w * 256; base < n16; base += nwaves * 256) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t i = min(base + 64 * k + lane, n16 - 1);
+            const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 2);
+            v[k] = make_uint4(r[0], r[1], r[2], r[3]);
+        }
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) x ^= v[k].x + v[k].y + v[k].z + v[k].w;
+        acc += x;
+        const uint64_t slot = base / 4 + lane;
+        if (slot < nslots)
+            for (uint32_t a = 0; a < nres; a++) __builtin_nontemporal_store(x + a, dst + a * nslots + slot);
+    }
+    acc = __reduce_add_sync(~0ull, acc);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
+}
+
 }  // namespace
+
+extern "C" int dk_diag_rw_probe(const void* buf, uint64_t bytes, uint32_t* dst, uint32_t nres, uint32_t* scratch,
+                                uint32_t grid, void* stream) {
+    if (!buf || !scratch || grid == 0 || (nres && !dst) || bytes > 0xFFFFFFFFull) return 22;
+    hipLaunchKernelGGL(rw_probe, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint4*)buf, bytes / 16, dst,
+                       nres, scratch);
+    return hipGetLastError() == hipSuccess ? 0 : 5;
+}
 
 extern "C" int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode,
                                   void* stream) {

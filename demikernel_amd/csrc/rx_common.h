@@ -189,6 +189,8 @@ struct TxParams {
     uint32_t n;
     uint32_t sched;  // as RxParams::sched
     uint32_t split;  // launch the split (stream waves / finish waves) kernel: one 512-thread workgroup per CU
+    uint32_t* fields;  // nullptr: fill in place (dk_tx_checksum); else dk_tx_checksum_fields' u32 per frame (frames
+                       // are only read)
 };
 
 }  // namespace dk

@@ -886,12 +886,13 @@ int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu) {
     return 0;
 }
 
-int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
-                   void* stream) {
+namespace {
+// dk_tx_checksum / dk_tx_checksum_fields: persistent grid on the current device, the receive kernel's schedule rule.
+int tx_launch(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
+              uint32_t* fields, void* stream) {
     if (n && (!frames || !off || !len)) return EINVAL;
     if (frames_bytes > DK_RX_MAX_BLOB) return EINVAL;
     if (n == 0) return 0;
-    // Persistent grid on the current device, same schedule rule as the receive kernel (launch_batch).
     static thread_local int dev_cached = -1;
     static thread_local uint32_t cus = 0, occ = 0;
     int dev = 0;
@@ -906,7 +907,7 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
     }
     // Large frames: the split kernel (stream waves + finish waves, one 512-thread workgroup per CU, sched 0).
     const bool big = frames_bytes / n >= 1024;
-    dk::TxParams p{frames, frames_bytes, off, len, n, big ? 1u : 0u, big ? 1u : 0u};
+    dk::TxParams p{frames, frames_bytes, off, len, n, big ? 1u : 0u, big ? 1u : 0u, fields};
     const TxTuning& T = tx_tuning();
     if (T.split >= 0) p.split = T.split ? 1u : 0u;
     uint32_t per_cu = p.split ? 1u : std::min<uint32_t>(occ, p.sched ? 3u : 4u);
@@ -914,6 +915,19 @@ int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, 
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     const uint32_t grid = std::min((n + 255) / 256, per_cu * cus);
     return dk_launch_tx(p, grid, stream);
+}
+}  // namespace
+
+int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
+                   void* stream) {
+    return tx_launch(frames, frames_bytes, off, len, n, nullptr, stream);
+}
+
+int dk_tx_checksum_fields(const uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
+                          uint32_t n, uint32_t* fields, void* stream) {
+    if (n && !fields) return EINVAL;
+    // the kernels only read the frames in this form (TxParams::fields set)
+    return tx_launch(const_cast<uint8_t*>(frames), frames_bytes, off, len, n, fields, stream);
 }
 
 const char* dk_rx_verdict_name(int v) {

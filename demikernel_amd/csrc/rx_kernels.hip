@@ -1093,6 +1093,9 @@ __device__ __forceinline__ void flow_add(const RxParams& P, bool lds_flows, uint
     else if (P.flow_mode == kFlowGlobal)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), (unsigned long long)cnt);
 }
+#ifndef DK_COUNT_MERGED
+#define DK_COUNT_MERGED 0  // 1: delivered verdicts counted by popcount, the other verdicts in the lanes' one flow add
+#endif
 __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32_t lane, uint32_t v, uint32_t fid,
                                             bool lds_flows, uint32_t* s_flow, uint32_t* s_vh) {
     const bool dl = live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP);
@@ -1104,6 +1107,21 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
         if (lane == leader) flow_add(P, lds_flows, s_flow, opaque_v(f0), opaque_v((uint32_t)__popcll(m)));
         todo &= ~m;
         if (__popcll(m) < kFlowAggMin) break;
+    }
+    if (DK_COUNT_MERGED && lds_flows) {
+        // One LDS add per lane for what is left: its flow (delivered, not aggregated above) or, for a frame that was
+        // not delivered, its verdict; the two delivered verdicts are counted by popcount (lane 0, <= 2 adds).
+        const bool vc = P.res.verdict_counts != nullptr;
+        if (vc) {
+            const uint64_t mt = __ballot(live && v == DK_V_OK_TCP), mu = __ballot(live && v == DK_V_OK_UDP);
+            if (lane == 0) {
+                if (mt) atomicAdd(&s_vh[opaque_v(DK_V_OK_TCP)], opaque_v((uint32_t)__popcll(mt)));
+                if (mu) atomicAdd(&s_vh[opaque_v(DK_V_OK_UDP)], opaque_v((uint32_t)__popcll(mu)));
+            }
+        }
+        const bool fl = (todo >> lane) & 1u;
+        if (fl || (vc && live && !dl)) atomicAdd(fl ? &s_flow[fid >> 1] : &s_vh[v], fl ? 1u << ((fid & 1u) * 16) : 1u);
+        return;
     }
     if ((todo >> lane) & 1u) flow_add(P, lds_flows, s_flow, fid, 1u);
     if (P.res.verdict_counts) {
@@ -1529,6 +1547,15 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
 #ifndef DK_SMALL_PRIO
 #define DK_SMALL_PRIO 1
 #endif
+#ifndef DK_SMALL_LATE_BARRIER
+#define DK_SMALL_LATE_BARRIER 0
+#endif
+// A workgroup barrier that orders LDS only (no wait for the wave's outstanding global loads and stores).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 template <bool kShift>
 __device__ __forceinline__ bool small_fast_eligible(const FrameDesc<kShift>& F, uint32_t len, const RegAcc& R) {
     const bool ihl5 = ((R.w[3] >> 16) & 0x0Fu) == 5u;
@@ -1653,7 +1680,11 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
     if (lds_flows)
         for (uint32_t k = tid; k < P.flow_words; k += kSmallBlock) s_flow[k] = 0;
     if (kUb) ub_load(P, tid, kSmallBlock);
-    __syncthreads();
+    // Without the LDS bind table the counters are the only shared LDS state: the barrier that orders their zeroing
+    // before any count can wait until the first chunk's counts (kLateBarrier), off the first window's path.
+    constexpr bool kLateBarrier = DK_SMALL_LATE_BARRIER && !kUb;
+    const bool have0 = have;
+    if (!kLateBarrier) __syncthreads();
     DK_STAMP(11);
     // The grid is one generation of waves and the chunks do not divide evenly: the waves with one chunk more than the
     // rest (the last round's) set the launch's length, so they issue first on their SIMD (s_setprio; round 4: C3
@@ -1706,6 +1737,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid);
         if (k < 3) DK_STAMP(3 + 3 * k);
         DK_ACC_SPLIT(1);
+        if (kLateBarrier && k == 0) lds_barrier();  // every wave of the workgroup arrives once (below if no chunk)
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
             if (lane == 0) P.defer[k * nw + gw] = dm;
@@ -1727,6 +1759,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
+    if (kLateBarrier && !have0) lds_barrier();
     DK_ACC_BEGIN();
     if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mask stores
@@ -2039,40 +2072,52 @@ __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
     *reinterpret_cast<uint16_t*>(p) = (uint16_t)bswap16(v);
 }
 
-// Byte path (misaligned frames, IHL != 5): lane per frame.
-__device__ __noinline__ void tx_slow(uint8_t* f, uint32_t len) {
-    if (len < 34) return;
+// The checksum pair of dk_tx_checksum_fields (dk_rx.h): IPv4 | L4 << 16, DK_TX_NOT_WRITTEN for a half not filled.
+constexpr uint32_t kTxNone = DK_TX_NOT_WRITTEN | (DK_TX_NOT_WRITTEN << 16);
+__device__ __forceinline__ uint32_t tx_pair(uint32_t ipc, bool l4, uint32_t c) {
+    return ipc | ((l4 ? c : DK_TX_NOT_WRITTEN) << 16);
+}
+
+// Byte path (misaligned frames, IHL != 5): lane per frame. Writes the fields in place unless kFields; returns the pair.
+template <bool kFields>
+__device__ __noinline__ uint32_t tx_slow(uint8_t* f, uint32_t len) {
+    if (len < 34) return kTxNone;
     const MemAcc M{f};
-    if (M.be16(12) != 0x0800u) return;
+    if (M.be16(12) != 0x0800u) return kTxNone;
     const uint32_t hs = (f[14] & 15u) * 4;
     const uint32_t tot = M.be16(16);
-    if (hs < 20 || 14 + tot > len || tot < hs) return;
+    if (hs < 20 || 14 + tot > len || tot < hs) return kTxNone;
     const uint32_t hsum = M.le16(14) + M.le16(16) + M.le16(18) + M.le16(20) + M.le16(22) + M.le16(26) + M.le16(28) +
                           M.le16(30) + M.le16(32);
     const uint32_t ipc = csum_from_residue(be_residue(hsum));
-    f[24] = (uint8_t)(ipc >> 8);
-    f[25] = (uint8_t)ipc;
+    if (!kFields) {
+        f[24] = (uint8_t)(ipc >> 8);
+        f[25] = (uint8_t)ipc;
+    }
     const uint32_t proto = f[23];
     const uint32_t S = 14 + hs, E = 14 + tot, seg = tot - hs;
     uint32_t cs_at;
     if (proto == 6u) {
-        if (seg < 20) return;
+        if (seg < 20) return tx_pair(ipc, false, 0);
         const uint32_t doff = (f[S + 12] >> 4) * 4u;
-        if (doff < 20 || doff > seg) return;
+        if (doff < 20 || doff > seg) return tx_pair(ipc, false, 0);
         cs_at = S + 16;
     } else if (proto == 17u) {
-        if (seg < 8) return;
+        if (seg < 8) return tx_pair(ipc, false, 0);
         cs_at = S + 6;
     } else {
-        return;
+        return tx_pair(ipc, false, 0);
     }
     const uint32_t s = M.sum_le16(S, E) - M.le16(cs_at);  // the field is summed as zero
     const uint32_t src = M.u32(26), dst = M.u32(30);
     const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) + bswap16(dst >> 16) +
                             proto + seg;
     const uint32_t c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
-    f[cs_at] = (uint8_t)(c >> 8);
-    f[cs_at + 1] = (uint8_t)c;
+    if (!kFields) {
+        f[cs_at] = (uint8_t)(c >> 8);
+        f[cs_at + 1] = (uint8_t)c;
+    }
+    return tx_pair(ipc, true, c);
 }
 
 // A frame's rewritten 64-byte header window, held in registers by the split TX kernel's finish waves until a burst.
@@ -2082,20 +2127,28 @@ struct TxWin {
     uint32_t off;  // frame offset in the blob; kNoWin: nothing staged
 };
 // Checksum computation and field writes of one lane's frame from what the streaming left in C and W. kStage: the
-// full-window rewrite is handed back in win instead of stored (other writes are stored at once).
-template <bool kStage>
+// full-window rewrite is handed back in win instead of stored (other writes are stored at once). kFields
+// (dk_tx_checksum_fields): nothing is written to the frame; frame i's checksum pair goes to P.fields[i].
+template <bool kStage, bool kFields = false>
 __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, const WaveLds& W, uint32_t off,
-                                          uint32_t len, const Chunk& C, TxWin& win) {
+                                          uint32_t len, const Chunk& C, TxWin& win, uint32_t i = 0, bool live = false) {
     win.off = kNoWin;
-    if (!C.inb) return;
+    if (!C.inb) {
+        if (kFields && live) __builtin_nontemporal_store(kTxNone, P.fields + i);
+        return;
+    }
     uint8_t* f = P.frames + off;
     const RegAcc& R = C.R;
     if (!(C.vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u)) {
-        tx_slow(f, len);
+        const uint32_t pr = tx_slow<kFields>(f, len);
+        if (kFields) __builtin_nontemporal_store(pr, P.fields + i);
         return;
     }
     const uint32_t tot = R.be16(16);
-    if (R.be16(12) != 0x0800u || 14 + tot > len || tot < 20) return;
+    if (R.be16(12) != 0x0800u || 14 + tot > len || tot < 20) {
+        if (kFields) __builtin_nontemporal_store(kTxNone, P.fields + i);
+        return;
+    }
     const uint32_t hsum = R.le16(14) + R.le16(16) + R.le16(18) + R.le16(20) + R.le16(22) + R.le16(26) + R.le16(28) +
                           R.le16(30) + R.le16(32);
     const uint32_t ipc = csum_from_residue(be_residue(hsum));
@@ -2111,6 +2164,10 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
         const uint32_t pseudo = bswap16(src & 0xFFFFu) + bswap16(src >> 16) + bswap16(dst & 0xFFFFu) +
                                 bswap16(dst >> 16) + proto + seg;
         c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
+    }
+    if (kFields) {
+        __builtin_nontemporal_store(tx_pair(ipc, l4, c), P.fields + i);
+        return;
     }
     if (len >= 64 && C.sh == 0) {  // rewrite the whole 64-byte header window: full-line writes, no partial-write merge below L2
         uint32_t d[16];
@@ -2134,12 +2191,13 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
     if (l4) store_be16(f + (tcp ? 50 : 40), c);
 }
 
+template <bool kFields>
 __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t lane, WaveLds& W, uint32_t off,
-                                        uint32_t len) {
+                                        uint32_t len, uint32_t i) {
     Chunk C;
     stream_chunk<true, true>(P.frames, P.frames_bytes, live, lane, W, off, len, C);
     TxWin win;
-    tx_finish<false>(P, lane, W, off, len, C, win);
+    tx_finish<false, kFields>(P, lane, W, off, len, C, win, i, live);
 }
 
 
@@ -2147,6 +2205,7 @@ __device__ __forceinline__ void tx_tile(const TxParams& P, bool live, uint32_t l
 // of their chunks into 3 LDS buffers each, finish waves 4..7 compute the checksums and rewrite the header windows, with
 // ready / free words instead of a per-period workgroup barrier; the streaming waves never wait on the checksum
 // arithmetic or the writes.
+template <bool kFields>
 __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P) {
     constexpr int kBufs = SplitShape<1>::kBufs;
     __shared__ WaveLds s_buf[kBufs][kWaves];  // [chunk % kBufs][stream wave]
@@ -2181,7 +2240,8 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
         for (uint32_t p = 0; D.have; p++) {
             const uint32_t b = p % kBufs;
             WaveLds& W = s_buf[b][sw];
-            const bool live = D.c + r.lane_off < D.lim;
+            const uint32_t i = D.c + r.lane_off;
+            const bool live = i < D.lim;
             const uint32_t off = D.off, len = D.len;
             D.next(P, r, p + 1);
             const FrameDesc<true> F(P.frames, P.frames_bytes, live, off, len);
@@ -2191,7 +2251,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
             const CoopPlan pl{(uint32_t)__popcll(__ballot(F.big)), 0, 1};
             coop_gather(F, pl, lane, W, C);
             TxWin win;
-            tx_finish<false>(P, lane, W, off, len, C, win);
+            tx_finish<false, kFields>(P, lane, W, off, len, C, win, i, live);
             asm volatile("" ::"v"(D.off), "v"(D.len));  // the next descriptors waited for before this chunk's writes
             if (lane == 0) lds_publish(&s_free[sw][b], p + 1);  // after this wave's last read of W (release)
         }
@@ -2199,6 +2259,7 @@ __global__ __launch_bounds__(kSplitBlock, 1) void dk_tx_split_kernel(TxParams P)
 }
 
 // Persistent, same schedule as dk_rx_kernel.
+template <bool kFields>
 __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P) {
     __shared__ WaveLds s_wave[kWaves];
     const uint32_t lane = lane_id();
@@ -2219,7 +2280,7 @@ __global__ __launch_bounds__(kBlock, DK_MIN_WAVES) void dk_tx_kernel(TxParams P)
             noff = P.off[nc + r.lane_off];
             nlen = P.len[nc + r.lane_off];
         }
-        tx_tile(P, i < lim, lane, s_wave[wv], off, len);
+        tx_tile<kFields>(P, i < lim, lane, s_wave[wv], off, len, i);
     }
 }
 
@@ -2308,15 +2369,21 @@ int dk_launch_reduce(const dk::RowCombine& q, void* stream) {
 
 int dk_tx_resident_blocks() {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_tx_kernel, dk::kBlock, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_tx_kernel<false>, dk::kBlock, 0) != hipSuccess)
+        return 0;
     return blocks;
 }
 
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
-    if (p.split)
-        hipLaunchKernelGGL(dk::dk_tx_split_kernel, dim3(grid), dim3(dk::kSplitBlock), 0, (hipStream_t)stream, p);
+    const hipStream_t s = (hipStream_t)stream;
+    if (p.split && p.fields)
+        hipLaunchKernelGGL(dk::dk_tx_split_kernel<true>, dim3(grid), dim3(dk::kSplitBlock), 0, s, p);
+    else if (p.split)
+        hipLaunchKernelGGL(dk::dk_tx_split_kernel<false>, dim3(grid), dim3(dk::kSplitBlock), 0, s, p);
+    else if (p.fields)
+        hipLaunchKernelGGL(dk::dk_tx_kernel<true>, dim3(grid), dim3(dk::kBlock), 0, s, p);
     else
-        hipLaunchKernelGGL(dk::dk_tx_kernel, dim3(grid), dim3(dk::kBlock), 0, (hipStream_t)stream, p);
+        hipLaunchKernelGGL(dk::dk_tx_kernel<false>, dim3(grid), dim3(dk::kBlock), 0, s, p);
     return hipGetLastError() == hipSuccess ? 0 : 5;
 }

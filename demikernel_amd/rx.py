@@ -353,6 +353,21 @@ class RxEngine:
                                        batch.n, ctypes.c_void_p(s.cuda_stream)), "dk_tx_checksum")
 
 
+    def tx_checksum_fields(self, batch: FrameBatch, fields=None, stream=None):
+        """dk_tx_checksum_fields: the same checksums returned, not written — an int32 device tensor of n entries, each
+        ipv4 | l4 << 16 (as u32; N.DK_TX_NOT_WRITTEN for a half the in-place fill leaves untouched). The frames are
+        only read."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if fields is None:
+            fields = torch.empty(max(batch.n, 1), dtype=torch.int32, device=batch.off.device)
+        _check(self.lib.dk_tx_checksum_fields(_ptr(batch.blob), batch.frames_bytes, _ptr(batch.off), _ptr(batch.len),
+                                              batch.n, _ptr(fields), ctypes.c_void_p(s.cuda_stream)),
+               "dk_tx_checksum_fields")
+        return fields
+
+
 def tx_tuning(split: int = -1, sched: int = -1, grid_per_cu: int = -1) -> None:
     """Diagnostics (dk_diag.h): TX kernel overrides for the process (-1 = the engine's rule)."""
     _check(N.load_library().dk_diag_tx_set_tuning(split, sched, grid_per_cu), "dk_diag_tx_set_tuning")

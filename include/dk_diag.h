@@ -19,6 +19,12 @@ extern "C" {
  * Returns 0, EINVAL or EIO. */
 int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint32_t grid, int mode, void* stream);
 
+/* The small-frame receive kernel's read/write mix alone: `bytes` (< 4 GiB, multiple of 64) read lane-contiguously in
+ * 4 KiB wave steps, each step followed by nres u32 stores per lane into dst = nres arrays of bytes / 64 u32 (one per
+ * 64-byte slot, as the result arrays are written); nres 0 reads only. The ceiling C3 is compared with. Async. */
+int dk_diag_rw_probe(const void* buf, uint64_t bytes, uint32_t* dst, uint32_t nres, uint32_t* scratch, uint32_t grid,
+                     void* stream);
+
 /* Per-path frame counters of a receive context (off by default). Paths: [0] vector path, frame <= 64 B in registers;
  * [1] vector path, frame streamed by a quarter-wave; [2] streamed but the L4 segment re-summed in-lane (IPv4
  * total_length far below the frame length); [3] per-lane byte-load path (unaligned frame, IHL != 5, or a frame too

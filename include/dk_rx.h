@@ -288,6 +288,16 @@ int dk_rx_flow_counts_allreduce_to(dk_rx_ctx* ctx, const dk_rx_results* res, uin
 int dk_tx_checksum(uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len, uint32_t n,
                    void* stream);
 
+/* The same checksums returned instead of written (for a host that builds the headers itself, as serialize_and_attach
+ * does, and patches two u16s per frame): the frames are only read, and fields[i] (u32, device memory) =
+ * ipv4 | l4 << 16, each half the value dk_tx_checksum would store big-endian at frame bytes 24..25 (IPv4 header
+ * checksum) and at the TCP (S + 16) / UDP (S + 6) checksum, S = 14 + IHL * 4; DK_TX_NOT_WRITTEN (0xFFFF, never a
+ * computed checksum: the fold maps a zero residue to 0) for a half the in-place fill leaves untouched. 4 bytes written per
+ * frame instead of a 64-byte header line. Device pointers, async. */
+#define DK_TX_NOT_WRITTEN 0xFFFFu
+int dk_tx_checksum_fields(const uint8_t* frames, uint64_t frames_bytes, const uint32_t* off, const uint16_t* len,
+                          uint32_t n, uint32_t* fields, void* stream);
+
 /* Introspection. */
 const char* dk_rx_verdict_name(int verdict);
 int dk_rx_verdict_errno(int verdict); /* errno the reference returns for this verdict; 0 for deliver/divert/drop */

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <unordered_map>
 #include <vector>
+#include <vector>
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -683,13 +684,13 @@ uint16_t dko_generic_checksum(const uint8_t* buf, size_t len, int has_start, uin
 
 // serialize_and_attach restatement (TX, offload off): fill the IPv4 header checksum and the TCP/UDP checksum of a full
 // Ethernet frame in place, using the frame's own src/dst (ipv4/header.rs:229-266, tcp/header.rs:397-404,
-// udp/header.rs:97-130). Returns 0, or -1 if the frame is not Eth/IPv4/{TCP,UDP} with a consistent length.
-int dko_tx_fill_checksums(uint8_t* f, size_t len) {
-    if (len < 34 || be16(f + 12) != IPV4) return -1;
+// udp/header.rs:97-130). Returns bit 0 = the IPv4 checksum was written, bit 1 = the L4 checksum was written (at *l4_at).
+static int tx_fill(uint8_t* f, size_t len, size_t* l4_at) {
+    if (len < 34 || be16(f + 12) != IPV4) return 0;
     uint8_t* ip = f + 14;
     size_t ihl = (size_t)(ip[0] & 0xF) * 4;
     size_t tot = be16(ip + 2);
-    if (ihl < 20 || 14 + tot > len || tot < ihl) return -1;
+    if (ihl < 20 || 14 + tot > len || tot < ihl) return 0;
     ip[10] = ip[11] = 0;
     uint16_t c = ipv4_compute_checksum(ip, ihl);
     ip[10] = (uint8_t)(c >> 8); ip[11] = (uint8_t)c;
@@ -697,22 +698,41 @@ int dko_tx_fill_checksums(uint8_t* f, size_t len) {
     uint8_t* l4 = ip + ihl;
     size_t seg = tot - ihl;
     if (ip[9] == 0x06) {
-        if (seg < 20) return -1;
+        if (seg < 20) return 1;
         size_t doff = (size_t)(l4[12] >> 4) * 4;
-        if (doff < 20 || doff > seg) return -1;
+        if (doff < 20 || doff > seg) return 1;
         l4[16] = l4[17] = 0;
         c = tcp_checksum(src, dst, l4, doff, l4 + doff, seg - doff);
         l4[16] = (uint8_t)(c >> 8); l4[17] = (uint8_t)c;
-        return 0;
+        *l4_at = 14 + ihl + 16;
+        return 3;
     }
     if (ip[9] == 0x11) {
-        if (seg < 8) return -1;
+        if (seg < 8) return 1;
         l4[6] = l4[7] = 0;
         c = udp_checksum(src, dst, l4, l4 + 8, seg - 8);
         l4[6] = (uint8_t)(c >> 8); l4[7] = (uint8_t)c;
-        return 0;
+        *l4_at = 14 + ihl + 6;
+        return 3;
     }
-    return -1;
+    return 1;
+}
+
+// Returns 0, or -1 if the frame is not Eth/IPv4/{TCP,UDP} with a consistent length.
+int dko_tx_fill_checksums(uint8_t* f, size_t len) {
+    size_t at = 0;
+    return tx_fill(f, len, &at) == 3 ? 0 : -1;
+}
+
+// The same checksums as dk_tx_checksum_fields reports them (include/dk_rx.h): ipv4 | l4 << 16, 0xFFFF for a field the
+// in-place fill leaves untouched; the frame itself is not modified.
+uint32_t dko_tx_checksum_fields(const uint8_t* f, size_t len) {
+    std::vector<uint8_t> g(f, f + len);
+    size_t at = 0;
+    const int m = tx_fill(g.data(), len, &at);
+    const uint32_t ip = (m & 1) ? be16(g.data() + 24) : 0xFFFFu;
+    const uint32_t l4 = (m & 2) ? be16(g.data() + at) : 0xFFFFu;
+    return ip | l4 << 16;
 }
 
 }  // extern "C"

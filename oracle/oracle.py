@@ -64,6 +64,8 @@ def lib() -> ctypes.CDLL:
         L.dko_generic_checksum.argtypes = [vp, c_size_t, c_int, c_uint32]
         L.dko_tx_fill_checksums.restype = c_int
         L.dko_tx_fill_checksums.argtypes = [vp, c_size_t]
+        L.dko_tx_checksum_fields.restype = ctypes.c_uint32
+        L.dko_tx_checksum_fields.argtypes = [vp, c_size_t]
         L.dko_tcp_process.restype = c_int
         L.dko_tcp_process.argtypes = [vp, c_uint32, c_uint32] + [vp] * 10
         _lib = L
@@ -198,6 +200,12 @@ def generic_checksum(buf: bytes, start: int | None = None) -> int:
 def tx_fill_checksums(frame: bytearray) -> int:
     a = np.frombuffer(frame, np.uint8)
     return lib().dko_tx_fill_checksums(a.ctypes.data, len(frame))
+
+
+def tx_checksum_fields(frame: bytes) -> int:
+    """dk_tx_checksum_fields' u32 for one frame: ipv4 | l4 << 16 (0xFFFF: not filled)."""
+    a = np.frombuffer(bytes(frame), np.uint8)
+    return lib().dko_tx_checksum_fields(a.ctypes.data, len(frame))
 
 
 # include/dk_tcp.h mirrors (tests/test_tcp_oracle.py checks them against demikernel_amd._native)

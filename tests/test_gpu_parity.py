@@ -459,7 +459,8 @@ def test_udp_bind_table_fit(torch_cuda, capfd, nbinds, want):
 
 
 def tx_check(blob, off, lens, ctx=""):
-    """dk_tx_checksum on the GPU vs the oracle's serialize_and_attach restatement, frame by frame, whole blob."""
+    """dk_tx_checksum on the GPU vs the oracle's serialize_and_attach restatement, frame by frame, whole blob; then
+    dk_tx_checksum_fields on the same frames vs the oracle's pairs."""
     import torch
 
     from oracle import oracle as O
@@ -484,6 +485,17 @@ def tx_check(blob, off, lens, ctx=""):
         exp[o:o + L] = np.frombuffer(bytes(fr), np.uint8)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, f"{ctx}: {bad.size} bytes differ, first at blob offset {bad[:8]}"
+    # the fields form (dk_tx_checksum_fields) on the same scrambled frames: the frames only read, each frame's u32
+    # the oracle's pair (0xFFFF halves where the in-place fill writes nothing)
+    b2 = FrameBatch.from_numpy(blob, off, lens)
+    fields = eng.tx_checksum_fields(b2)
+    torch.cuda.synchronize()
+    assert np.array_equal(b2.blob.cpu().numpy(), blob), f"{ctx}: dk_tx_checksum_fields wrote to the frames"
+    gf = fields.cpu().numpy().view(np.uint32)[: len(off)]
+    ef = np.array([O.tx_checksum_fields(blob[o:o + L].tobytes()) for o, L in zip(off, lens)], np.uint32)
+    badf = np.nonzero(gf != ef)[0]
+    assert badf.size == 0, f"{ctx}: fields differ at frames {badf[:8]}: got {gf[badf[:4]]} exp {ef[badf[:4]]}"
+    assert ((ef & 0xFFFF) != 0xFFFF).any() and ((ef >> 16) != 0xFFFF).any(), ctx
 
 
 @pytest.fixture

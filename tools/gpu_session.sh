@@ -16,13 +16,14 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
 }
 export TMPDIR=/tmp
 
-# s1 (round 6): GPU suite at the env-free tuning; C3 / IMIX fixed-vs-per-frame sweeps and phase totals; C3 at 8
-# waves/SIMD (2 chunks per wave) as an A/B
+# s2: GPU suite (TX fields form); the C3 read/write-mix ceiling; C3 sweep at sizes near the bench's and a
+# no-counters ablation; interleaved A/B of merged counting and the late barrier on C3, IMIX, C2
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step c3_sweep 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M,8M --rotate 8 --tag base
-step c3_sweep_w8 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M,8M --rotate 8 --tag w8 --lib build/variants/w8.so
-step c3_sweep_w8b16 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M,8M --rotate 8 --tag w8b16 --lib build/variants/w8b16.so
-step c3_stamps 300 python tools/stamps.py build/variants/stamps.so --workload c3_udp64
-step imix_sweep 500 python tools/sweep.py --workload c4_imix --frames 512K,1M,2M,4M --rotate 2 --tag base
-step imix_stamps 300 python tools/stamps_staged.py build/variants/stamps.so --workload c4_imix --rotate 2
+step rw_probe 200 python tools/rw_probe.py
+step c3_sweep 400 python tools/sweep.py --workload c3_udp64 --frames 1M,1536K,2M,3M,4M --rotate 8 --tag base
+step c3_sweep_nocnt 400 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M --rotate 8 --tag nocounts --no-counts
+step c3_ab 400 python tools/abtest.py --workload c3_udp64 --grids 0 --rotate 8 --defer --reps 9 --iters 20 build/variants/base.so build/variants/cnt2.so build/variants/lateb.so build/variants/both.so
+step imix_ab 400 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 7 --iters 10 build/variants/base.so build/variants/cnt2.so
+step c2_ab 400 python tools/abtest.py --workload c2_tcp1500 --grids 0 --defer --reps 7 --iters 10 build/variants/base.so build/variants/cnt2.so
+step imix_sweep 400 python tools/sweep.py --workload c4_imix --frames 256K,512K,1M,1536K,2M --rotate 2 --tag base
 echo done

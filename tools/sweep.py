@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--lib", default=None)
     ap.add_argument("--tuning", default="", help="dk_diag_rx_set_tuning knobs, e.g. grid_per_cu=2,tail=0")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--no-counts", action="store_true", help="no flow / verdict counters (cost attribution)")
     args = ap.parse_args()
     import torch
 
@@ -57,7 +58,7 @@ def main():
         tr = made[0][2]
         fb = int(tr.frame_len.astype(np.int64).sum())
         algo = fb + n * (bench.DESC_BYTES + bench.RESULT_BYTES)
-        res = eng.results(n)
+        res = eng.results(n, counts=not args.no_counts)
         runs.append({"n": n, "eng": eng, "batches": batches, "res": res, "algo": algo, "fb": fb, "t": []})
     bench.preheat(runs[0]["eng"], runs[0]["batches"][0], stream, 0.3)
     for rep in range(args.reps):
@@ -81,7 +82,8 @@ def main():
         print(json.dumps({"tag": args.tag, "workload": args.workload, "frames": R["n"], "rotate": args.rotate,
                           "us_per_launch": round(us, 3), "us_spread": [round(min(R["t"]), 3), round(max(R["t"]), 3)],
                           "algo_bytes": R["algo"], "algo_TBps": round(R["algo"] / us / 1e6, 3),
-                          "frac": round(R["algo"] / us / 1e6 / 8.0, 4), "tuning": knobs}), flush=True)
+                          "frac": round(R["algo"] / us / 1e6 / 8.0, 4), "tuning": knobs,
+                          "counts": not args.no_counts}), flush=True)
     A = np.vstack([np.ones(len(xs)), np.asarray(xs, float)]).T
     (a, b), *_ = np.linalg.lstsq(A, np.asarray(ys), rcond=None)
     per_frame_bytes = runs[-1]["algo"] / runs[-1]["n"]
