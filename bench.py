@@ -386,6 +386,7 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0, bu
     conns = pristine.clone()
     out = TcpOut(nseg, len(table), dev.index or 0)
     times = []
+    walks = []
     with torch.cuda.stream(stream):
         for i in range(iters + 2):
             conns.copy_(pristine)
@@ -394,6 +395,7 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0, bu
             tcp.process(r, conns, out, stream=stream)
             e1.record(stream)
             torch.cuda.synchronize()
+            walks.append(tcp.last_walk)
             if i >= 2:
                 times.append(e0.elapsed_time(e1) / 1e3)
     got = out.to_numpy()
@@ -413,12 +415,13 @@ def tcp_rate(stream, nseg=1 << 20, nconns=1 << 14, iters=10, cpu_seconds=3.0, bu
             "delivered_frac": round(float(hist[1]) / nseg, 3),
             "actions": {name: int(c) for name, c in zip(TCP_ACTION_NAMES, hist) if c},
             "cpu_baseline": {"mseg_s": round(nseg / tc / 1e6, 2), "cores": 1, "kind": "port", "reps": reps},
-            "walk": os.environ.get("DK_TCP_WALK") or ("scan" if nseg >= 1024 * nconns and nconns <= 256 else
-                                                       "wave" if nseg >= 8 * nconns else "lane"),
+            "walk": walks[-1], "walk_first_call": walks[0],
             "pipeline": "key + onesweep radix sort (rocPRIM) + ranges + per-connection walk (lanes = connections, "
                         "store in LDS; one wave per connection with a parallel 64-segment check at >= 8 "
                         "segments per connection; at >= 1,024 and <= 256 connections the scan walk: windows "
-                        "precomputed across the chip, 64 windows per wave scan, decided windows written in parallel)"}
+                        "precomputed across the chip, 64 windows per wave scan, decided windows written in parallel — "
+                        "unless the context's last finished call stored >= 0.1 % of its segments out of order at >= 16 "
+                        "connections: then the wave walk)"}
 
 
 def rx_kernel_name(frame_bytes, n):

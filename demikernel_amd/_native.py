@@ -189,6 +189,7 @@ DIAG_FUNCTIONS = [
     ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p, c_uint32]),
     ("dk_diag_tx_set_tuning", c_int, [c_int32, c_int32, c_int32]),
     ("dk_diag_tcp_set_walk", c_int, [c_void_p, c_int32, c_int32]),
+    ("dk_diag_tcp_last_walk", c_int, [c_void_p]),
 ]
 DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table", "tail", "udp_table",
                     "host_zc"]

@@ -80,6 +80,9 @@ struct Params {
     uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
     uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
                           // fin_pending, fin_seq}, saved by the scan kernel for the post kernel
+    uint32_t* shape;      // device [2] {STORED segments, finished blocks} of this call (zero between calls)
+    uint32_t* shape_host; // host-mapped [3] {STORED, n, call number}: written by the fix kernel's last block
+    uint32_t call;
     dk_tcp_out out;
 };
 constexpr uint32_t kNoConn = 0xFFFFFFFFu;
@@ -126,12 +129,34 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_key_kernel(Params P) {
     }
 }
 
-// Classified segments after their connection's close are UNPROCESSED (the walks' queued-behind-the-close rule).
+// Classified segments after their connection's close are UNPROCESSED (the walks' queued-behind-the-close rule). The
+// same pass counts the call's STORED segments (the stream's shape: the walk choice of the context's next call, below)
+// and the last block to finish writes the count to the context's host-mapped word.
 __global__ __launch_bounds__(kBlock) void dk_tcp_fix_kernel(Params P) {
+    __shared__ uint32_t s_cnt[kBlock / 64];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= P.n) return;
-    const uint32_t c = P.cls[i];
-    if (c != kNoConn && i >= P.open_until[c]) P.out.action[i] = DK_TCP_UNPROCESSED;
+    bool stored = false;
+    if (i < P.n) {
+        const uint32_t c = P.cls[i];
+        if (c != kNoConn && i >= P.open_until[c]) P.out.action[i] = DK_TCP_UNPROCESSED;
+        else stored = c == kNoConn && P.out.action[i] == DK_TCP_STORED;
+    }
+    const uint64_t m = __ballot(stored);
+    if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x / 64] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+        for (uint32_t w = 0; w < kBlock / 64; w++) sum += s_cnt[w];
+        if (sum) atomicAdd(P.shape, sum);
+        __threadfence();
+        if (atomicAdd(P.shape + 1, 1u) == gridDim.x - 1) {  // the last block: every count is in
+            const uint32_t total = atomicExch(P.shape, 0u);
+            atomicExch(P.shape + 1, 0u);  // zero for the context's next call (ordered after it on the stream)
+            __hip_atomic_store(P.shape_host + 0, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(P.shape_host + 1, P.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(P.shape_host + 2, P.call, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void dk_tcp_range_kernel(Params P) {
@@ -1338,8 +1363,10 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_post_kernel(Params P) 
 }
 #undef DK_U
 
-// Which walk runs: `force` (dk_diag_tcp_set_walk: 0 lane, 1 wave, 2 relay, 3 scan, -1 the rule); otherwise one lane per connection below kWaveWalkMinSegs segments per connection, the
-// scan walk from kScanMinSegs (16 windows) for up to DK_TCP_SCAN_MAX_CONNS connections, else one wave per connection.
+// Which walk runs: `force` (dk_diag_tcp_set_walk: 0 lane, 1 wave, 2 relay, 3 scan, -1 the rule); otherwise one lane
+// per connection below kWaveWalkMinSegs segments per connection, the scan walk from kScanMinSegs (16 windows) for up
+// to DK_TCP_SCAN_MAX_CONNS connections — unless the context's last finished call showed a reordered stream (below) —,
+// else one wave per connection.
 // 1M segments (sessions r05zt-r05zv, profiles/r05_tcp_walks.jsonl): 1 connection scan 0.87 ms, relay 3.8, wave 12.7;
 // 16: scan 0.29, wave 0.94; 64: scan 0.22, relay 0.23, wave 0.31; 256: scan 0.19, wave 0.18; 1,024: wave 0.14, relay
 // 0.16, scan 0.18 (a wave per connection fills the chip). The relay walk stays selectable.
@@ -1354,13 +1381,26 @@ constexpr uint32_t kScanMinSegs = 16 * kWave;
 #define DK_TCP_DEEP_MAX_CONNS 2048
 #endif
 constexpr uint32_t kDeepAheadMaxConns = DK_TCP_DEEP_MAX_CONNS;
+// The stream's shape (the scan walk's weak spot): a window in which a segment goes to the out-of-order store is not
+// decided by the scan's thresholds and runs the state machine through the rings, as the wave walk does, after the
+// precompute the scan walk paid for it — so on reordered streams the wave walk is ahead (the bench's 1M-segment stream
+// with local reordering: 16 / 64 / 256 connections 0.60 / 0.39 / 0.22 ms against the scan walk's 0.63 / 0.42 / 0.25,
+// at 29 % / 6.6 % / 0.1 % of the segments STORED, i.e. 100 % / 99 % / 6 % of its 64-segment windows storing), while on
+// in-order streams (no segment stored) the scan walk is (1 / 16 / 64 / 256 connections 0.41 / 0.21 / 0.18 / 0.17
+// against 12.7 / 0.85 / 0.28 / 0.17 ms). STORED is the same in every walk (bit-exact outputs), so the count the fix
+// kernel takes is a walk-independent measure of the shape. Rule: from kShapeMinConns connections on, a context whose
+// last finished call stored at least 1 segment in kShapeStoredDen (0.1 %: ~6 % of the windows) takes the wave walk.
+// Below 16 connections one wave per connection is too little of the chip (1 connection: 12.7 ms) whatever the shape.
+constexpr uint32_t kShapeMinConns = 16, kShapeStoredDen = 1024;
 enum Walker { kLaneWalk = 0, kWaveWalk = 1, kRelayWalk = 2, kScanWalk = 3 };
-Walker pick_walk(uint32_t n, uint32_t nconns, int force) {
+Walker pick_walk(uint32_t n, uint32_t nconns, int force, bool reordered) {
     if (nconns > (1u << 24)) return kLaneWalk;  // grid of nconns workgroups
     if (force == 3 && nconns > 65535) return kRelayWalk;  // the scan walk's grids have one row per connection
     if (force >= 0 && force <= 3) return (Walker)force;
     if ((uint64_t)n < (uint64_t)kWaveWalkMinSegs * nconns) return kLaneWalk;
-    if ((uint64_t)n >= (uint64_t)kScanMinSegs * nconns && nconns <= DK_TCP_SCAN_MAX_CONNS) return kScanWalk;
+    if ((uint64_t)n >= (uint64_t)kScanMinSegs * nconns && nconns <= DK_TCP_SCAN_MAX_CONNS &&
+        !(reordered && nconns >= kShapeMinConns))
+        return kScanWalk;
     return kWaveWalk;
 }
 
@@ -1409,6 +1449,14 @@ struct dk_tcp_ctx {
     int* scan_ends = nullptr;
     uint32_t* scan_head = nullptr;
     size_t scan_sum_cap = 0, scan_post_cap = 0, scan_ends_cap = 0, scan_head_cap = 0;
+    // the stream's shape (pick_walk): the fix kernel's STORED count of each call, in host-mapped memory
+    uint32_t* shape = nullptr;            // device [2], zero between calls
+    volatile uint32_t* shape_host = nullptr;  // host-mapped [3] {STORED, n, call}
+    uint32_t* shape_host_dev = nullptr;   // its device alias
+    uint32_t calls = 0;                   // calls issued (the number the next fix kernel writes is calls + 1)
+    uint32_t seen = 0;                    // the last call whose count was read
+    bool reordered = false;               // the last read count: >= 1 in kShapeStoredDen segments STORED
+    int last_walk = -1;                   // the walk the last call ran (dk_diag_tcp_last_walk)
 };
 
 extern "C" {
@@ -1421,13 +1469,27 @@ int dk_tcp_ctx_create(int32_t device, dk_tcp_ctx** out) {
     dk_tcp::DeviceGuard g(device);
     dk_tcp_ctx* t = new dk_tcp_ctx();
     t->device = device;
+    void* hs = nullptr;
     if (hipEventCreateWithFlags(&t->last, hipEventDisableTiming) != hipSuccess) {
         delete t;
         return EINVAL;
     }
+    if (hipMalloc(&t->shape, 2 * sizeof(uint32_t)) != hipSuccess || hipMemset(t->shape, 0, 8) != hipSuccess ||
+        hipHostMalloc(&hs, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&t->shape_host_dev), hs, 0) != hipSuccess) {
+        if (hs) (void)hipHostFree(hs);
+        if (t->shape) (void)hipFree(t->shape);
+        (void)hipEventDestroy(t->last);
+        delete t;
+        return ENOMEM;
+    }
+    t->shape_host = static_cast<volatile uint32_t*>(hs);
+    t->shape_host[0] = t->shape_host[1] = t->shape_host[2] = 0;
     *out = t;
     return 0;
 }
+
+int dk_diag_tcp_last_walk(const dk_tcp_ctx* t) { return t ? t->last_walk : -1; }
 
 int dk_diag_tcp_set_walk(dk_tcp_ctx* t, int32_t walk, int32_t relay_waves) {
     if (!t || walk < -1 || walk > 3) return EINVAL;
@@ -1442,8 +1504,9 @@ void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     if (t->used) (void)hipEventSynchronize(t->last);
     for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp,
                     (void*)t->cls, (void*)t->open_until, (void*)t->scan_sum, (void*)t->scan_post, (void*)t->scan_ends,
-                    (void*)t->scan_head})
+                    (void*)t->scan_head, (void*)t->shape})
         if (p) (void)hipFree(p);
+    if (t->shape_host) (void)hipHostFree(const_cast<uint32_t*>(t->shape_host));
     (void)hipEventDestroy(t->last);
     delete t;
 }
@@ -1472,7 +1535,18 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
         (rc = grow(t->range, t->range_cap, 2 * (size_t)nconns + 1)) || (rc = grow(t->cls, t->cls_cap, n)) ||
         (rc = grow(t->open_until, t->open_cap, nconns)))
         return rc;
-    const dk_tcp::Walker walker = nconns ? dk_tcp::pick_walk(n, nconns, t->walk) : dk_tcp::kLaneWalk;
+    // The shape of the stream from the last call whose fix kernel has completed (never waited for: a call still in
+    // flight leaves the previous reading in place).
+    if (t->calls != t->seen && t->shape_host[2] != t->seen) {
+        const uint32_t call = t->shape_host[2];
+        const uint32_t stored = t->shape_host[0], segs = t->shape_host[1];
+        if (call == t->shape_host[2] && call != t->seen) {  // a consistent snapshot of that call's words
+            t->seen = call;
+            t->reordered = (uint64_t)stored * dk_tcp::kShapeStoredDen >= (uint64_t)std::max(segs, 1u);
+        }
+    }
+    const dk_tcp::Walker walker = nconns ? dk_tcp::pick_walk(n, nconns, t->walk, t->reordered) : dk_tcp::kLaneWalk;
+    t->last_walk = (int)walker;
     if (walker == dk_tcp::kScanWalk) {  // windows: ws = range[2c] / 64 + c + v < n / 64 + nconns + 1
         const size_t nw = (size_t)n / 64 + nconns + 1;
         if (t->used && (t->scan_sum_cap < nw || t->scan_ends_cap < nw * 64 || t->scan_head_cap < 8ull * nconns) &&
@@ -1513,6 +1587,9 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     P.scan_post = t->scan_post;
     P.scan_ends = t->scan_ends;
     P.scan_head = t->scan_head;
+    P.shape = t->shape;
+    P.shape_host = t->shape_host_dev;
+    P.call = t->calls + 1;
     P.out = *out;
     const dim3 gn((n + kBlock - 1) / kBlock), gr((2 * nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
     if (n) {
@@ -1551,7 +1628,10 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
                 hipLaunchKernelGGL(dk_tcp_walk_kernel, gc, dim3(kWalkBlock), 0, s, P);
         }
     }
-    if (n && nconns) hipLaunchKernelGGL(dk_tcp_fix_kernel, gn, dim3(kBlock), 0, s, P);
+    if (n && nconns) {
+        hipLaunchKernelGGL(dk_tcp_fix_kernel, gn, dim3(kBlock), 0, s, P);
+        t->calls++;
+    }
     if (hipGetLastError() != hipSuccess) return EINVAL;
     if (hipEventRecord(t->last, s) != hipSuccess) return EINVAL;
     t->last_stream = s;

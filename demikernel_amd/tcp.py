@@ -80,6 +80,12 @@ class TcpReceiver:
             _check(self.lib.dk_diag_tcp_set_walk(self._ctx, N.DK_TCP_WALKS[walk] if walk else -1, relay_waves),
                    "dk_diag_tcp_set_walk")
 
+    @property
+    def last_walk(self) -> Optional[str]:
+        """The walk the last process() call ran (dk_diag_tcp_last_walk), None before the first."""
+        w = self.lib.dk_diag_tcp_last_walk(self._ctx)
+        return {v: k for k, v in N.DK_TCP_WALKS.items()}.get(w)
+
     def close(self) -> None:
         if self._ctx:
             self.lib.dk_tcp_ctx_destroy(self._ctx)

@@ -56,6 +56,8 @@ int dk_diag_tx_set_tuning(int32_t split, int32_t sched, int32_t grid_per_cu);
  * starts on the rule; the environment is never read. 0 or EINVAL. */
 struct dk_tcp_ctx;
 int dk_diag_tcp_set_walk(struct dk_tcp_ctx* ctx, int32_t walk, int32_t relay_waves);
+/* The walk the context's last dk_tcp_rx_process call ran (0 lane, 1 wave, 2 relay, 3 scan; -1 none yet). */
+int dk_diag_tcp_last_walk(const struct dk_tcp_ctx* ctx);
 
 #ifdef __cplusplus
 }

@@ -26,4 +26,6 @@ step c3_ab 400 python tools/abtest.py --workload c3_udp64 --grids 0 --rotate 8 -
 step imix_ab 400 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 7 --iters 10 build/variants/base.so build/variants/cnt2.so
 step c2_ab 400 python tools/abtest.py --workload c2_tcp1500 --grids 0 --defer --reps 7 --iters 10 build/variants/base.so build/variants/cnt2.so
 step imix_sweep 400 python tools/sweep.py --workload c4_imix --frames 256K,512K,1M,1536K,2M --rotate 2 --tag base
+step tcp_walks 400 python tools/tcp_walk_probe.py --nconns 16 64 256 --streams bench clean --walks rule wave scan --iters 6
+step ring_numa 300 python tools/ring_numa.py
 echo done
