@@ -37,6 +37,14 @@ constexpr bool kPathStatsOn = true;
 #define DK_SUB_STAMP(j) do {} while (0)
 #endif
 
+// Section markers for the static per-block instruction budget (tools/isa_blocks.py on a -DDK_ISA_MARKS -S build): an
+// assembly comment "; MARK_<name>" where a section starts. Nothing in the product build.
+#ifdef DK_ISA_MARKS
+#define DK_MARK(name) asm volatile("; MARK_" #name)
+#else
+#define DK_MARK(name) do {} while (0)
+#endif
+
 // Per-wave phase totals over ALL of a wave's chunks (stamps only cover chunks k < 3): DK_ACC_BEGIN() at a phase
 // boundary, DK_ACC_SPLIT(j) adds the shader-clock ticks since the last boundary to total j (< 6); DK_ACC_WRITE
 // stores the totals into slots 20..25 and the chunk count into slot 26. Nothing in the product build.

@@ -687,12 +687,14 @@ template <bool kShift, bool kHdrT = false, uint32_t kR = kRoundsPerStep, uint32_
 __device__ __forceinline__ void coop_stream(const CoopPlan& pl, uint32_t lane, WaveLds& W, const Blob& B) {
 #if DK_COOP_MED_U > 0
     for (uint32_t r = 0; r * 4 < pl.nmed; r += kMR) {
+        DK_MARK(med_step);
         CoopStep<kMedU, kMR> S;
         coop_issue<kMedU, kMR, kHdrT>(0, pl.nmed, r, lane, W, B, S, 0);
         coop_finish<kShift, kMedU, kMR, kHdrT>(0, pl.nmed, 1, r, lane, W, B, S);
     }
 #endif
     for (uint32_t r = 0; r * 4 < pl.ncoop - pl.nmed; r += kR) {
+        DK_MARK(large_step);
         CoopStep<kCoopU, kR> S;
         coop_issue<kCoopU, kR, kHdrT>(pl.nmed, pl.ncoop, r, lane, W, B, S, 0);
         coop_finish<kShift, kCoopU, kR, kHdrT>(pl.nmed, pl.ncoop, pl.maxit, r, lane, W, B, S);
@@ -744,11 +746,14 @@ __device__ __forceinline__ void coop_gather(const FrameDesc<kShift>& F, const Co
 template <bool kShift, bool kHdrT = false, uint32_t kR = kRoundsPerStep>
 __device__ __forceinline__ void stream_chunk(const uint8_t* frames, uint64_t frames_bytes, bool live, uint32_t lane,
                                              WaveLds& W, uint32_t off, uint32_t len, Chunk& C) {
+    DK_MARK(phaseA);
     const FrameDesc<kShift> F(frames, frames_bytes, live, off, len);
     const Blob B(frames, frames_bytes);
     small_load(F, B, off, C.R);
+    DK_MARK(plan);
     const CoopPlan pl = coop_plan(F, lane, off, W);
     coop_stream<kShift, kHdrT, kR>(pl, lane, W, B);
+    DK_MARK(gather);
     coop_gather(F, pl, lane, W, C);
 }
 
@@ -874,6 +879,7 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     resum = false;  // path-stats: streamed frame whose segment is re-summed in-lane
     L.v = kNone; L.src = L.dst = L.ports = L.mhi = L.seq = L.ack = L.winurg = 0;
     L.S = L.E = L.hlen = L.stored = L.need = L.lsum = 0;
+    DK_MARK(parse);
     if (!live) {
         L.v = kNone;
     } else if (!inb) {
@@ -881,9 +887,11 @@ __device__ __forceinline__ void rx_front(const RxParams& P, bool live, uint32_t 
     } else if (fast) {
         parse_fast(R, len, P, L);
     } else {
+        DK_MARK(parse_slow);
         parse_headers(MemAcc{f}, len, P, L);
     }
     DK_SUB_STAMP(0);
+    DK_MARK(probe_l4sum);
     // First demux probe, issued before the checksum work (speculative: used only if the frame passes T4/U3/T5).
     // TCP: the Active slot (hashed); UDP: the flow bound to (local_ip, port), one load of the port table.
     St.fast = fast;
@@ -914,6 +922,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
     const bool fast = St.fast, resum = St.resum, big = St.big, inb = St.inb;
     const uint8_t* f = P.frames + off;
 
+    DK_MARK(verdict_demux);
     uint32_t fid = DK_FLOW_NONE;
     if (L.v == kPendIcmp) {
         // compute_checksum over header + body must fold to 0, i.e. the BE word sum is 0 mod 0xFFFF; the LE-half sum
@@ -934,6 +943,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
             if (c != L.stored) L.v = tcp ? DK_V_TCP_CSUM : DK_V_UDP_CSUM;
         }
         if (L.v == kPendTcp && L.hlen > 20) {
+            DK_MARK(tcp_options);
             const uint32_t e = tcp_options(f + L.S + 20, L.hlen - 20,
                                            kOpt && live && P.res.tcp_opts ? P.res.tcp_opts + i : nullptr);
             if (e) L.v = e;
@@ -955,6 +965,7 @@ __device__ __forceinline__ void rx_back(const RxParams& P, uint32_t i, bool live
     }
 
     DK_SUB_STAMP(2);
+    DK_MARK(results);
     const uint32_t v = L.v;
     if (live) {
         // fields for delivered / no-socket TCP and UDP and for parsed ARP and ICMPv4 (codes 0..3, dk_rx.h)
@@ -1292,6 +1303,7 @@ void dk_rx_kernel(RxParams P) {
     DK_ACC_DECL;
     for (uint32_t k = 0; have; k++, c = nc, lim = nlim) {
         DK_ACC_BEGIN();
+        DK_MARK(loop_top);
         // The lane id re-materialised per chunk: without this the compiler keeps ~20 lane-derived address constants
         // of phases A-C in VGPRs across the whole loop, and this kernel sits at its 168-VGPR budget (3 waves/SIMD).
         uint32_t lane = lane_id();
@@ -1316,6 +1328,7 @@ void dk_rx_kernel(RxParams P) {
         rec.meta = kNoRec;
         Chunk C;
         if (k < 3) DK_STAMPW(2 + 3 * k);
+        DK_MARK(stream);
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
         // the grab for chunk k + 2, resolved at the top of the next round: issued after the frame stream (its return
@@ -1324,12 +1337,14 @@ void dk_rx_kernel(RxParams P) {
         if (have && k + 2 >= ks) Q.issue(P, lane);
         if (k < 3) DK_STAMPW(3 + 3 * k);
         DK_ACC_SPLIT(0);
+        DK_MARK(phaseC);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (k < 3) DK_STAMPW(4 + 3 * k);
         DK_ACC_SPLIT(1);
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
         // at the top of the next chunk, after a staged flush, their wait also waited for every store's write ack.
         asm volatile("" ::"v"(noff), "v"(nlen));
+        DK_MARK(stage);
         if (kStage) {  // the last kStageK chunks' results; stored when full and at exit
             stage_put(stg, rec);
             if (lane == 0) W.cb[nstg] = c;
@@ -1339,12 +1354,15 @@ void dk_rx_kernel(RxParams P) {
             }
         }
         DK_ACC_SPLIT(2);
+        DK_MARK(count);
         count_chunk(P, live, lane, v, fid, lds_flows, s_flow, s_vh);
         DK_ACC_SPLIT(3);
         DK_ACC_CHUNK();
+        DK_MARK(loop_tail);
     }
 
     DK_STAMPW(11);
+    DK_MARK(epilogue);
     DK_ACC_BEGIN();
     if (kStage && nstg) flush_staged(P, reinterpret_cast<const StgRec<false>(&)[kStageK]>(stg), nstg, W.cb, lane);
     DK_ACC_SPLIT(4);
@@ -1711,6 +1729,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         DK_ACC_BEGIN();
         // the lane id re-materialised per chunk (as in dk_rx_kernel): lane-derived constants are not held in VGPRs
         // across the loop
+        DK_MARK(s_loop_top);
         uint32_t lane = lane_id();
         asm volatile("" : "+v"(lane));
         const uint32_t i = c + lane;
@@ -1724,8 +1743,10 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         const FrameDesc<kShift> F1(P.frames, P.frames_bytes, have1 && c1 + lane < lim1, off1, len1);
         uint32_t v, fid;
         if (k == 0) DK_STAMP(1);
+        DK_MARK(s_window);
         small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
         if (k < 3) DK_STAMP(2 + 3 * k);
+        DK_MARK(s_eligible);
         DK_ACC_SPLIT(0);
         if (kShift && __ballot(live && F.vec && !F.big && F.sh != 0)) {  // realign the windows of shifted frames
             uint32_t x[4] = {0, 0, 0, 0};
@@ -1734,11 +1755,14 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         const bool take = live && small_fast_eligible(F, len, C.R);
         const uint64_t dm = __ballot(live && !take);
         deferred = deferred || dm != 0;
+        DK_MARK(s_fast);
         small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid);
         if (k < 3) DK_STAMP(3 + 3 * k);
         DK_ACC_SPLIT(1);
         if (kLateBarrier && k == 0) lds_barrier();  // every wave of the workgroup arrives once (below if no chunk)
+        DK_MARK(s_count);
         count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
+        DK_MARK(s_loop_tail);
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
             if (lane == 0) P.defer[k * nw + gw] = dm;
             if (k < 64) had |= 1ull << k;
@@ -1759,6 +1783,7 @@ __global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_k
         off1 = off2;
         len1 = len2;
     }
+    DK_MARK(s_epilogue);
     if (kLateBarrier && !have0) lds_barrier();
     DK_ACC_BEGIN();
     if (deferred) {  // the general pass over the frames the loop left (byte path, streamed frames, options, ARP)
