@@ -15,6 +15,8 @@ step() {  # step <name> <seconds> <cmd...>: stdout+stderr to $O/<name>.log
   if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc"; tail -20 $O/$name.log; exit 10; fi
 }
 export TMPDIR=/tmp
+# the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
+python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
 # s2: GPU suite (TX fields form); the C3 read/write-mix ceiling; C3 sweep at sizes near the bench's and a
 # no-counters ablation; interleaved A/B of merged counting and the late barrier on C3, IMIX, C2
