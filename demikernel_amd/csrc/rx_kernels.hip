@@ -1263,6 +1263,9 @@ struct TailQ {
 #ifndef DK_MIN_WAVES_ALIGNED
 #define DK_MIN_WAVES_ALIGNED DK_MIN_WAVES
 #endif
+#ifndef DK_STAGED_PRIO
+#define DK_STAGED_PRIO 0  // > 0: a wave streaming its chunk's frames issues at this priority, phase C at 0
+#endif
 template <bool kShift, bool kStage>
 __global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED)
 void dk_rx_kernel(RxParams P) {
@@ -1329,6 +1332,7 @@ void dk_rx_kernel(RxParams P) {
         Chunk C;
         if (k < 3) DK_STAMPW(2 + 3 * k);
         DK_MARK(stream);
+        if (DK_STAGED_PRIO) __builtin_amdgcn_s_setprio(DK_STAGED_PRIO);  // the frame stream issues ahead of phase C
         stream_chunk<kShift, false, kStage ? kRoundsStaged : kRoundsPerStep>(P.frames, P.frames_bytes, live, lane, W, off,
                                                                               len, C);
         // the grab for chunk k + 2, resolved at the top of the next round: issued after the frame stream (its return
@@ -1337,6 +1341,7 @@ void dk_rx_kernel(RxParams P) {
         if (have && k + 2 >= ks) Q.issue(P, lane);
         if (k < 3) DK_STAMPW(3 + 3 * k);
         DK_ACC_SPLIT(0);
+        if (DK_STAGED_PRIO) __builtin_amdgcn_s_setprio(0);
         DK_MARK(phaseC);
         rx_finish<kShift, kStage>(P, i, live, lane, W, off, len, C, v, fid, rec);
         if (k < 3) DK_STAMPW(4 + 3 * k);

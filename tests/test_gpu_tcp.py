@@ -289,24 +289,25 @@ def test_rejects_misaligned_conns(tcp):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("nconns,reorder", [(64, 3.0), (64, 0.0), (16, 3.0), (15, 3.0), (256, 3.0), (8, 3.0)])
+@pytest.mark.parametrize("nconns,reorder", [(64, 3.0), (64, 0.0), (15, 3.0), (14, 3.0), (255, 3.0), (8, 3.0)])
 def test_walk_follows_stream_shape(nconns, reorder):
     """The engine's own rule (no forced walk) at the scan walk's envelope (1,024 segments per connection): the first
     call runs the scan walk; later calls run the wave walk when the last finished call stored >= 1 segment in 1,024
-    out of order and there are >= 16 connections (the rule's two boundaries: 16 vs 15 connections, and the stored
-    fraction, which the oracle's STORED count decides here; 256 connections with this stream sit near 0.1 %), the
-    scan walk otherwise. Every call bit-exact vs the oracle, whichever walk ran."""
+    out of order and the table has >= 16 connections (the rule's two boundaries: 16 vs 15 rows — the listener's row
+    counts — and the stored fraction, which the oracle's STORED count decides here), the scan walk otherwise (256 rows:
+    the scan walk's upper bound). Every call bit-exact vs the oracle, whichever walk ran."""
     import torch
 
-    n = 1024 * nconns
+    n = 1024 * len(synth.make_flows(nconns, seed=77 + nconns))  # the table has a row per flow (the listener's too)
     _, tr, table = synth.tcp_streams(n, nconns, 1500, buffer_size=1 << 24, reorder=reorder, seed=77 + nconns)
+    assert n == 1024 * len(table)
     rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
           "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
           "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
     exp_t = table.copy()
     exp = O.tcp_process(exp_t, rx)
     stored = int((exp["action"] == N.A["STORED"]).sum())
-    want = "wave" if stored * 1024 >= n and nconns >= 16 else "scan"
+    want = "wave" if stored * 1024 >= n and len(table) >= 16 else "scan"
     r = rx_device(rx)
     tcp = TcpReceiver(0)
     walks = []

@@ -122,24 +122,29 @@ def main():
             o[:] = template
             forms["bind_other"] = (o, True, err)
     rings = {k: RG.TpacketRing(buf, a.block, register=reg) for k, (buf, reg, _) in forms.items()}
+    # the same rings through staged copies (the copy engine moves each chunk's byte range to HBM: layout-blind)
+    eng_st = RxEngine(Config(synth.BOB_IPV4), device=0, tuning={"host_zc": 0})
+    eng_st.set_sockets(flows)
     # the packed host path from pinned memory, as bench.py host_path
     pin = torch.from_numpy(packed).pin_memory().numpy()
-    rates = {k: [] for k in list(rings) + ["packed_pinned"]}
+    rates = {k: [] for k in list(rings) + [k + "+staged" for k in rings] + ["packed_pinned"]}
     for rep in range(a.reps):
         for k, r in rings.items():
-            t = time.perf_counter()
-            nf, nb = r.receive(eng, 0, used, res)
-            rates[k].append(nbytes / (time.perf_counter() - t) / 1e9)
-            assert nf == n and nb == used
+            for e, kk in ((eng, k), (eng_st, k + "+staged")):
+                t = time.perf_counter()
+                nf, nb = r.receive(e, 0, used, res)
+                rates[kk].append(nbytes / (time.perf_counter() - t) / 1e9)
+                assert nf == n and nb == used
         t = time.perf_counter()
         eng.receive_batch_host(pin, poff, lens, res)
         rates["packed_pinned"].append(nbytes / (time.perf_counter() - t) / 1e9)
     for k in rates:
-        buf = forms[k][0] if k in forms else pin
+        base = k.split("+")[0]
+        buf = forms[base][0] if base in forms else pin
         row = {"form": k, "gbps": round(float(np.median(rates[k])), 2), "gbps_max": round(max(rates[k]), 2),
                "page_nodes": page_nodes(buf.ctypes.data, buf.nbytes)}
-        if k in forms and forms[k][2]:
-            row["bind_error"] = forms[k][2]
+        if base in forms and forms[base][2]:
+            row["bind_error"] = forms[base][2]
         print(json.dumps(row), flush=True)
     for r in rings.values():
         r.close()
