@@ -339,7 +339,10 @@ def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=5):
     lens = batch.len[:n].cpu().numpy().view(np.uint16).copy()
     end = int(off[-1]) + int(lens[-1])
     blob = batch.blob[:end].cpu().numpy()
-    ring, used, _, elen = RG.build_tpacket3(blob, off, lens, block_size)
+    # the ring's pages on the GPU's NUMA node (as a LibOS creating the PACKET_RX_RING from a thread there gets them):
+    # placed by first touch on the other socket the path lost 5 % (tools/ring_numa.py)
+    node = RG.gpu_numa_node(batch.blob.device.index or 0)
+    ring, used, _, elen = RG.build_tpacket3(blob, off, lens, block_size, numa_node=node)
     r = RG.TpacketRing(ring, block_size)
     res = RxResults(n, len(flows), host=True)
     nbytes = int(elen.astype(np.int64).sum())
@@ -357,7 +360,7 @@ def ring_path_rate(eng, batch, flows, nframes, block_size=1 << 22, reps=5):
         r.close()
     return {"gbps": round(float(np.median(rates)), 2), "gbps_max": round(max(rates), 2), "frames": n, "bytes": nbytes,
             "blocks": used, "block_size": block_size, "reps": reps, "stat": "median",
-            "host_scan_ms": round(float(np.median(scans)) * 1e3, 3),
+            "host_scan_ms": round(float(np.median(scans)) * 1e3, 3), "ring_numa_node": node,
             "pipeline": "TPACKET_V3 block scan + dk_rx_process_host over the registered ring"}
 
 

@@ -31,18 +31,46 @@ def _check_blocks(rc: int, what: str, blocks: int) -> None:
         raise e
 
 
-def page_aligned_empty(nbytes: int) -> np.ndarray:
-    """Anonymous-mmap backed u8 array (page aligned, like a PACKET_RX_RING mapping; hipHostRegister-able)."""
+def gpu_numa_node(device: int = 0) -> int:
+    """The host NUMA node the GPU's PCIe root sits on (/sys/bus/pci/devices/<bdf>/numa_node), -1 if unknown."""
+    import torch
+
+    p = torch.cuda.get_device_properties(device)
+    bdf = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    try:
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            return int(f.read().strip())
+    except (OSError, ValueError):
+        return -1
+
+
+def _mbind(addr: int, nbytes: int, node: int) -> bool:
+    """Bind [addr, addr + nbytes) to one NUMA node before its first touch (mbind MPOL_BIND; x86_64 syscall 237)."""
+    libc = ctypes.CDLL(None, use_errno=True)
+    mask = (ctypes.c_ulong * 16)()
+    mask[node // 64] = 1 << (node % 64)
+    return libc.syscall(237, ctypes.c_void_p(addr), ctypes.c_ulong(nbytes), 2, mask, ctypes.c_ulong(16 * 64), 0) == 0
+
+
+def page_aligned_empty(nbytes: int, numa_node: int = -1) -> np.ndarray:
+    """Anonymous-mmap backed u8 array (page aligned, like a PACKET_RX_RING mapping; hipHostRegister-able). numa_node
+    >= 0: its pages are placed on that node (the GPU's, gpu_numa_node: a ring the kernel reads over PCIe from the other
+    socket's memory lost 5 % in tools/ring_numa.py), as a LibOS gets by creating the ring from a thread
+    on the GPU's node."""
     import mmap
 
     m = mmap.mmap(-1, max(nbytes, 1), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
-    return np.frombuffer(m, np.uint8, count=nbytes)
+    a = np.frombuffer(m, np.uint8, count=nbytes)
+    if numa_node >= 0 and nbytes:
+        _mbind(a.ctypes.data, nbytes, numa_node)  # best effort: placement is a speed property only
+    return a
 
 
 def build_tpacket3(blob: np.ndarray, off: np.ndarray, lens: np.ndarray, block_size: int = 1 << 20,
-                   nblocks: Optional[int] = None, seq0: int = 1):
+                   nblocks: Optional[int] = None, seq0: int = 1, numa_node: int = -1):
     """Pack frames blob[off[i]:off[i]+lens[i]] into TPACKET_V3 blocks, every used block closed (TP_STATUS_USER).
-    Returns (ring u8 array, blocks used, expected off u32[], expected len u16[]): the descriptors a scan must give."""
+    Returns (ring u8 array, blocks used, expected off u32[], expected len u16[]): the descriptors a scan must give.
+    numa_node: see page_aligned_empty."""
     lens = np.asarray(lens, np.int64)
     n = len(lens)
     need = (TP_MAC + lens + 7) & ~7  # TOTAL_PKT_LEN_INCL_ALIGN (8-byte packet alignment)
@@ -58,7 +86,7 @@ def build_tpacket3(blob: np.ndarray, off: np.ndarray, lens: np.ndarray, block_si
     used = b + 1 if n else 0
     nblocks = used if nblocks is None else nblocks
     assert nblocks >= used
-    ring = page_aligned_empty(nblocks * block_size)
+    ring = page_aligned_empty(nblocks * block_size, numa_node)
     ring[:] = 0
     start = block_of * block_size + pos
     exp_off = (start + TP_MAC).astype(np.uint32)
