@@ -343,12 +343,13 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
     }
     if (T.grid_per_cu > 0) per_cu = (uint32_t)T.grid_per_cu;
     // workgroups of the small-frame kernel take (waves / 4) 256-frame tiles per round
-    const uint32_t tiles_per_wg = p.small ? std::max(dk_rx_small_block_waves() / 4u, 1u) : 1u;
+    const uint32_t small_waves = p.small ? dk_rx_small_block_waves(p.ub != nullptr) : 0u;
+    const uint32_t tiles_per_wg = p.small ? std::max(small_waves / 4u, 1u) : 1u;
     uint32_t grid = std::min((ntiles + tiles_per_wg - 1) / tiles_per_wg, per_cu * c->cu_count);
     if (T.grid > 0) grid = std::min(ntiles, (uint32_t)T.grid);
     if (p.flow_mode == dk::kFlowLds)
         grid = std::max(grid, (ntiles + dk::kMaxTilesPerBlockLds - 1) / dk::kMaxTilesPerBlockLds);
-    p.small_kmin = p.small ? ((p.n + 63) / 64) / (grid * dk_rx_small_block_waves()) : 0u;
+    p.small_kmin = p.small ? ((p.n + 63) / 64) / (grid * small_waves) : 0u;
     // The staged kernel's dynamic tail (rx_common.h): with `per` whole round-robin rounds of chunks per wave, the
     // first per + 1 - d stay round-robin and the rest (d - 1 rounds + the partial one) are grabbed from per-XCD
     // counters; at least 2 round-robin rounds (the first grab is issued during round ks - 2).
@@ -372,7 +373,7 @@ int launch_batch(dk_rx_ctx* c, dk::RxParams& p, uint64_t size_hint, hipStream_t 
         if (s.used && s.stream == stream && s.cs.pending) has_pending = true;
     p.row_words = p.flow_words + (p.res.verdict_counts ? dk::kVerdictWords : 0u);
     // per (wave, chunk): at most ceil(n / 64) + 2 chunks per wave of the grid (sched 1's partial chunks)
-    const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * dk_rx_small_block_waves() : 0;
+    const size_t ndefer = p.small ? ((size_t)p.n + 63) / 64 + 2ull * grid * small_waves : 0;
     if (p.row_words || ndefer || has_pending || p.tail_ks) {
         if ((rc = acquire_slot(c, stream, &slot))) return rc;
         if (p.tail_ks) {

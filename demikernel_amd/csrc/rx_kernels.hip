@@ -1436,8 +1436,18 @@ struct SmallLds<true> {
 #define DK_SMALL_WAVES 8  // waves per workgroup of the small-frame kernel: 8 since round 5 (at 6 waves/SIMD, half the
                           // counter rows: C3 -2.7 %, random ports -2 %, session r05v; 4 was ahead at 5 waves/SIMD)
 #endif
-constexpr uint32_t kSmallWaves = DK_SMALL_WAVES;
-constexpr int kSmallBlock = 64 * DK_SMALL_WAVES;
+#ifndef DK_SMALL_WAVES_PORT
+#define DK_SMALL_WAVES_PORT DK_SMALL_WAVES  // the instantiation that looks UDP binds up in the port table
+#endif
+#ifndef DK_SMALL_WAVES_UB
+#define DK_SMALL_WAVES_UB DK_SMALL_WAVES  // the instantiation with the LDS bind table (binds on scattered ports)
+#endif
+// Waves per workgroup of one small-kernel instantiation (the host asks dk_rx_small_block_waves(ub)).
+template <bool kUb>
+struct SmallShape {
+    static constexpr uint32_t kWaves = kUb ? DK_SMALL_WAVES_UB : DK_SMALL_WAVES_PORT;
+    static constexpr int kBlock = 64 * (int)kWaves;
+};
 // The window lives in LDS swizzled: slot s holds window granule s ^ ((s >> 4) & 3) (an involution: it swaps granules
 // within aligned groups of 4 by bits 4-5 of the index, so each DMA piece still reads the same 64-byte pieces of the
 // blob). Unswizzled, 64 packed 64-byte frames read back as 4 ds_read_b128 at a 64-byte lane stride put lanes
@@ -1674,7 +1684,9 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
 }
 
 template <bool kShift, bool kOpt, bool kUb = false>
-__global__ __launch_bounds__(kSmallBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
+__global__ __launch_bounds__(SmallShape<kUb>::kBlock, DK_MIN_WAVES_SMALL) void dk_rx_small_kernel(RxParams P) {
+    constexpr uint32_t kSmallWaves = SmallShape<kUb>::kWaves;
+    constexpr int kSmallBlock = SmallShape<kUb>::kBlock;
     __shared__ SmallLds<kUb> s_wave[kSmallWaves];
     __shared__ uint32_t s_vh[DK_V_COUNT];  // verdict histogram
     extern __shared__ __attribute__((aligned(16))) uint32_t s_flow[];  // kFlowLds: packed u16 flow counters
@@ -2324,11 +2336,12 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_split_kernel<true, 1>, dk::kSplitBlock,
                                                           dyn_lds_bytes);
     else if (family == dk::kFamilySmall)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>, dk::kSmallBlock,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true>,
+                                                          dk::SmallShape<false>::kBlock,
                                                           dyn_lds_bytes);
     else if (family == dk::kFamilySmallUb)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dk::dk_rx_small_kernel<true, true, true>,
-                                                          dk::kSmallBlock, dyn_lds_bytes);
+                                                          dk::SmallShape<true>::kBlock, dyn_lds_bytes);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &blocks, family == dk::kFamilyStaged ? dk::dk_rx_kernel<true, true> : dk::dk_rx_kernel<true, false>,
@@ -2336,7 +2349,7 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family) {
     return e == hipSuccess ? blocks : 0;
 }
 
-uint32_t dk_rx_small_block_waves() { return dk::kSmallWaves; }
+uint32_t dk_rx_small_block_waves(bool ub) { return ub ? dk::SmallShape<true>::kWaves : dk::SmallShape<false>::kWaves; }
 
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     if (p.n == 0 || grid == 0) return 0;
@@ -2346,22 +2359,23 @@ int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream) {
     const hipStream_t s = (hipStream_t)stream;
     const bool opt = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win || p.res.tcp_opts || p.path_stats;
     const bool tcp = p.res.tcp_seq || p.res.tcp_ack || p.res.tcp_win;  // the split kernel stages the TCP fields
+    const int SMALL_BLOCK = p.ub ? dk::SmallShape<true>::kBlock : dk::SmallShape<false>::kBlock;
     if (p.small && p.ub && p.aligned16 && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true, true>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small && p.ub && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false, true>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small && p.ub && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true, true>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small && p.ub)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false, true>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small && p.aligned16 && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, true>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small && p.aligned16)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<false, false>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small && opt)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, true>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.small)
-        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(dk::kSmallBlock), dyn, s, p);
+        hipLaunchKernelGGL((dk::dk_rx_small_kernel<true, false>), dim3(grid), dim3(SMALL_BLOCK), dyn, s, p);
     else if (p.split && p.aligned16 && tcp)
         hipLaunchKernelGGL((dk::dk_rx_split_kernel<false, 1, true>), dim3(grid), dim3(dk::kSplitBlock), dyn, s, p);
     else if (p.split && tcp)
