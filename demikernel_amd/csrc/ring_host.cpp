@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/dk_ring.h"
+#include "rx_common.h"
 
 namespace {
 
@@ -207,7 +208,7 @@ int dk_rx_process_tpacket3(dk_rx_ctx* ctx, const void* ring, uint64_t ring_bytes
                                n_frames, n_blocks);
     if (rc || *n_frames == 0) return rc;
     const dk_rx_batch b{static_cast<const uint8_t*>(ring), ring_bytes, t_descs.off, t_descs.len, *n_frames, 0};
-    return dk_rx_process_host(ctx, &b, res, 0);
+    return dk_rx_process_ring_host(ctx, &b, res);
 }
 
 }  // extern "C"

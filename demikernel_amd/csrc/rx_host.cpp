@@ -701,7 +701,29 @@ const uint8_t* mapped_alias(const uint8_t* p, uint64_t bytes) {
 }
 }  // namespace
 
+namespace {
+int process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, uint32_t chunk_frames, bool allow_zc);
+}  // namespace
+
 int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, uint32_t chunk_frames) {
+    if (!c) return EINVAL;
+    return process_host(c, b, r, chunk_frames, c->tune.host_zc != 0);
+}
+
+}  // extern "C"
+
+// A TPACKET_V3 ring's frames go through staged copies by default: the copy engine moves each chunk's byte range
+// (headers included) to HBM, which is blind to the ring's layout and to the NUMA node of its pages, where the kernel
+// reading the ring in place over PCIe loses to both (tools/ring_numa.py, session r6s3: staged 46.2-46.4 GB/s whatever
+// the placement; in place 45.0 from the GPU's node, 42.4 from the other). host_zc = 1 (dk_diag) forces the
+// in-place reads for A/B.
+int dk_rx_process_ring_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r) {
+    if (!c) return EINVAL;
+    return process_host(c, b, r, 0, c->tune.host_zc > 0);
+}
+
+namespace {
+int process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r, uint32_t chunk_frames, bool allow_zc) {
     if (!c || !b || !r) return EINVAL;
     if (b->n && (!b->frames || !b->off || !b->len)) return EINVAL;
     if (b->n && (!r->meta || !r->src_ip || !r->ports || !r->payload || !r->flow_id)) return EINVAL;
@@ -715,7 +737,7 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
     // For packed frames both forms run at the PCIe rate (C5 shard 51-53 GB/s); for frames scattered in
     // mbuf slots the staged copies would also move the unused bytes between them. Chunked zero-copy launches
     // measured slower (44 GB/s).
-    const uint8_t* zc = c->tune.host_zc != 0 ? mapped_alias(b->frames, b->frames_bytes) : nullptr;
+    const uint8_t* zc = allow_zc ? mapped_alias(b->frames, b->frames_bytes) : nullptr;
     const uint32_t chunk_n = zc && !chunk_frames ? b->n : chunk;
     // Chunk boundaries: consecutive frame ranges whose covering byte range stays under kMaxChunkBytes (staged).
     std::vector<dk::HostChunk> chunks;
@@ -821,6 +843,9 @@ int dk_rx_process_host(dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* 
     }
     return 0;
 }
+}  // namespace
+
+extern "C" {
 
 #ifdef DK_DIAG_STAMPS
 constexpr size_t kPathStatsWords = 4 + (1u << 21);  // + 16 stamps per wave

@@ -80,7 +80,7 @@ struct Params {
     uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
     uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
                           // fin_pending, fin_seq}, saved by the scan kernel for the post kernel
-    uint32_t* shape;      // device [2] {STORED segments, finished blocks} of this call (zero between calls)
+    uint32_t* shape;      // device u64: finished blocks << 40 | STORED segments of this call (zero between calls)
     uint32_t* shape_host; // host-mapped [3] {STORED, n, call number}: written by the fix kernel's last block
     uint32_t call;
     dk_tcp_out out;
@@ -147,14 +147,18 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_fix_kernel(Params P) {
     if (threadIdx.x == 0) {
         uint32_t sum = 0;
         for (uint32_t w = 0; w < kBlock / 64; w++) sum += s_cnt[w];
-        if (sum) atomicAdd(P.shape, sum);
-        __threadfence();
-        if (atomicAdd(P.shape + 1, 1u) == gridDim.x - 1) {  // the last block: every count is in
-            const uint32_t total = atomicExch(P.shape, 0u);
-            atomicExch(P.shape + 1, 0u);  // zero for the context's next call (ordered after it on the stream)
+        // One 64-bit atomic per block carries both its count (low 40 bits) and its arrival (high 24 bits): the block
+        // that arrives last holds the total without any fence (a device-scope release here wrote back the L2 in every
+        // block: +45 % on the 16,384-connection call). Host-mapped words are visible once the kernel has completed,
+        // which is when the host reads them (the call's event).
+        const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(P.shape),
+                                                 (1ull << 40) | (unsigned long long)sum);
+        if ((uint32_t)(old >> 40) == gridDim.x - 1) {
+            const uint32_t total = (uint32_t)(old & ((1ull << 40) - 1)) + sum;
+            atomicExch(reinterpret_cast<unsigned long long*>(P.shape), 0ull);  // zero for the context's next call
             __hip_atomic_store(P.shape_host + 0, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(P.shape_host + 1, P.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(P.shape_host + 2, P.call, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(P.shape_host + 2, P.call, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -1450,7 +1454,7 @@ struct dk_tcp_ctx {
     uint32_t* scan_head = nullptr;
     size_t scan_sum_cap = 0, scan_post_cap = 0, scan_ends_cap = 0, scan_head_cap = 0;
     // the stream's shape (pick_walk): the fix kernel's STORED count of each call, in host-mapped memory
-    uint32_t* shape = nullptr;            // device [2], zero between calls
+    uint32_t* shape = nullptr;            // device u64 (8-byte aligned: hipMalloc), zero between calls
     volatile uint32_t* shape_host = nullptr;  // host-mapped [3] {STORED, n, call}
     uint32_t* shape_host_dev = nullptr;   // its device alias
     uint32_t calls = 0;                   // calls issued (the number the next fix kernel writes is calls + 1)

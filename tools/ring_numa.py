@@ -7,8 +7,9 @@ land? One process, the same 1500-byte frames in the same ring layout, the ring b
   bind_gpu      the mmap bound to the GPU's NUMA node (mbind MPOL_BIND) before the first touch, then registered;
   bind_other    the same bound to another node (the contrast), when the host has one.
 For each: the NUMA nodes of its pages (move_pages query on every 16th page), then the ring path (dk_rx_process_tpacket3,
-block scan + kernel reading the ring in place + results back) `--reps` times interleaved, median GB/s of frame bytes,
-and the packed host path (dk_rx_process_host from pinned memory) beside them. One JSON line per form."""
+block scan + kernel reading the ring in place (host_zc 1) / through staged copies (+staged, the default since round 6)
++ results back) `--reps` times interleaved, median GB/s of frame bytes, and the packed host path (dk_rx_process_host
+from pinned memory, read in place) beside them. One JSON line per form."""
 import argparse
 import ctypes
 import json
@@ -93,7 +94,7 @@ def main():
     flows = synth.make_flows(1024)
     tr = synth.traffic(n, np.full(n, 1486, np.uint16), flows, seed=synth.SEED + 5)
     packed, poff, lens = synth.build_numpy(tr)
-    eng = RxEngine(Config(synth.BOB_IPV4), device=0)
+    eng = RxEngine(Config(synth.BOB_IPV4), device=0, tuning={"host_zc": 1})  # the ring read in place (zero-copy)
     eng.set_sockets(flows)
     res = RxResults(n, len(flows), host=True)
     nbytes = int(lens.astype(np.int64).sum())
@@ -122,7 +123,8 @@ def main():
             o[:] = template
             forms["bind_other"] = (o, True, err)
     rings = {k: RG.TpacketRing(buf, a.block, register=reg) for k, (buf, reg, _) in forms.items()}
-    # the same rings through staged copies (the copy engine moves each chunk's byte range to HBM: layout-blind)
+    # the same rings through staged copies (the copy engine moves each chunk's byte range to HBM: layout-blind; the
+    # ring path's default since round 6)
     eng_st = RxEngine(Config(synth.BOB_IPV4), device=0, tuning={"host_zc": 0})
     eng_st.set_sockets(flows)
     # the packed host path from pinned memory, as bench.py host_path
