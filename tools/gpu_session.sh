@@ -18,12 +18,8 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s3: C3 with 12-wave workgroups (a third fewer counter rows), IMIX with stream-phase issue priority, the ring path
-# in NUMA-placed and staged-copy forms, and the full bench line at the current tree
+# s4: GPU suite and the bench line after the fence-free TCP shape count and the staged ring path; ring forms again
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step c3_ab 400 python tools/abtest.py --workload c3_udp64 --grids 0 --rotate 8 --defer --reps 9 --iters 20 build/variants/base.so build/variants/w12p.so
-step c3r_ab 400 python tools/abtest.py --workload c3_udp64_random_ports --grids 0 --rotate 8 --defer --reps 9 --iters 20 build/variants/base.so build/variants/w12p.so
-step imix_ab 400 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 7 --iters 10 build/variants/base.so build/variants/prio1.so build/variants/prio2.so
-step ring_numa 300 python tools/ring_numa.py
 step bench 600 python bench.py
+step ring_numa 300 python tools/ring_numa.py
 echo done
