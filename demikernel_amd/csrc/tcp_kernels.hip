@@ -130,8 +130,11 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_key_kernel(Params P) {
 }
 
 // Classified segments after their connection's close are UNPROCESSED (the walks' queued-behind-the-close rule). The
-// same pass counts the call's STORED segments (the stream's shape: the walk choice of the context's next call, below)
-// and the last block to finish writes the count to the context's host-mapped word.
+// same pass counts the STORED segments of the first kShapeBlocks blocks (16,384 segments in arrival order, every
+// connection's: the stream's shape, the walk choice of the context's next call, below) and the last of those blocks
+// writes the count to the context's host-mapped words. (Counting in every block meant thousands of same-address
+// atomics: 40-50 us on a 1M-segment call, session r6s4.)
+constexpr uint32_t kShapeBlocks = 64;
 __global__ __launch_bounds__(kBlock) void dk_tcp_fix_kernel(Params P) {
     __shared__ uint32_t s_cnt[kBlock / 64];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -139,25 +142,27 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_fix_kernel(Params P) {
     if (i < P.n) {
         const uint32_t c = P.cls[i];
         if (c != kNoConn && i >= P.open_until[c]) P.out.action[i] = DK_TCP_UNPROCESSED;
-        else stored = c == kNoConn && P.out.action[i] == DK_TCP_STORED;
+        else stored = blockIdx.x < kShapeBlocks && c == kNoConn && P.out.action[i] == DK_TCP_STORED;
     }
+    if (blockIdx.x >= kShapeBlocks) return;  // block-uniform
     const uint64_t m = __ballot(stored);
     if ((threadIdx.x & 63u) == 0) s_cnt[threadIdx.x / 64] = (uint32_t)__popcll(m);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t sum = 0;
         for (uint32_t w = 0; w < kBlock / 64; w++) sum += s_cnt[w];
-        // One 64-bit atomic per block carries both its count (low 40 bits) and its arrival (high 24 bits): the block
-        // that arrives last holds the total without any fence (a device-scope release here wrote back the L2 in every
-        // block: +45 % on the 16,384-connection call). Host-mapped words are visible once the kernel has completed,
-        // which is when the host reads them (the call's event).
+        // One 64-bit atomic per sampling block carries both its count (low 40 bits) and its arrival (high 24 bits):
+        // the block that arrives last holds the total without any fence (a device-scope release here wrote back the
+        // L2 in every block). Host-mapped words are visible once the kernel has completed, which is when the host
+        // reads them (the call's event).
+        const uint32_t nb = min(gridDim.x, kShapeBlocks);
         const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(P.shape),
                                                  (1ull << 40) | (unsigned long long)sum);
-        if ((uint32_t)(old >> 40) == gridDim.x - 1) {
+        if ((uint32_t)(old >> 40) == nb - 1) {
             const uint32_t total = (uint32_t)(old & ((1ull << 40) - 1)) + sum;
             atomicExch(reinterpret_cast<unsigned long long*>(P.shape), 0ull);  // zero for the context's next call
             __hip_atomic_store(P.shape_host + 0, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(P.shape_host + 1, P.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(P.shape_host + 1, min(P.n, nb * kBlock), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(P.shape_host + 2, P.call, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }

@@ -18,8 +18,7 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s4: GPU suite and the bench line after the fence-free TCP shape count and the staged ring path; ring forms again
+# s5: GPU suite and the bench line after sampling the TCP shape count (64 blocks)
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
 step bench 600 python bench.py
-step ring_numa 300 python tools/ring_numa.py
 echo done
