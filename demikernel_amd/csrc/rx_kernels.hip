@@ -1098,15 +1098,22 @@ __device__ __forceinline__ uint32_t opaque_v(uint32_t x) {
     asm volatile("" : "+v"(x));
     return x;
 }
+// An LDS add the compiler does not see as an LDS access: issued while the wave's LDS-DMA window is in flight (the
+// pipelined small-frame loop), a compiler-visible LDS atomic waits for the DMA first (it may alias the DMA's target);
+// these never do (the counters are not in any wave's window). No return value, so no wait of its own.
+__device__ __forceinline__ void lds_add_asm(uint32_t* p, uint32_t v) {
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)p;
+    asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(v));
+}
+template <bool kAsm = false>
 __device__ __forceinline__ void flow_add(const RxParams& P, bool lds_flows, uint32_t* s_flow, uint32_t fid,
                                          uint32_t cnt) {
-    if (lds_flows) atomicAdd(&s_flow[fid >> 1], cnt << ((fid & 1u) * 16));
+    if (kAsm && lds_flows) lds_add_asm(&s_flow[fid >> 1], cnt << ((fid & 1u) * 16));
+    else if (lds_flows) atomicAdd(&s_flow[fid >> 1], cnt << ((fid & 1u) * 16));
     else if (P.flow_mode == kFlowGlobal)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.res.flow_counts + fid), (unsigned long long)cnt);
 }
-#ifndef DK_COUNT_MERGED
-#define DK_COUNT_MERGED 0  // 1: delivered verdicts counted by popcount, the other verdicts in the lanes' one flow add
-#endif
+template <bool kAsm = false>
 __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32_t lane, uint32_t v, uint32_t fid,
                                             bool lds_flows, uint32_t* s_flow, uint32_t* s_vh) {
     const bool dl = live && (v == DK_V_OK_TCP || v == DK_V_OK_UDP);
@@ -1115,33 +1122,19 @@ __device__ __forceinline__ void count_chunk(const RxParams& P, bool live, uint32
         const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
         const uint32_t f0 = __builtin_amdgcn_readlane(fid, leader);
         const uint64_t m = __ballot(fid == f0) & todo;
-        if (lane == leader) flow_add(P, lds_flows, s_flow, opaque_v(f0), opaque_v((uint32_t)__popcll(m)));
+        if (lane == leader) flow_add<kAsm>(P, lds_flows, s_flow, opaque_v(f0), opaque_v((uint32_t)__popcll(m)));
         todo &= ~m;
         if (__popcll(m) < kFlowAggMin) break;
     }
-    if (DK_COUNT_MERGED && lds_flows) {
-        // One LDS add per lane for what is left: its flow (delivered, not aggregated above) or, for a frame that was
-        // not delivered, its verdict; the two delivered verdicts are counted by popcount (lane 0, <= 2 adds).
-        const bool vc = P.res.verdict_counts != nullptr;
-        if (vc) {
-            const uint64_t mt = __ballot(live && v == DK_V_OK_TCP), mu = __ballot(live && v == DK_V_OK_UDP);
-            if (lane == 0) {
-                if (mt) atomicAdd(&s_vh[opaque_v(DK_V_OK_TCP)], opaque_v((uint32_t)__popcll(mt)));
-                if (mu) atomicAdd(&s_vh[opaque_v(DK_V_OK_UDP)], opaque_v((uint32_t)__popcll(mu)));
-            }
-        }
-        const bool fl = (todo >> lane) & 1u;
-        if (fl || (vc && live && !dl)) atomicAdd(fl ? &s_flow[fid >> 1] : &s_vh[v], fl ? 1u << ((fid & 1u) * 16) : 1u);
-        return;
-    }
-    if ((todo >> lane) & 1u) flow_add(P, lds_flows, s_flow, fid, 1u);
+    if ((todo >> lane) & 1u) flow_add<kAsm>(P, lds_flows, s_flow, fid, 1u);
     if (P.res.verdict_counts) {
         uint64_t todo = __ballot(live);
         while (todo) {
             const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
             const uint32_t v0 = __builtin_amdgcn_readlane(v, leader);
             const uint64_t m = __ballot(live && v == v0);
-            if (lane == leader) atomicAdd(&s_vh[opaque_v(v0)], opaque_v((uint32_t)__popcll(m)));
+            if (kAsm && lane == leader) lds_add_asm(&s_vh[v0], (uint32_t)__popcll(m));
+            else if (lane == leader) atomicAdd(&s_vh[opaque_v(v0)], opaque_v((uint32_t)__popcll(m)));
             todo &= ~m;
         }
     }
@@ -1583,6 +1576,9 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
 #ifndef DK_SMALL_LATE_BARRIER
 #define DK_SMALL_LATE_BARRIER 0
 #endif
+#ifndef DK_SMALL_PIPE
+#define DK_SMALL_PIPE 1  // the next window's DMA in flight through a chunk's stores and counts (round 6)
+#endif
 // A workgroup barrier that orders LDS only (no wait for the wave's outstanding global loads and stores).
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1596,9 +1592,15 @@ __device__ __forceinline__ bool small_fast_eligible(const FrameDesc<kShift>& F, 
     const bool topt = R.b8(23) == 6u && (R.b8(46) >> 4) > 5u;
     return F.vec && !F.big && len >= 34 && ihl5 && !arp && !topt;
 }
-template <bool kOpt, bool kUb>
+struct NoMid {
+    __device__ __forceinline__ void operator()() const {}
+};
+// mid(): called between the verdicts (every socket-table load waited for) and the result stores: the pipelined loop
+// issues the next window's DMA there. (Issued right after the table load, the compiler waited for the DMA with it:
+// it counts LDS-DMA and loads as events that may complete out of order, so only vmcnt(0) covers the table load.)
+template <bool kOpt, bool kUb, class Mid = NoMid>
 __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool live, uint32_t lane, const RegAcc& R,
-                                           uint32_t len, uint32_t& v_out, uint32_t& fid_out) {
+                                           uint32_t len, uint32_t& v_out, uint32_t& fid_out, const Mid& mid = Mid()) {
     Lane L;
     parse_fast(R, len, P, L);
     if (!live) {
@@ -1658,6 +1660,7 @@ __device__ __forceinline__ void small_fast(const RxParams& P, uint32_t i, bool l
         }
     }
     const uint32_t v = L.v;
+    mid();
     if (live) {
         const bool full = v <= DK_V_ICMP || v == DK_V_TCP_NOSOCK || v == DK_V_UDP_NOSOCK;
         const bool is_tcp = v == DK_V_OK_TCP || v == DK_V_TCP_NOSOCK;
@@ -1742,6 +1745,33 @@ __global__ __launch_bounds__(SmallShape<kUb>::kBlock, DK_MIN_WAVES_SMALL) void d
     // wave-uniform: bit k set = chunk k (< 64) stored its deferral mask; chunks from 64 on always store theirs
     uint64_t had = 0;
     DK_ACC_DECL;
+    // kPipe (no LDS bind table; its general-pass granules share the window's LDS): chunk k + 1's window DMA is issued
+    // inside chunk k, once k's verdicts are decided (its socket-table loads waited for), and is in flight through k's
+    // result stores, counts and the loop's turn; chunk k + 3's descriptors come by LDS-DMA into
+    // the wave's general-pass granule slots with it (registers holding a load in flight would be waited for at the
+    // loop's turn) and are read out at the top of chunk k + 1. The counts' LDS adds are inline asm: a compiler-visible
+    // LDS atomic would first wait for the pending DMA.
+    constexpr bool kPipe = DK_SMALL_PIPE != 0 && !kUb;
+    WinPlan pl{false, 0};
+    uint32_t* const dsc = reinterpret_cast<uint32_t*>(&W.tail[0]);  // [0, 64): offsets; [64, 97): length dwords
+    // Chunk j's descriptors into dsc: 64 offsets, and the 33 dwords covering its 64 lengths from the 4-byte boundary
+    // below &len[j] (the length array is only 2-byte aligned); every load stays inside a dword that holds an element.
+    const auto desc_dma = [&](uint32_t cj, uint32_t limj, uint32_t ln) {
+        const uint32_t o = min(cj + ln, limj - 1);
+        __builtin_amdgcn_global_load_lds(P.off + o, (lds_void*)dsc, 4, 0, 0);
+        if (ln < 33) {
+            const uintptr_t lb = reinterpret_cast<uintptr_t>(P.len + cj) & ~(uintptr_t)3;
+            const uintptr_t hi = (reinterpret_cast<uintptr_t>(P.len + limj) - 1) & ~(uintptr_t)3;
+            const uintptr_t la = min(lb + 4 * (uintptr_t)ln, hi);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(la), (lds_void*)(dsc + 64), 4, 0, 0);
+        }
+    };
+    if (kPipe && have) {
+        const uint32_t ln = lane_id();
+        pl = small_window_issue(F, B, off, len, c + ln < lim, ln, W);
+        uint32_t c2p, lim2p;
+        if (have1 && r.chunk(2, c2p, lim2p)) desc_dma(c2p, lim2p, ln);
+    }
     for (uint32_t k = 0; have; k++) {
         DK_ACC_BEGIN();
         // the lane id re-materialised per chunk (as in dk_rx_kernel): lane-derived constants are not held in VGPRs
@@ -1753,7 +1783,7 @@ __global__ __launch_bounds__(SmallShape<kUb>::kBlock, DK_MIN_WAVES_SMALL) void d
         const bool live = i < lim;
         const bool have2 = have1 && r.chunk(k + 2, c2, lim2);
         uint32_t off2 = 0, len2 = 0;
-        if (have2 && c2 + lane < lim2) {  // descriptors two chunks ahead, before this chunk's window DMA
+        if (!kPipe && have2 && c2 + lane < lim2) {  // descriptors two chunks ahead, before this chunk's window DMA
             off2 = P.off[c2 + lane];
             len2 = P.len[c2 + lane];
         }
@@ -1761,7 +1791,17 @@ __global__ __launch_bounds__(SmallShape<kUb>::kBlock, DK_MIN_WAVES_SMALL) void d
         uint32_t v, fid;
         if (k == 0) DK_STAMP(1);
         DK_MARK(s_window);
-        small_window_read(small_window_issue(F, B, off, len, live, lane, W), F, B, off, W, C.R);
+        if (!kPipe) pl = small_window_issue(F, B, off, len, live, lane, W);
+        small_window_read(pl, F, B, off, W, C.R);  // waits for every load and store in flight (vmcnt 0)
+        if (kPipe && have2) {  // chunk k + 2's descriptors, DMA'd during chunk k - 1 (or before the loop)
+            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(P.len + c2) & 3u) + 2 * lane;
+            const uint32_t o2 = dsc[lane], l2 = (dsc[64 + (sh >> 2)] >> ((sh & 3u) * 8)) & 0xFFFFu;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before chunk k + 3's DMA reuses the slots
+            if (c2 + lane < lim2) {
+                off2 = o2;
+                len2 = l2;
+            }
+        }
         if (k < 3) DK_STAMP(2 + 3 * k);
         DK_MARK(s_eligible);
         DK_ACC_SPLIT(0);
@@ -1773,12 +1813,22 @@ __global__ __launch_bounds__(SmallShape<kUb>::kBlock, DK_MIN_WAVES_SMALL) void d
         const uint64_t dm = __ballot(live && !take);
         deferred = deferred || dm != 0;
         DK_MARK(s_fast);
-        small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid);
+        if (kPipe) {
+            const auto mid = [&]() {
+                uint32_t c3, lim3;
+                if (have2 && r.chunk(k + 3, c3, lim3)) desc_dma(c3, lim3, lane);
+                if (have1) pl = small_window_issue(F1, B, off1, len1, c1 + lane < lim1, lane, W);
+                asm volatile("" ::: "memory");  // issued here, not sunk to the loop's end (the compiler did)
+            };
+            small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid, mid);
+        } else {
+            small_fast<kOpt, kUb>(P, i, take, lane, C.R, len, v, fid);
+        }
         if (k < 3) DK_STAMP(3 + 3 * k);
         DK_ACC_SPLIT(1);
         if (kLateBarrier && k == 0) lds_barrier();  // every wave of the workgroup arrives once (below if no chunk)
         DK_MARK(s_count);
-        count_chunk(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
+        count_chunk<kPipe>(P, take, lane, v, fid, lds_flows, s_flow, s_vh);
         DK_MARK(s_loop_tail);
         if (dm != 0 || k >= 64) {  // read back by this wave after the loop
             if (lane == 0) P.defer[k * nw + gw] = dm;

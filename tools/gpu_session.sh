@@ -18,7 +18,10 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s5: GPU suite and the bench line after sampling the TCP shape count (64 blocks)
+# s6: the small-frame kernel with the next window's DMA in flight through a chunk's stores and counts (DK_SMALL_PIPE,
+# now the default): GPU suite, interleaved A/B against the previous loop, C3 sweep at the new default
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step bench 600 python bench.py
+step c3_ab 400 python tools/abtest.py --workload c3_udp64 --grids 0 --rotate 8 --defer --reps 11 --iters 20 build/variants/nopipe.so build/variants/pipe.so
+step c3r_ab 400 python tools/abtest.py --workload c3_udp64_random_ports --grids 0 --rotate 8 --defer --reps 7 --iters 20 build/variants/nopipe.so build/variants/pipe.so
+step c3_sweep 400 python tools/sweep.py --workload c3_udp64 --frames 1M,1536K,2M,3M,4M --rotate 8 --tag pipe
 echo done
