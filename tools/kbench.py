@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--probe-one", action="store_true", help="one probe config (mode 1, grid 1024): PMC calibration")
     ap.add_argument("--no-rx", action="store_true")
     ap.add_argument("--tx", action="store_true", help="also time dk_tx_checksum (rewrites the batch's checksums)")
+    ap.add_argument("--tx-fields", action="store_true",
+                    help="also time dk_tx_checksum_fields (the checksum pair returned, frames untouched)")
     ap.add_argument("--no-counts", action="store_true", help="pass NULL flow/verdict counters (cost attribution)")
     ap.add_argument("--modes", default="3,4,6,7,8")
     ap.add_argument("--grids", default="256,512,768,1024")
@@ -79,6 +81,13 @@ def main():
         t = time_events(lambda: eng.tx_checksum(batch), args.iters)
         algo = fb + batch.n * (bench.DESC_BYTES + 4)
         print(json.dumps({"kernel": "dk_tx", "workload": args.workload, "frames": batch.n, "frame_bytes": fb,
+                          "algo_bytes": algo, "ms": round(t * 1e3, 4), "frame_GBps": round(fb / t / 1e9, 1),
+                          "algo_GBps": round(algo / t / 1e9, 1)}), flush=True)
+    if args.tx_fields:
+        fields = torch.empty(batch.n, dtype=torch.int32, device=batch.off.device)
+        t = time_events(lambda: eng.tx_checksum_fields(batch, fields), args.iters)
+        algo = fb + batch.n * (bench.DESC_BYTES + 4)
+        print(json.dumps({"kernel": "dk_tx_fields", "workload": args.workload, "frames": batch.n, "frame_bytes": fb,
                           "algo_bytes": algo, "ms": round(t * 1e3, 4), "frame_GBps": round(fb / t / 1e9, 1),
                           "algo_GBps": round(algo / t / 1e9, 1)}), flush=True)
     if args.probe or args.probe_one:

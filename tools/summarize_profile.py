@@ -40,7 +40,7 @@ def kbench_info(path):
             rx = d
         elif d.get("kernel") == "read_probe":
             probe = d
-        elif d.get("kernel") == "dk_tx":
+        elif d.get("kernel") in ("dk_tx", "dk_tx_fields"):
             tx = d
     return rx, probe, tx
 
@@ -53,7 +53,7 @@ def main():
     stats = os.path.join(src, "bench", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
-    for sub in ("c3", "tx", "c1"):
+    for sub in ("c3", "tx", "txf", "c1"):
         st = os.path.join(src, sub, "run_kernel_stats.csv")
         if os.path.exists(st):
             shutil.copy(st, os.path.join(dst, f"{tag}_{sub}_kernel_stats.csv"))
@@ -67,7 +67,7 @@ def main():
     rows = [["workload", "kernel", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "calib_factor", "hbm_read_bytes",
              "hbm_write_bytes", "algo_bytes", "traffic_over_algo"]]
     for wl in ("c2_tcp1500", "c3_udp64", "c4_imix", "c5_tcp1500_10k", "c1_tcp1078", "c3_udp64_random_ports",
-               "c2_tcp1500_libos"):
+               "c2_tcp1500_libos", "c2_tcp1500_txf"):
         fdir, wdir = os.path.join(src, f"fetch_{wl}"), os.path.join(src, f"write_{wl}")
         if not os.path.exists(os.path.join(fdir, "run_counter_collection.csv")):
             continue
@@ -83,15 +83,20 @@ def main():
         rd = fk[rxk] * 1024.0 * factor
         wr = wk.get(rxk, 0.0) * 1024.0
         algo = rx["algo_bytes"]
-        traffic[wl] = {"hbm_bytes_per_launch": int(rd + wr), "hbm_read_bytes": int(rd), "hbm_write_bytes": int(wr),
-                       "kernel": rxname, "fetch_size_kb_raw": fk[rxk], "write_size_kb_raw": wk.get(rxk, 0.0),
-                       "fetch_calibration_factor": round(factor, 4), "algorithmic_bytes_per_launch": algo,
-                       "source": f"profiles/{tag}_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
+        if not wl.endswith("_txf"):  # the fields-form pass repeats c2_tcp1500's receive: only its TX kernel is new
+            traffic[wl] = {"hbm_bytes_per_launch": int(rd + wr), "hbm_read_bytes": int(rd),
+                           "hbm_write_bytes": int(wr), "kernel": rxname, "fetch_size_kb_raw": fk[rxk],
+                           "write_size_kb_raw": wk.get(rxk, 0.0), "fetch_calibration_factor": round(factor, 4),
+                           "algorithmic_bytes_per_launch": algo,
+                           "source": f"profiles/{tag}_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                                     "separate passes)"}
         rows.append([wl, rxname, f"{fk[rxk]:.0f}", f"{wk.get(rxk, 0.0):.0f}", f"{factor:.4f}", f"{rd:.0f}",
                      f"{wr:.0f}", algo, f"{(rd + wr) / algo:.3f}"])
         rows.append([wl, "read_probe", f"{fk[pk]:.0f}", f"{wk.get(pk, 0.0):.0f}", "", probe["bytes"], "", "", ""])
         txk = next((k for k in fk if "dk_tx_kernel" in k or "dk_tx_split_kernel" in k), None)
         txname = "dk_tx_split_kernel" if txk and "split" in txk else "dk_tx_kernel"
+        if tx and tx["kernel"] == "dk_tx_fields":
+            txname += "<fields>"
         if tx and txk:
             trd, twr = fk[txk] * 1024.0 * factor, wk.get(txk, 0.0) * 1024.0
             traffic[wl + "_tx"] = {"hbm_bytes_per_launch": int(trd + twr), "hbm_read_bytes": int(trd),
