@@ -1259,6 +1259,10 @@ struct TailQ {
 #ifndef DK_STAGED_PRIO
 #define DK_STAGED_PRIO 0  // > 0: a wave streaming its chunk's frames issues at this priority, phase C at 0
 #endif
+#ifndef DK_TAIL_LATE
+#define DK_TAIL_LATE 0  // 1: a tail grab is for the next round (issued after this round's stream, resolved after its
+                        // phase C, the descriptors loaded then): committed half a round ahead instead of 1.5
+#endif
 template <bool kShift, bool kStage>
 __global__ __launch_bounds__(kBlock, kStage ? DK_MIN_WAVES_STAGED : kShift ? DK_MIN_WAVES : DK_MIN_WAVES_ALIGNED)
 void dk_rx_kernel(RxParams P) {
@@ -1307,15 +1311,17 @@ void dk_rx_kernel(RxParams P) {
         const uint32_t i = c + lane;
         const bool live = i < lim;
         const uint32_t off = noff, len = nlen;
+        constexpr bool kLate = DK_TAIL_LATE != 0;
+        const bool late = kLate && k + 1 >= ks;  // wave-uniform: the next chunk comes from a grab issued this round
         if (k + 1 < ks) {
             have = r.chunk(k + 1, nc, nlim);
-        } else {  // the tail: the chunk grabbed a round ago
+        } else if (!kLate) {  // the tail: the chunk grabbed a round ago
             const uint32_t j = Q.resolve(P);
             have = j != kNoChunk;
             nc = 64 * j;
             nlim = P.n;
         }
-        if (have && nc + lane < nlim) {  // prefetch the next chunk's descriptors
+        if (!late && have && nc + lane < nlim) {  // prefetch the next chunk's descriptors
             noff = P.off[nc + lane];
             nlen = P.len[nc + lane];
         }
@@ -1331,7 +1337,7 @@ void dk_rx_kernel(RxParams P) {
         // the grab for chunk k + 2, resolved at the top of the next round: issued after the frame stream (its return
         // register would be live through the stream's load registers, the kernel's register peak); phase C covers
         // its latency
-        if (have && k + 2 >= ks) Q.issue(P, lane);
+        if (kLate ? late : have && k + 2 >= ks) Q.issue(P, lane);
         if (k < 3) DK_STAMPW(3 + 3 * k);
         DK_ACC_SPLIT(0);
         if (DK_STAGED_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -1341,7 +1347,18 @@ void dk_rx_kernel(RxParams P) {
         DK_ACC_SPLIT(1);
         // The next chunk's descriptors (loaded a chunk ago) are waited for here, before this chunk's stores: used first
         // at the top of the next chunk, after a staged flush, their wait also waited for every store's write ack.
-        asm volatile("" ::"v"(noff), "v"(nlen));
+        if (late) {  // DK_TAIL_LATE: resolve this round's grab; staging and counting cover the descriptors' latency
+            const uint32_t j = Q.resolve(P);
+            have = j != kNoChunk;
+            nc = 64 * j;
+            nlim = P.n;
+            if (have && nc + lane < nlim) {
+                noff = P.off[nc + lane];
+                nlen = P.len[nc + lane];
+            }
+        } else {
+            asm volatile("" ::"v"(noff), "v"(nlen));
+        }
         DK_MARK(stage);
         if (kStage) {  // the last kStageK chunks' results; stored when full and at exit
             stage_put(stg, rec);
@@ -1577,7 +1594,7 @@ __device__ __forceinline__ void small_big_frames(const FrameDesc<kShift>& F, uin
 #define DK_SMALL_LATE_BARRIER 0
 #endif
 #ifndef DK_SMALL_PIPE
-#define DK_SMALL_PIPE 1  // the next window's DMA in flight through a chunk's stores and counts (round 6)
+#define DK_SMALL_PIPE 0  // 1: the next window's DMA in flight through a chunk's stores and counts (round 6: +5 % on C3)
 #endif
 // A workgroup barrier that orders LDS only (no wait for the wave's outstanding global loads and stores).
 __device__ __forceinline__ void lds_barrier() {

@@ -23,5 +23,7 @@ python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_
 step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
 step c3_ab 400 python tools/abtest.py --workload c3_udp64 --grids 0 --rotate 8 --defer --reps 11 --iters 20 build/variants/nopipe.so build/variants/pipe.so
 step c3r_ab 400 python tools/abtest.py --workload c3_udp64_random_ports --grids 0 --rotate 8 --defer --reps 7 --iters 20 build/variants/nopipe.so build/variants/pipe.so
+# the staged kernel's tail grabs committed half a round ahead (DK_TAIL_LATE) against 1.5, tail slack 1-3 rounds
+step imix_tail_ab 500 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 7 --iters 10 --knob DK_RX_TAIL=1,2,3 --check build/variants/tbase.so build/variants/tlate.so
 step c3_sweep 400 python tools/sweep.py --workload c3_udp64 --frames 1M,1536K,2M,3M,4M --rotate 8 --tag pipe
 echo done
