@@ -205,8 +205,8 @@ int dk_rx_resident_blocks(uint32_t dyn_lds_bytes, uint32_t family);  // resident
 int dk_launch_rx(const dk::RxParams& p, uint32_t grid, void* stream);
 // dk_flow_reduce_kernel over rows left pending by a deferred launch (dk_rx_counts_flush and the scratch paths).
 int dk_launch_reduce(const dk::RowCombine& q, void* stream);
-uint32_t dk_rx_small_block_waves(bool ub);
+uint32_t dk_rx_small_block_waves(bool ub);  // waves per workgroup of the small-frame kernel (ub: the LDS bind table's)
 // The host pipeline under the ring's copy policy (rx_host.cpp; dk_rx_process_tpacket3).
-int dk_rx_process_ring_host(struct dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r);  // waves per workgroup of the small-frame kernel (ub: the LDS bind table's)
+int dk_rx_process_ring_host(struct dk_rx_ctx* c, const dk_rx_batch* b, const dk_rx_results* r);
 int dk_tx_resident_blocks();  // occupancy of dk_tx_kernel per CU (0 on error)
 int dk_launch_tx(const dk::TxParams& p, uint32_t grid, void* stream);

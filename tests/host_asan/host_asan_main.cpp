@@ -35,6 +35,7 @@
 // dk_rx_process_tpacket3 (ring_host.cpp) hands the scanned frames to the GPU pipeline; this host-only build never
 // reaches it (the driver exercises the scan and release entry points), so the symbol resolves to a refusal here.
 extern "C" int dk_rx_process_host(dk_rx_ctx*, const dk_rx_batch*, const dk_rx_results*, uint32_t) { return ENOSYS; }
+int dk_rx_process_ring_host(dk_rx_ctx*, const dk_rx_batch*, const dk_rx_results*) { return ENOSYS; }
 
 namespace {
 FILE* g_in;

@@ -18,12 +18,8 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s6: the small-frame kernel with the next window's DMA in flight through a chunk's stores and counts (DK_SMALL_PIPE,
-# now the default): GPU suite, interleaved A/B against the previous loop, C3 sweep at the new default
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
-step c3_ab 400 python tools/abtest.py --workload c3_udp64 --grids 0 --rotate 8 --defer --reps 11 --iters 20 build/variants/nopipe.so build/variants/pipe.so
-step c3r_ab 400 python tools/abtest.py --workload c3_udp64_random_ports --grids 0 --rotate 8 --defer --reps 7 --iters 20 build/variants/nopipe.so build/variants/pipe.so
-# the staged kernel's tail grabs committed half a round ahead (DK_TAIL_LATE) against 1.5, tail slack 1-3 rounds
-step imix_tail_ab 500 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 7 --iters 10 --knob DK_RX_TAIL=1,2,3 --check build/variants/tbase.so build/variants/tlate.so
-step c3_sweep 400 python tools/sweep.py --workload c3_udp64 --frames 1M,1536K,2M,3M,4M --rotate 8 --tag pipe
+# s7: the round's final tree: GPU suite, smoke(), the default bench line (profiles: tools/profile_bench.sh next)
+step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
+step bench 600 python bench.py
 echo done
