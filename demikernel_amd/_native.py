@@ -184,6 +184,7 @@ COMM_FUNCTIONS = [
 DIAG_FUNCTIONS = [
     ("dk_diag_read_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_int, c_void_p]),
     ("dk_diag_rw_probe", c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p]),
+    ("dk_diag_patch_probe", c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_uint32, c_void_p, c_uint32, c_void_p]),
     ("dk_diag_path_stats_enable", c_int, [c_void_p, c_int]),
     ("dk_diag_path_stats_read", c_int, [c_void_p, c_void_p]),
     ("dk_diag_rx_set_tuning", c_int, [c_void_p, c_void_p, c_uint32]),

@@ -207,7 +207,69 @@ __global__ __launch_bounds__(kBlock) void rw_probe(const uint4* __restrict__ p, 
     if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
 }
 
+// The in-place TX contract's memory pattern alone: the same 4 KiB wave-step read stream, plus one 64-byte line
+// rewritten at the head of every `stride`-byte slot (a frame's header window) by the lane whose 16-byte piece starts
+// it; `late` steps later (0: the step that read it), as the checksum is known only after the whole frame is read.
+// flags bit 0: no read stream (the rewrites alone); bit 1: two 16-bit stores at +24 and +50 (the IPv4 and TCP
+// checksum fields) instead of the 64-byte line; bit 2: the 128-byte line instead.
+__global__ __launch_bounds__(kBlock) void patch_probe(uint4* __restrict__ p, uint64_t n16, uint32_t stride16,
+                                                      uint32_t late, uint32_t flags, uint32_t* out) {
+    uint32_t acc = 0;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0xFFFFFFFF, 0x00020000);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (uint64_t base = w * 256; base < n16; base += nwaves * 256) {
+        uint32_t x = (uint32_t)base;
+        if (!(flags & 1)) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint64_t i = min(base + 64 * k + lane, n16 - 1);
+                const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 2);
+                v[k] = make_uint4(r[0], r[1], r[2], r[3]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) x ^= v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        acc += x;
+        const uint64_t wb = base - (uint64_t)late * nwaves * 256;  // the step whose heads this one rewrites
+        if (stride16 && base >= (uint64_t)late * nwaves * 256)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint64_t i = wb + 64 * k + lane;
+                if (i % stride16 == 0 && i + 8 <= n16) {
+                    if (flags & 4) {  // the 128-byte line (the L2 line of gfx950)
+                        u32x4* q = reinterpret_cast<u32x4*>(p + i);
+#pragma unroll
+                        for (int j = 0; j < 8; j++) q[j] = u32x4{x, x + 1, x + 2, x + j};
+                    } else if (flags & 2) {
+                        uint16_t* h = reinterpret_cast<uint16_t*>(p + i);
+                        h[12] = (uint16_t)x;
+                        h[25] = (uint16_t)(x >> 16);
+                    } else {
+                        u32x4* q = reinterpret_cast<u32x4*>(p + i);
+#pragma unroll
+                        for (int j = 0; j < 4; j++) q[j] = u32x4{x, x + 1, x + 2, x + j};
+                    }
+                }
+            }
+    }
+    acc = __reduce_add_sync(~0ull, acc);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + blockIdx.x, acc);
+}
+
 }  // namespace
+
+extern "C" int dk_diag_patch_probe(void* buf, uint64_t bytes, uint32_t stride, uint32_t late, uint32_t flags,
+                                   uint32_t* scratch, uint32_t grid, void* stream) {
+    if (!buf || !scratch || grid == 0 || stride % 64 || bytes % 64 || bytes > 0xFFFFFFFFull || flags > 7) return 22;
+    if ((flags & 4) && stride % 128) return 22;
+    hipLaunchKernelGGL(patch_probe, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (uint4*)buf, bytes / 16,
+                       stride / 16, late, flags, scratch);
+    return hipGetLastError() == hipSuccess ? 0 : 5;
+}
 
 extern "C" int dk_diag_rw_probe(const void* buf, uint64_t bytes, uint32_t* dst, uint32_t nres, uint32_t* scratch,
                                 uint32_t grid, void* stream) {

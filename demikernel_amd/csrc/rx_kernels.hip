@@ -1904,6 +1904,15 @@ __global__ __launch_bounds__(SmallShape<kUb>::kBlock, DK_MIN_WAVES_SMALL) void d
 
 // A wave's chunks with their descriptors loaded one chunk ahead: D.off / D.len belong to chunk D.c (0 outside the
 // batch); next() starts the loads of the following chunk.
+// A global pointer in address space 1: where the compiler cannot prove a parameter's pointer global (TxParams in the
+// split TX kernel) it emits flat loads and stores, which count in lgkmcnt too, so every LDS wait after them (the split
+// kernels' hand-off spins and releases) also waits for the memory access: a descriptor prefetch or a window rewrite
+// then stalls the hand-off for a full memory round trip.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+    return (__attribute__((address_space(1))) T*)(p);
+}
+
 struct DescAhead {
     uint32_t c, lim, off, len;
     bool have;
@@ -1912,8 +1921,8 @@ struct DescAhead {
         have = r.chunk(p0, c, lim);
         off = len = 0;
         if (have && c + r.lane_off < lim) {
-            off = P.off[c + r.lane_off];
-            len = P.len[c + r.lane_off];
+            off = gptr(P.off)[c + r.lane_off];
+            len = gptr(P.len)[c + r.lane_off];
         }
     }
     template <class PT>
@@ -1921,8 +1930,8 @@ struct DescAhead {
         have = r.chunk(p, c, lim);
         off = len = 0;
         if (have && c + r.lane_off < lim) {
-            off = P.off[c + r.lane_off];
-            len = P.len[c + r.lane_off];
+            off = gptr(P.off)[c + r.lane_off];
+            len = gptr(P.len)[c + r.lane_off];
         }
     }
 };
@@ -2178,7 +2187,7 @@ __global__ __launch_bounds__(kBlock) void dk_flow_reduce_kernel(const uint32_t* 
 // partial-write merge below L2 (16-bit stores, nontemporal 16-bit stores and 16-byte block rewrites measured slower,
 // round 1-2, profiles/HISTORY.md).
 __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
-    *reinterpret_cast<uint16_t*>(p) = (uint16_t)bswap16(v);
+    *gptr(reinterpret_cast<uint16_t*>(p)) = (uint16_t)bswap16(v);
 }
 
 // The checksum pair of dk_tx_checksum_fields (dk_rx.h): IPv4 | L4 << 16, DK_TX_NOT_WRITTEN for a half not filled.
@@ -2229,6 +2238,9 @@ __device__ __noinline__ uint32_t tx_slow(uint8_t* f, uint32_t len) {
     return tx_pair(ipc, true, c);
 }
 
+#ifndef DK_TX_LINE128
+#define DK_TX_LINE128 0  // 1: frames of >= 128 bytes on a 128-byte boundary rewrite their whole first 128-byte line
+#endif
 // A frame's rewritten 64-byte header window, held in registers by the split TX kernel's finish waves until a burst.
 constexpr uint32_t kNoWin = 0xFFFFFFFFu;
 struct TxWin {
@@ -2243,19 +2255,19 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
                                           uint32_t len, const Chunk& C, TxWin& win, uint32_t i = 0, bool live = false) {
     win.off = kNoWin;
     if (!C.inb) {
-        if (kFields && live) __builtin_nontemporal_store(kTxNone, P.fields + i);
+        if (kFields && live) __builtin_nontemporal_store(kTxNone, gptr(P.fields) + i);
         return;
     }
     uint8_t* f = P.frames + off;
     const RegAcc& R = C.R;
     if (!(C.vec && len >= 34 && ((R.w[3] >> 16) & 0x0Fu) == 5u)) {
         const uint32_t pr = tx_slow<kFields>(f, len);
-        if (kFields) __builtin_nontemporal_store(pr, P.fields + i);
+        if (kFields) __builtin_nontemporal_store(pr, gptr(P.fields) + i);
         return;
     }
     const uint32_t tot = R.be16(16);
     if (R.be16(12) != 0x0800u || 14 + tot > len || tot < 20) {
-        if (kFields) __builtin_nontemporal_store(kTxNone, P.fields + i);
+        if (kFields) __builtin_nontemporal_store(kTxNone, gptr(P.fields) + i);
         return;
     }
     const uint32_t hsum = R.le16(14) + R.le16(16) + R.le16(18) + R.le16(20) + R.le16(22) + R.le16(26) + R.le16(28) +
@@ -2275,7 +2287,7 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
         c = csum_from_residue(mod_ffff(be_residue(s) + pseudo));
     }
     if (kFields) {
-        __builtin_nontemporal_store(tx_pair(ipc, l4, c), P.fields + i);
+        __builtin_nontemporal_store(tx_pair(ipc, l4, c), gptr(P.fields) + i);
         return;
     }
     if (len >= 64 && C.sh == 0) {  // rewrite the whole 64-byte header window: full-line writes, no partial-write merge below L2
@@ -2291,9 +2303,22 @@ __device__ __forceinline__ void tx_finish(const TxParams& P, uint32_t lane, cons
             win.off = off;
             return;
         }
-        uint4* q = reinterpret_cast<uint4*>(f);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const auto q = gptr(reinterpret_cast<u32x4*>(f));
+        if (DK_TX_LINE128 && len >= 128 && (reinterpret_cast<uintptr_t>(f) & 127u) == 0) {
+            // the frame's whole first 128-byte line (the L2 line): bytes [64, 128) read back (an L2 hit: kHdrT loads
+            // them temporally) so the line goes out whole
+            u32x4 e[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) q[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+            for (int k = 0; k < 4; k++) e[k] = q[4 + k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) q[k] = u32x4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+#pragma unroll
+            for (int k = 0; k < 4; k++) q[4 + k] = e[k];
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) q[k] = u32x4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
         return;
     }
     store_be16(f + 24, ipc);

@@ -25,6 +25,15 @@ int dk_diag_read_probe(const void* buf, uint64_t bytes, uint32_t* scratch, uint3
 int dk_diag_rw_probe(const void* buf, uint64_t bytes, uint32_t* dst, uint32_t nres, uint32_t* scratch, uint32_t grid,
                      void* stream);
 
+/* The in-place TX checksum fill's memory pattern alone: the rw probe's read stream over `bytes` (< 4 GiB, multiple of
+ * 64) plus one 64-byte line rewritten in place at the start of every `stride`-byte slot (multiple of 64; 0: none),
+ * `late` wave-step rounds after it was read. flags bit 0: no read stream (the rewrites alone); bit 1: two 16-bit
+ * stores at +24 and +50 (the IPv4 and TCP checksum fields) instead of the line; bit 2: the whole 128-byte line
+ * (stride a multiple of 128). Overwrites the buffer. The ceiling
+ * dk_tx_checksum is compared with. Async. */
+int dk_diag_patch_probe(void* buf, uint64_t bytes, uint32_t stride, uint32_t late, uint32_t flags, uint32_t* scratch,
+                        uint32_t grid, void* stream);
+
 /* Per-path frame counters of a receive context (off by default). Paths: [0] vector path, frame <= 64 B in registers;
  * [1] vector path, frame streamed by a quarter-wave; [2] streamed but the L4 segment re-summed in-lane (IPv4
  * total_length far below the frame length); [3] per-lane byte-load path (unaligned frame, IHL != 5, or a frame too

@@ -18,8 +18,10 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s7: the round's final tree: GPU suite, smoke(), the default bench line (profiles: tools/profile_bench.sh next)
-step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
-step bench 600 python bench.py
+# s11: 128-byte line rewrites in the probe (flags 4, 5); the TX kernels rewriting a frame's whole first 128-byte line
+# (DK_TX_LINE128, in-tree default for this session): GPU suite, interleaved A/B against the 64-byte rewrite
+step patch_probe 400 python tools/patch_probe.py --lates 0 --flags 0,1,4,5 --grids 1024,2048
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step tx_ab 400 python tools/abtest.py --workload c2_tcp1500 --grids 0 --tx --reps 11 --iters 20 build/variants/tx64.so build/variants/tx128.so
+step tx_bench 300 python tools/kbench.py --workload c2_tcp1500 --iters 20 --no-rx --tx --tx-fields
 echo done
