@@ -74,8 +74,8 @@ struct Params {
     uint32_t* cls;     // [n]: the connection of a segment classified in the key kernel (never walked), else kNoConn
     uint32_t* open_until;  // [nconns]: frames of the connection from this index on come after its close
     // the scan walk's per-window scratch (window v of connection c at ws = range[2c] / 64 + c + v: disjoint per c)
-    uint4* scan_sum;   // [ws]: {A, U, window maximum, A2} against the connection's state at the call's start (decided
-                       // iff A <= R <= U or R >= A2)
+    uint4* scan_sum;   // [3 ws]: {A, U, window maximum, A2} against the connection's state at the call's start (decided
+                       // iff A <= R <= U or R >= A2); {n0, lo, e0, e1}, {e2, e3}: the count summary (pre kernel)
     int* scan_ends;    // [ws][lane]: each lane's candidate end if it delivers at R below it, else INT_MIN
     uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
     uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
@@ -1095,7 +1095,17 @@ struct ConnHead {
 };
 __device__ __forceinline__ uint32_t scan_ws(const Params& P, uint32_t c) { return P.range[2 * c] / kWave + c; }
 
+#ifndef DK_TCP_SCAN_STATS
+#define DK_TCP_SCAN_STATS 0  // diagnostics build: the scan kernel prints its per-connection step counts
+#endif
 constexpr uint32_t kScanBlock = 256, kScanWaves = kScanBlock / kWave;
+#ifndef DK_TCP_SCAN_DEPTH
+#define DK_TCP_SCAN_DEPTH 8
+#endif
+constexpr uint32_t kScanDepth = DK_TCP_SCAN_DEPTH;  // summary batches of 64 windows the scan kernel keeps in flight
+constexpr uint32_t kScanSum = 3;  // uint4 per window in scan_sum: thresholds, then the delivery-count summary
+constexpr uint32_t kScanLow = 4;  // smallest delivering ends a window's count summary carries
+constexpr uint32_t kScanPost = 1024;  // decided windows' post records the scan kernel gathers in LDS per burst
 // windows the scan kernel walks in the rings after two undecided in a row: kScanRingRun, doubled while that repeats
 // (up to kScanRingRunMax), back to kScanRingRun once the scan took more than a batch again
 constexpr uint32_t kScanRingRun = 8, kScanRingRunMax = 512;
@@ -1154,7 +1164,26 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
         const int E = pr.synd ? er + 1 : dr;
         const bool deliv0 = (pr.cand || pr.synd) && pmi < E;
         P.scan_ends[(size_t)(ws0 + v) * kWave + lane] = deliv0 ? E : INT_MIN;
-        if (lane == 0) P.scan_sum[ws0 + v] = make_uint4((uint32_t)A, (uint32_t)Umin, pr.wmax, (uint32_t)A2);
+        // the count summary: n0 delivering lanes, their kScanLow smallest ends ascending and the next one (lo): at any
+        // R below lo the window delivers n0 less those of the smallest ends at or below R (a retransmission's end
+        // sits below the R its window starts at: the in-order stream's usual outlier)
+        int e = deliv0 ? E : INT_MAX, low[kScanLow + 1];
+#pragma unroll
+        for (uint32_t k = 0; k <= kScanLow; k++) {
+            uint32_t mm;  // the wave's minimum by a DPP scan (a shuffle tree is an LDS round trip per level)
+            WaveScan().inclusive_scan((uint32_t)e ^ 0x80000000u, mm, scan_tmp[wv], rocprim::minimum<uint32_t>());
+            const int m = (int)((uint32_t)__builtin_amdgcn_readlane(mm, kWave - 1) ^ 0x80000000u);
+            low[k] = m;
+            const uint64_t hit = __ballot(e == m && m != INT_MAX);
+            if (hit && lane == (uint32_t)__builtin_ctzll(hit)) e = INT_MAX;
+        }
+        const uint32_t n0 = (uint32_t)__popcll(__ballot(deliv0));
+        if (lane == 0) {
+            uint4* sw = P.scan_sum + kScanSum * (size_t)(ws0 + v);
+            sw[0] = make_uint4((uint32_t)A, (uint32_t)Umin, pr.wmax, (uint32_t)A2);
+            sw[1] = make_uint4(n0, (uint32_t)low[kScanLow], (uint32_t)low[0], (uint32_t)low[1]);
+            sw[2] = make_uint4((uint32_t)low[2], (uint32_t)low[3], 0u, 0u);
+        }
     }
 }
 
@@ -1162,6 +1191,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
     __shared__ WaveScan::storage_type scan_tmp[1];
     __shared__ uint32_t sidx[kIdxSlots][kWave];
     __shared__ uint4 srec[kRecSlots][kWave];
+    __shared__ uint4 spost[kScanPost];
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     dk_tcp_conn* t = P.conns + c;
     const ConnHead h(t);
@@ -1188,48 +1218,84 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
     uint32_t n = 0, open_until = h.state == DK_TCP_ESTABLISHED ? 0xFFFFFFFFu : 0u;
     const bool transparent = h.state == DK_TCP_ESTABLISHED && h.nooo < DK_TCP_OOO_MAX;
     bool stale = !transparent;  // the precomputed windows no longer describe the state
-    // lane k of a batch at v: window v + k's summary and its 64 lanes' ends (unconditional loads, clamped to the last
-    // window; a lane past it fails the check)
+    // lane k of a batch at v: window v + k's two summaries (unconditional loads, clamped to the last window; a lane past
+    // it fails the check). Its 64 lanes' ends are read only when R reaches the smallest of them (cx.y).
     struct Batch {
-        uint4 sm;
-        int4 ends[kWave / 4];
+        uint4 sm, c1, c2;
     };
     const auto load_batch = [&](uint32_t v0, Batch& b) {
-        const uint32_t wk = ws0 + min(v0 + lane, nwin - 1);
-        b.sm = P.scan_sum[wk];
-        const int4* er = reinterpret_cast<const int4*>(P.scan_ends + (size_t)wk * kWave);
-#pragma unroll
-        for (uint32_t m = 0; m < kWave / 4; m++) b.ends[m] = er[m];
+        const uint4* sw = P.scan_sum + kScanSum * (size_t)(ws0 + min(v0 + lane, nwin - 1));
+        b.sm = sw[0];
+        b.c1 = sw[1];
+        b.c2 = sw[2];
     };
     uint32_t v = 0;
+#if DK_TCP_SCAN_STATS
+    uint32_t st_batch = 0, st_full = 0, st_slow = 0, st_ring = 0, st_runs = 0, st_restart = 0;
+    uint64_t ck_batch = 0, ck_slow = 0, ck_ring = 0, ck_t0 = wall_clock64(), ck_a;
+#endif
+    // One batch at v from b (loaded for v): the decided windows' R and deliveries; returns how many windows it took
+    // (64: all; fewer: window v + f is undecided, or the connection ends).
+    // The decided windows' post records ({R, deliveries before it, 1}) gather in LDS (spost, windows vflush ..) and go
+    // out in bursts: a global store pending while the next batches' loads are in flight makes every later wait a full
+    // vmcnt(0) (loads and stores complete out of order), which would expose the prefetch's latency at every step.
+    uint32_t vflush = 0;
+    const auto flush_post = [&]() {
+        for (uint32_t u = lane; u < v - vflush; u += kWave) P.scan_post[ws0 + vflush + u] = spost[u];
+        vflush = v;
+    };
     // One batch at v from b (loaded for v): the decided windows' R and deliveries; returns how many windows it took
     // (64: all; fewer: window v + f is undecided, or the connection ends).
     const auto batch_step = [&](const Batch& b) -> uint32_t {
+#if DK_TCP_SCAN_STATS
+        ck_a = wall_clock64();
+#endif
         const uint32_t R0 = w.rn - h.rn0;
         const bool have = v + lane < nwin;
         uint32_t wx;
         WaveScan().exclusive_scan(b.sm.z, wx, 0u, scan_tmp[0], rocprim::maximum<uint32_t>());
         const uint32_t Rk = max(R0, wx);
-        const bool ok = have && (((int)Rk >= (int)b.sm.x && (int)Rk <= (int)b.sm.y) || (int)Rk >= (int)b.sm.w);
-        const uint64_t bad = __ballot(!ok);
+        const int R = (int)Rk;
+        // every test on the batch unconditional (bitwise, no short circuit): a load used only under a branch is sunk
+        // into it by the compiler and issued there, a full round trip at every step
+        const bool dec = ((R >= (int)b.sm.x) & (R <= (int)b.sm.y)) | (R >= (int)b.sm.w);
+        const uint64_t bad = __ballot(!(have & dec));
         const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : kWave;
-        uint32_t cntk = 0;
+        // below lo: n0 less the smallest ends at or below R
+        const uint32_t fast = b.c1.x - (R >= (int)b.c1.z ? 1u : 0u) - (R >= (int)b.c1.w ? 1u : 0u) -
+                              (R >= (int)b.c2.x ? 1u : 0u) - (R >= (int)b.c2.y ? 1u : 0u);
+        const bool exact = (lane < f) & (R >= (int)b.c1.y);
+        uint32_t cntk = lane < f ? fast : 0u;
+        if (exact) {  // count the window's ends above R
+            const int4* er = reinterpret_cast<const int4*>(P.scan_ends + (size_t)(ws0 + v + lane) * kWave);
+            cntk = 0;
 #pragma unroll
-        for (uint32_t m = 0; m < kWave / 4; m++)
-            cntk += ((int)Rk < b.ends[m].x ? 1u : 0u) + ((int)Rk < b.ends[m].y ? 1u : 0u) +
-                    ((int)Rk < b.ends[m].z ? 1u : 0u) + ((int)Rk < b.ends[m].w ? 1u : 0u);
+            for (uint32_t m = 0; m < kWave / 4; m++) {
+                const int4 e = er[m];
+                cntk += (R < e.x ? 1u : 0u) + (R < e.y ? 1u : 0u) + (R < e.z ? 1u : 0u) + (R < e.w ? 1u : 0u);
+            }
+        }
         uint32_t nx;
         WaveScan().exclusive_scan(cntk, nx, 0u, scan_tmp[0], rocprim::plus<uint32_t>());
-        if (lane < f) P.scan_post[ws0 + v + lane] = make_uint4(Rk, n + nx, 1u, 0u);
+        if (lane < f) spost[v - vflush + lane] = make_uint4(Rk, n + nx, 1u, 0u);
         if (f > 0) {
             w.rn = h.rn0 + (uint32_t)__builtin_amdgcn_readlane(max(Rk, b.sm.z), f - 1);
             n += (uint32_t)__builtin_amdgcn_readlane(nx + cntk, f - 1);
         }
         v += f;
+#if DK_TCP_SCAN_STATS
+        st_batch++;
+        st_full += f == kWave;
+        ck_batch += wall_clock64() - ck_a;
+#endif
         return f;
     };
     // window v is not decided by the thresholds: the relay's slow path on the walk's state
     const auto slow_window = [&]() {
+#if DK_TCP_SCAN_STATS
+        st_slow++;
+        const uint64_t ck_s = wall_clock64();
+#endif
         if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t base = v * kWave, lim = min(cnt - base, kWave), i = idx(v);
         const uint4 g = P.rec[i];
@@ -1272,9 +1338,17 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
             open_until = W.open_until;
         }
         v++;
+#if DK_TCP_SCAN_STATS
+        ck_slow += wall_clock64() - ck_s;
+#endif
     };
     // windows v .. v1 - 1 as the wave walk does (the LDS rings)
     const auto ring_run = [&](uint32_t v1) {
+#if DK_TCP_SCAN_STATS
+        st_ring += v1 - v;
+        st_runs++;
+        const uint64_t ck_r = wall_clock64();
+#endif
         for (uint32_t u = v + lane; u < v1; u += kWave) P.scan_post[ws0 + u] = make_uint4(0u, 0u, 0u, 0u);
         WaveWalk W{P, w, s, Out{dv, n, cap}, open_until, h.wend, cnt, lane, scan_tmp[0]};
         ring_walk(P, W, sidx, srec, k0, cnt, v, v1);
@@ -1283,23 +1357,31 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         n = W.o.n;
         open_until = W.open_until;
         v = v1;
+#if DK_TCP_SCAN_STATS
+        ck_ring += wall_clock64() - ck_r;
+#endif
     };
-    // Three batches in flight (b0, b1, b2 for v, v + 64, v + 128), each reloaded 128 windows ahead once used: no
-    // register copies, so no wait for a batch before its turn.
-    Batch b0, b1, b2;
+    // Super-rounds of kScanDepth batches (b[j] for v + 64 j, 48 bytes per lane each) loaded together and then stepped
+    // through: one load latency per kScanDepth steps. (Reloading each batch kScanDepth - 1 ahead as it is used keeps
+    // loads in flight across the loop's back edge, where the compiler's waits fall back to vmcnt(0) and expose a
+    // reload's latency every other step.)
+    Batch b[kScanDepth];
     uint32_t last_slow = 0xFFFFFFFEu, run = kScanRingRun;  // the last window the slow path took, the next ring run
     while (v < nwin && !stale) {
-        load_batch(v, b0);
-        load_batch(v + kWave, b1);
-        load_batch(v + 2 * kWave, b2);
-        for (;;) {
-            if (batch_step(b0) < kWave) break;
-            load_batch(v + 2 * kWave, b0);
-            if (batch_step(b1) < kWave) break;
-            load_batch(v + 2 * kWave, b1);
-            if (batch_step(b2) < kWave) break;
-            load_batch(v + 2 * kWave, b2);
+#if DK_TCP_SCAN_STATS
+        st_restart++;
+#endif
+        bool more = true;
+        while (more && v < nwin) {
+            if (v + kScanDepth * kWave > vflush + kScanPost) flush_post();  // room for this round's records
+#pragma unroll
+            for (uint32_t j = 0; j < kScanDepth; j++)
+                if (v + j * kWave < nwin) load_batch(v + j * kWave, b[j]);  // (wave-uniform: no loads past the end)
+#pragma unroll
+            for (uint32_t j = 0; j < kScanDepth; j++)
+                if (more && batch_step(b[j]) < kWave) more = false;
         }
+        flush_post();  // before the slow path's and the rings' own stores
         if (v >= nwin) break;
         if (v == last_slow + 1) {  // two undecided windows in a row (reordering): the next ones in the rings
             ring_run(v + min(run, nwin - v));
@@ -1310,11 +1392,21 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
             last_slow = v;
             slow_window();
         }
+        vflush = v;
         const uint32_t front = w.nooo ? s.start(0) : 0u;
         stale = w.state != h.state || w.nooo != h.nooo || front != h.front || w.fin_pending != h.finp ||
                 w.fin_seq != h.fins;
     }
     if (v < nwin) ring_run(nwin);  // stale: the rest as the wave walk does
+#if DK_TCP_SCAN_STATS
+    if (lane == 0)
+        printf("{\"scan_stats\": 1, \"conn\": %u, \"windows\": %u, \"batch_steps\": %u, \"full_steps\": %u, "
+               "\"slow_windows\": %u, \"ring_windows\": %u, \"ring_runs\": %u, \"restarts\": %u, \"stale\": %u, "
+               "\"us_total\": %.2f, \"us_batch_steps\": %.2f, \"us_slow\": %.2f, \"us_ring\": %.2f}\n",
+               c, nwin, st_batch, st_full, st_slow, st_ring, st_runs, st_restart, (uint32_t)stale,
+               (double)(wall_clock64() - ck_t0) / 100.0, (double)ck_batch / 100.0, (double)ck_slow / 100.0,
+               (double)ck_ring / 100.0);
+#endif
     if (lane == 0) {
         P.out.deliv_start[c] = d0;
         P.open_until[c] = open_until;
@@ -1558,10 +1650,11 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     t->last_walk = (int)walker;
     if (walker == dk_tcp::kScanWalk) {  // windows: ws = range[2c] / 64 + c + v < n / 64 + nconns + 1
         const size_t nw = (size_t)n / 64 + nconns + 1;
-        if (t->used && (t->scan_sum_cap < nw || t->scan_ends_cap < nw * 64 || t->scan_head_cap < 8ull * nconns) &&
+        if (t->used &&
+            (t->scan_sum_cap < dk_tcp::kScanSum * nw || t->scan_ends_cap < nw * 64 || t->scan_head_cap < 8ull * nconns) &&
             hipEventSynchronize(t->last) != hipSuccess)
             return EINVAL;
-        if ((rc = grow(t->scan_sum, t->scan_sum_cap, nw)) || (rc = grow(t->scan_post, t->scan_post_cap, nw)) ||
+        if ((rc = grow(t->scan_sum, t->scan_sum_cap, dk_tcp::kScanSum * nw)) || (rc = grow(t->scan_post, t->scan_post_cap, nw)) ||
             (rc = grow(t->scan_ends, t->scan_ends_cap, nw * 64)) ||
             (rc = grow(t->scan_head, t->scan_head_cap, 8 * (size_t)nconns)))
             return rc;

@@ -18,10 +18,7 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s11: 128-byte line rewrites in the probe (flags 4, 5); the TX kernels rewriting a frame's whole first 128-byte line
-# (DK_TX_LINE128, in-tree default for this session): GPU suite, interleaved A/B against the 64-byte rewrite
-step patch_probe 400 python tools/patch_probe.py --lates 0 --flags 0,1,4,5 --grids 1024,2048
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step tx_ab 400 python tools/abtest.py --workload c2_tcp1500 --grids 0 --tx --reps 11 --iters 20 build/variants/tx64.so build/variants/tx128.so
-step tx_bench 300 python tools/kbench.py --workload c2_tcp1500 --iters 20 --no-rx --tx --tx-fields
+# s16f: per-kernel times of the scan walk at 64 connections in order, round 5's build and the new one
+step prof_old 200 rocprofv3 --kernel-trace --stats -T -d $O/old -o run --output-format csv -- python3 tools/tcp_ab.py build/variants/scanold.so --nconns 64 --reorder 0 --buffer-size 1073741824 --walk scan --reps 3
+step prof_new 200 rocprofv3 --kernel-trace --stats -T -d $O/new -o run --output-format csv -- python3 tools/tcp_ab.py build/variants/scansrd.so --nconns 64 --reorder 0 --buffer-size 1073741824 --walk scan --reps 3
 echo done

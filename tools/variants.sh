@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build tuning variants of libdk_rx.so into build/variants/<name>.so (same sources, different -D knobs).
 # usage: tools/variants.sh "name1:-DX=1 -DY=2" "name2:..."      (SRC=<dir> builds from another source tree)
-# tcp_kernels.hip (rocPRIM sort, slow to compile, no knobs) is compiled once into build/obj/ and linked in.
+# tcp_kernels.hip (rocPRIM sort, slow to compile) is compiled once into build/obj/ and linked in, or per variant when
+# its flags name a DK_TCP_* knob.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 S=${SRC:-$R}
@@ -17,7 +18,12 @@ for spec in "$@"; do
   for f in rx_kernels.hip rx_host.cpp diag.hip ring_host.cpp demi_host.cpp comm_host.cpp; do
     [ -f $S/demikernel_amd/csrc/$f ] && srcs="$srcs $S/demikernel_amd/csrc/$f"
   done
-  $HIPCC -shared $flags -o $R/build/variants/$name.so $srcs -x none $TCPO -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
+  tcpo=$TCPO
+  if [[ "$flags" == *-DDK_TCP_* ]]; then  # TCP knobs: this variant's own tcp_kernels object
+    tcpo=$R/build/obj/tcp_kernels_$name.o
+    $HIPCC -c $flags -o $tcpo $S/demikernel_amd/csrc/tcp_kernels.hip
+  fi
+  $HIPCC -shared $flags -o $R/build/variants/$name.so $srcs -x none $tcpo -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
 done
 wait
 ls $R/build/variants
