@@ -191,6 +191,7 @@ DIAG_FUNCTIONS = [
     ("dk_diag_tx_set_tuning", c_int, [c_int32, c_int32, c_int32]),
     ("dk_diag_tcp_set_walk", c_int, [c_void_p, c_int32, c_int32]),
     ("dk_diag_tcp_last_walk", c_int, [c_void_p]),
+    ("dk_diag_tcp_set_sort", c_int, [c_void_p, c_int32]),
 ]
 DK_DIAG_RX_KNOBS = ["stage", "split", "small", "sched", "grid", "grid_per_cu", "debug", "lds_table", "tail", "udp_table",
                     "host_zc"]

@@ -182,6 +182,116 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_range_kernel(Params P) {
     P.range[c] = lo;
 }
 
+// ---------------- Few connections: a stable counting sort instead of the radix sort ----------------
+// Keys 0 .. 2 nconns take K = 2 nconns + 1 <= kCsortMaxKeys values: (1) each block counts its tile's keys in LDS
+// (H[k][b], key-major); (2) one block scans H flat, so H[k][b] becomes the position of tile b's first key-k segment
+// in the sorted order and range[k] = H[k][0]; (3) each wave of a block places its quarter of the tile, 64 segments a
+// round in arrival order: per round, one gather of each lane's key's position, then one ballot per distinct key
+// gives each lane its rank among the round's lanes of its key (the wave's running position per key lives in LDS).
+// The radix sort's launches cost ~9 µs each at 1M segments whatever the key width (5 per call); this is three short
+// passes, and its scan yields the ranges.
+#ifndef DK_TCP_CSORT_ROWS
+#define DK_TCP_CSORT_ROWS 24
+#endif
+// table rows up to which the counting sort runs: a round's distinct keys grow with the rows (one ballot each), and
+// at 32 rows the sort cost more than the radix sort's launches (session r6s17b: 1 / 17 rows -12 / -6 % per call,
+// 32 rows +3 %, 64 rows +17 %)
+constexpr uint32_t kCsortMaxRows = DK_TCP_CSORT_ROWS;
+constexpr uint32_t kCsortMaxKeys = 2 * kCsortMaxRows + 1, kCsortTile = 4096, kCsortWaves = kBlock / 64;
+constexpr uint32_t kCsortSub = kCsortTile / kCsortWaves;  // segments a wave places, in rounds of 64
+
+__global__ __launch_bounds__(kBlock) void dk_tcp_csort_count_kernel(Params P, uint32_t* H, uint32_t K) {
+    __shared__ uint32_t hist[kCsortMaxKeys];
+    const uint32_t b = blockIdx.x, nb = gridDim.x;
+    for (uint32_t k = threadIdx.x; k < K; k += kBlock) hist[k] = 0;
+    __syncthreads();
+    const uint32_t i0 = b * kCsortTile, i1 = min(P.n, i0 + kCsortTile);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBlock) atomicAdd(&hist[P.keys[i]], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < K; k += kBlock) H[(size_t)k * nb + b] = hist[k];
+}
+
+// One block: exclusive scan of H's m = K nb entries in place (key-major), and range[k] = H[k][0].
+constexpr uint32_t kCsortScanBlock = 1024, kCsortScanPer = 4;
+__global__ __launch_bounds__(kCsortScanBlock) void dk_tcp_csort_scan_kernel(Params P, uint32_t* H, uint32_t K,
+                                                                            uint32_t nb) {
+    __shared__ uint32_t wsum[kCsortScanBlock / 64];
+    const uint32_t m = K * nb, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < m; base += kCsortScanBlock * kCsortScanPer) {
+        const uint32_t j0 = base + tid * kCsortScanPer;
+        uint32_t x[kCsortScanPer], t = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kCsortScanPer; q++) {
+            x[q] = j0 + q < m ? H[j0 + q] : 0u;
+            t += x[q];
+        }
+        uint32_t incl = t;  // the thread's total, scanned over the wave
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = carry, all = 0;
+        for (uint32_t w = 0; w < kCsortScanBlock / 64; w++) {
+            const uint32_t ws = wsum[w];
+            before += w < wv ? ws : 0u;
+            all += ws;
+        }
+        uint32_t run = before + incl - t;
+#pragma unroll
+        for (uint32_t q = 0; q < kCsortScanPer; q++) {
+            if (j0 + q < m) {
+                H[j0 + q] = run;
+                if ((j0 + q) % nb == 0) P.range[(j0 + q) / nb] = run;
+            }
+            run += x[q];
+        }
+        carry += all;
+        __syncthreads();  // wsum reused
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void dk_tcp_csort_scatter_kernel(Params P, const uint32_t* H, uint32_t K) {
+    __shared__ uint32_t cur[kCsortWaves][kCsortMaxKeys];  // per wave: next position per key
+    const uint32_t b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t k = tid; k < kCsortWaves * kCsortMaxKeys; k += kBlock) (&cur[0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t s0 = b * kCsortTile + wv * kCsortSub, s1 = min(P.n, s0 + kCsortSub);
+    for (uint32_t i = s0 + lane; i < s1; i += 64) atomicAdd(&cur[wv][P.keys[i]], 1u);  // this wave's counts
+    __syncthreads();
+    for (uint32_t k = tid; k < K; k += kBlock) {  // -> each wave's first position per key
+        uint32_t pos = H[(size_t)k * nb + b];
+#pragma unroll
+        for (uint32_t w = 0; w < kCsortWaves; w++) {
+            const uint32_t c = cur[w][k];
+            cur[w][k] = pos;
+            pos += c;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    for (uint32_t r = s0; r < s1; r += 64) {
+        const uint32_t i = r + lane;
+        const bool live = i < s1;
+        const uint32_t key = live ? P.keys[i] : 0u;
+        const uint32_t at = cur[wv][key];  // every lane's key's next position, one gather per round
+        uint64_t todo = __ballot(live);
+        uint32_t rank = 0;
+        while (todo) {  // one ballot per distinct key of the round; the leader moves its key's position on
+            const uint32_t lead = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t kk = __builtin_amdgcn_readlane(key, lead);
+            const uint64_t mk = __ballot(live && key == kk);
+            if (key == kk) rank = (uint32_t)__popcll(mk & lt);
+            if (lane == lead) cur[wv][kk] = at + (uint32_t)__popcll(mk);
+            todo &= ~mk;
+        }
+        if (live) P.svals[at + rank] = i;
+    }
+}
+
 // One connection's scalar receive state, in registers during the walk.
 struct Walk {
     uint32_t state, rn, reader, bufsz, snd, fin_pending, fin_seq, nooo;
@@ -1542,6 +1652,8 @@ struct dk_tcp_ctx {
     bool used = false;
     uint32_t *keys = nullptr, *skeys = nullptr, *svals = nullptr, *range = nullptr, *cls = nullptr, *open_until = nullptr;
     size_t keys_cap = 0, skeys_cap = 0, svals_cap = 0, range_cap = 0, cls_cap = 0, open_cap = 0;
+    uint32_t* csort = nullptr;  // the counting sort's per-tile key counts (few connections)
+    size_t csort_cap = 0;
     uint4* rec = nullptr;
     size_t rec_cap = 0;
     uint8_t* temp = nullptr;
@@ -1558,6 +1670,7 @@ struct dk_tcp_ctx {
     uint32_t seen = 0;                    // the last call whose count was read
     bool reordered = false;               // the last read count: >= 1 in kShapeStoredDen segments STORED
     int last_walk = -1;                   // the walk the last call ran (dk_diag_tcp_last_walk)
+    int sort = -1;                        // dk_diag_tcp_set_sort: 1 the radix sort always, -1 the rule
 };
 
 extern "C" {
@@ -1599,13 +1712,19 @@ int dk_diag_tcp_set_walk(dk_tcp_ctx* t, int32_t walk, int32_t relay_waves) {
     return 0;
 }
 
+int dk_diag_tcp_set_sort(dk_tcp_ctx* t, int32_t sort) {
+    if (!t || (sort != -1 && sort != 1)) return EINVAL;
+    t->sort = sort;
+    return 0;
+}
+
 void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     if (!t) return;
     dk_tcp::DeviceGuard g(t->device);
     if (t->used) (void)hipEventSynchronize(t->last);
     for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp,
                     (void*)t->cls, (void*)t->open_until, (void*)t->scan_sum, (void*)t->scan_post, (void*)t->scan_ends,
-                    (void*)t->scan_head, (void*)t->shape})
+                    (void*)t->scan_head, (void*)t->shape, (void*)t->csort})
         if (p) (void)hipFree(p);
     if (t->shape_host) (void)hipHostFree(const_cast<uint32_t*>(t->shape_host));
     (void)hipEventDestroy(t->last);
@@ -1662,12 +1781,21 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     int bits = 1;
     while (bits < 32 && (1ull << bits) <= 2ull * nconns) bits++;  // keys are 0 .. 2 nconns
     const rocprim::counting_iterator<uint32_t> index(0);
-    size_t sort_bytes = 0;
-    if (rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, t->keys, t->skeys, index, t->svals, n, 0, bits,
-                                              s) != hipSuccess)
-        return EINVAL;
-    if (t->used && t->temp_cap < sort_bytes && hipEventSynchronize(t->last) != hipSuccess) return EINVAL;
-    if ((rc = grow(t->temp, t->temp_cap, sort_bytes))) return rc;
+    // few connections: the counting sort (its scan writes the ranges); else the radix sort and the range kernel
+    const uint32_t nkeys = 2 * nconns + 1, ntiles = (n + dk_tcp::kCsortTile - 1) / dk_tcp::kCsortTile;
+    const bool csort = nconns && n && nkeys <= dk_tcp::kCsortMaxKeys && t->sort != 1;
+    if (csort) {
+        if (t->used && t->csort_cap < (size_t)nkeys * ntiles && hipEventSynchronize(t->last) != hipSuccess)
+            return EINVAL;
+        if ((rc = grow(t->csort, t->csort_cap, (size_t)nkeys * ntiles))) return rc;
+    } else {
+        size_t sort_bytes = 0;
+        if (rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, t->keys, t->skeys, index, t->svals, n, 0, bits,
+                                                  s) != hipSuccess)
+            return EINVAL;
+        if (t->used && t->temp_cap < sort_bytes && hipEventSynchronize(t->last) != hipSuccess) return EINVAL;
+        if ((rc = grow(t->temp, t->temp_cap, sort_bytes))) return rc;
+    }
 
     Params P{};
     P.meta = rx->meta;
@@ -1694,14 +1822,20 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     P.call = t->calls + 1;
     P.out = *out;
     const dim3 gn((n + kBlock - 1) / kBlock), gr((2 * nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
-    if (n) {
-        hipLaunchKernelGGL(dk_tcp_key_kernel, gn, dim3(kBlock), 0, s, P);
-        size_t b = t->temp_cap;
-        if (rocprim::radix_sort_pairs<SortConfig>(t->temp, b, t->keys, t->skeys, index, t->svals, n, 0, bits, s) !=
-            hipSuccess)
-            return EINVAL;
+    if (n) hipLaunchKernelGGL(dk_tcp_key_kernel, gn, dim3(kBlock), 0, s, P);
+    if (csort) {
+        hipLaunchKernelGGL(dk_tcp_csort_count_kernel, dim3(ntiles), dim3(kBlock), 0, s, P, t->csort, nkeys);
+        hipLaunchKernelGGL(dk_tcp_csort_scan_kernel, dim3(1), dim3(kCsortScanBlock), 0, s, P, t->csort, nkeys, ntiles);
+        hipLaunchKernelGGL(dk_tcp_csort_scatter_kernel, dim3(ntiles), dim3(kBlock), 0, s, P, t->csort, nkeys);
+    } else {
+        if (n) {
+            size_t b = t->temp_cap;
+            if (rocprim::radix_sort_pairs<SortConfig>(t->temp, b, t->keys, t->skeys, index, t->svals, n, 0, bits, s) !=
+                hipSuccess)
+                return EINVAL;
+        }
+        if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
     }
-    if (nconns) hipLaunchKernelGGL(dk_tcp_range_kernel, gr, dim3(kBlock), 0, s, P);
     if (nconns) {
         switch (walker) {
             case kScanWalk: {

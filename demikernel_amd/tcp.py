@@ -68,9 +68,11 @@ class TcpOut:
 class TcpReceiver:
     """Per-GPU TCP receive processing over a device connection table (the ControlBlock receive halves)."""
 
-    def __init__(self, device: int = 0, lib_path: str | None = None, walk: str | None = None, relay_waves: int = 8):
+    def __init__(self, device: int = 0, lib_path: str | None = None, walk: str | None = None, relay_waves: int = 8,
+                 radix_sort: bool = False):
         """walk: a diagnostic override of the engine's walk choice ("lane", "wave", "relay", "scan"; None = the rule),
-        set through dk_diag_tcp_set_walk."""
+        set through dk_diag_tcp_set_walk; radix_sort: order the batch with the radix sort even where the rule takes
+        the counting sort (dk_diag_tcp_set_sort)."""
         self.lib = N.load_library(lib_path) if lib_path else N.load_library()
         self.device = device
         h = ctypes.c_void_p()
@@ -79,6 +81,8 @@ class TcpReceiver:
         if walk is not None or relay_waves != 8:
             _check(self.lib.dk_diag_tcp_set_walk(self._ctx, N.DK_TCP_WALKS[walk] if walk else -1, relay_waves),
                    "dk_diag_tcp_set_walk")
+        if radix_sort:
+            _check(self.lib.dk_diag_tcp_set_sort(self._ctx, 1), "dk_diag_tcp_set_sort")
 
     @property
     def last_walk(self) -> Optional[str]:

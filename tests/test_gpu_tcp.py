@@ -324,3 +324,27 @@ def test_walk_follows_stream_shape(nconns, reorder):
         assert want == "wave"
     if reorder == 0.0:
         assert stored == 0 and want == "scan"
+
+
+@pytest.mark.parametrize("nconns,reorder", [(1, 0.0), (15, 3.0), (23, 3.0), (24, 3.0), (200, 3.0)])
+def test_counting_sort_matches_radix(nconns, reorder):
+    """Up to 24 table rows (tcp_kernels.hip kCsortMaxRows) the batch is ordered by the counting sort (per-tile key
+    counts, one scan that also yields the ranges, a ballot-ranked scatter); above, by the radix sort. Both orders,
+    forced radix against the rule, give bit-exact results vs the oracle at the boundary (23 / 24 flows + the
+    listener row = 24 / 25 rows) and across tiles (4,096 segments per tile, a partial last one)."""
+    import torch
+
+    n = 3 * 4096 + 777
+    _, tr, table = synth.tcp_streams(n, nconns, 1500, buffer_size=1 << 24, reorder=reorder, seed=91 + nconns)
+    rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
+          "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,
+          "payload": (54 | (tr.ip_len.astype(np.uint32) - 40) << 16).astype(np.uint32)}
+    exp_t = table.copy()
+    exp = O.tcp_process(exp_t, rx)
+    r = rx_device(rx)
+    for radix in (False, True):
+        tcp = TcpReceiver(0, radix_sort=radix)
+        got_t, got = gpu_process(tcp, table.copy(), r)
+        torch.cuda.synchronize()
+        tcp.close()
+        assert_same(got_t, got, exp_t, exp, f"{len(table)} rows reorder {reorder} radix {radix}")

@@ -18,7 +18,9 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s16f: per-kernel times of the scan walk at 64 connections in order, round 5's build and the new one
-step prof_old 200 rocprofv3 --kernel-trace --stats -T -d $O/old -o run --output-format csv -- python3 tools/tcp_ab.py build/variants/scanold.so --nconns 64 --reorder 0 --buffer-size 1073741824 --walk scan --reps 3
-step prof_new 200 rocprofv3 --kernel-trace --stats -T -d $O/new -o run --output-format csv -- python3 tools/tcp_ab.py build/variants/scansrd.so --nconns 64 --reorder 0 --buffer-size 1073741824 --walk scan --reps 3
+# s17b: the counting sort's rounds with one position gather each (ballots only in the loop), up to 32 rows; 128 rows
+# as a variant: GPU suite, A/B against the radix sort (same build) and the scan-walk build before it
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step sort_ab 300 python tools/tcp_ab.py build/variants/scansrd.so build/variants/tcpnew.so:radix build/variants/tcpnew.so build/variants/csort128.so --nconns 1,16,31,63 --reorder 0 --buffer-size 1073741824
+step sort_ab3 300 python tools/tcp_ab.py build/variants/scansrd.so build/variants/tcpnew.so:radix build/variants/tcpnew.so build/variants/csort128.so --nconns 16,31,63 --reorder 3 --buffer-size 16777216
 echo done

@@ -4,7 +4,7 @@ connection count, the same inputs through every build, `--reps` rounds of `--ite
 table restored between calls, outside the timed span), median ms per call; outputs compared with the first build's
 (actions, views, deliveries, connection table).
 
-    python tools/tcp_ab.py build/variants/a.so build/variants/b.so --nconns 1,16,64 [--reorder 0] [--walk scan]
+    python tools/tcp_ab.py build/variants/a.so build/variants/b.so[:radix] --nconns 1,16,64 [--reorder 0] [--walk scan]
 """
 import argparse
 import json
@@ -42,10 +42,12 @@ def main():
         for k, v in rx.items():
             r.t[k].copy_(torch.from_numpy(v.view(np.int32)))
         runs = []
-        for lib in a.libs:
-            tcp = TcpReceiver(0, lib_path=os.path.abspath(lib), walk=a.walk)
+        for spec in a.libs:  # path[:radix] (the radix sort forced: dk_diag_tcp_set_sort)
+            lib, _, opt = spec.partition(":")
+            tcp = TcpReceiver(0, lib_path=os.path.abspath(lib), walk=a.walk, radix_sort=opt == "radix")
             pristine = tcp.conns_to_device(table)
-            runs.append({"name": os.path.basename(lib)[:-3], "tcp": tcp, "pristine": pristine,
+            runs.append({"name": os.path.basename(lib)[:-3] + (":" + opt if opt else ""), "tcp": tcp,
+                         "pristine": pristine,
                          "conns": pristine.clone(), "out": TcpOut(a.nseg, len(table), 0), "t": []})
         for rep in range(a.reps + 1):
             for R in runs:
