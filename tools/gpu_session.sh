@@ -18,9 +18,9 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s18: the round's final tree: GPU suite, smoke(), the default bench line, then the rocprofv3 evidence pass
-step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
-step bench 600 python bench.py
-step profile 900 bash tools/profile_bench.sh r6g
+# s19: C3 re-check (s18's box ran the small kernel 26 µs under rocprofv3 against 20.7 the session before, same ISA)
+step c3k 200 python tools/kbench.py --workload c3_udp64 --iters 20 --rotate 8 --defer
+step c3rk 200 python tools/kbench.py --workload c3_udp64_random_ports --iters 20 --rotate 8 --defer
+step c3sweep 300 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M --rotate 8 --tag s19
+step c3prof 200 rocprofv3 --kernel-trace --stats -T -d $O/c3 -o run --output-format csv -- python3 tools/kbench.py --workload c3_udp64 --iters 20 --rotate 8 --defer
 echo done

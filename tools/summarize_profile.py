@@ -45,6 +45,24 @@ def kbench_info(path):
     return rx, probe, tx
 
 
+def trace_summary(src):
+    """Per kernel of each stats run: calls, mean, median and the mean without the first call (a run's first launch
+    carries one-time costs: rocprofv3's stats average it in), from the kernel trace."""
+    out = {}
+    for sub in ("bench", "c3", "c1", "tx", "txf", "tcp"):
+        f = os.path.join(src, sub, "run_kernel_trace.csv")
+        if not os.path.exists(f):
+            continue
+        d = defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            if r["Kernel_Name"].startswith("dk_"):
+                d[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
+        out[sub] = {k: {"calls": len(v), "mean_us": round(sum(v) / len(v), 2),
+                        "median_us": round(sorted(v)[len(v) // 2], 2),
+                        "mean_after_first_us": round(sum(v[1:]) / max(len(v) - 1, 1), 2)} for k, v in d.items()}
+    return out
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
@@ -63,6 +81,9 @@ def main():
         shutil.copy(os.path.join(src, "tcp.json"), os.path.join(dst, f"{tag}_tcp_under_rocprof.json"))
     if os.path.exists(os.path.join(src, "bench.json")):
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench_under_rocprof.json"))
+    ts = trace_summary(src)
+    if ts:
+        json.dump(ts, open(os.path.join(dst, f"{tag}_kernel_trace_summary.json"), "w"), indent=1)
     traffic = {}
     rows = [["workload", "kernel", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "calib_factor", "hbm_read_bytes",
              "hbm_write_bytes", "algo_bytes", "traffic_over_algo"]]
