@@ -1259,6 +1259,9 @@ struct TailQ {
 #ifndef DK_STAGED_PRIO
 #define DK_STAGED_PRIO 0  // > 0: a wave streaming its chunk's frames issues at this priority, phase C at 0
 #endif
+#ifndef DK_STAGED_LATE_INIT
+#define DK_STAGED_LATE_INIT 0  // 1: the LDS init, table copy and barrier after a wave's first frame stream
+#endif
 #ifndef DK_TAIL_LATE
 #define DK_TAIL_LATE 0  // 1: a tail grab is for the next round (issued after this round's stream, resolved after its
                         // phase C, the descriptors loaded then): committed half a round ahead instead of 1.5
@@ -1280,11 +1283,18 @@ void dk_rx_kernel(RxParams P) {
     DK_STAMPW_RT(12);
     DK_STAMPW(0);
     const bool lds_flows = P.flow_mode == kFlowLds;
-    for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
-    if (lds_flows)
-        for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
-    lt_load(P, tid, kBlock);
-    __syncthreads();
+    // the histograms' zeroing, the Active table's copy and the workgroup barrier: before the first chunk, or
+    // (DK_STAGED_LATE_INIT) after a wave's first frame stream, which needs none of them (a wave without a chunk at its
+    // end): the copy then overlaps the first stream
+    const auto init = [&]() {
+        for (uint32_t k = tid; k < DK_V_COUNT; k += kBlock) s_vh[k] = 0;
+        if (lds_flows)
+            for (uint32_t k = tid; k < P.flow_words; k += kBlock) s_flow[k] = 0;
+        lt_load(P, tid, kBlock);
+        __syncthreads();
+    };
+    constexpr bool kLateInit = DK_STAGED_LATE_INIT != 0 && kStage;
+    if (!kLateInit) init();
     DK_STAMPW(1);
 
     const WaveRange r = wave_range(P.sched, P.n, wv, lane);
@@ -1294,6 +1304,7 @@ void dk_rx_kernel(RxParams P) {
     const uint32_t ks = dyn ? P.tail_ks : ~0u;  // chunks from round ks on come from the tail (host: ks >= 2)
     uint32_t c, lim, nc, nlim;
     bool have = r.chunk(0, c, lim);
+    const bool had = have;
     uint32_t noff = 0, nlen = 0;  // descriptors of this wave's next chunk
     if (have && c + r.lane_off < lim) {
         noff = P.off[c + r.lane_off];
@@ -1338,6 +1349,7 @@ void dk_rx_kernel(RxParams P) {
         // register would be live through the stream's load registers, the kernel's register peak); phase C covers
         // its latency
         if (kLate ? late : have && k + 2 >= ks) Q.issue(P, lane);
+        if (kLateInit && k == 0) init();
         if (k < 3) DK_STAMPW(3 + 3 * k);
         DK_ACC_SPLIT(0);
         if (DK_STAGED_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -1376,6 +1388,7 @@ void dk_rx_kernel(RxParams P) {
         DK_MARK(loop_tail);
     }
 
+    if (kLateInit && !had) init();  // a wave without a chunk: its share of the copy and the barrier
     DK_STAMPW(11);
     DK_MARK(epilogue);
     DK_ACC_BEGIN();

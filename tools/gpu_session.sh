@@ -18,9 +18,7 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s19: C3 re-check (s18's box ran the small kernel 26 µs under rocprofv3 against 20.7 the session before, same ISA)
-step c3k 200 python tools/kbench.py --workload c3_udp64 --iters 20 --rotate 8 --defer
-step c3rk 200 python tools/kbench.py --workload c3_udp64_random_ports --iters 20 --rotate 8 --defer
-step c3sweep 300 python tools/sweep.py --workload c3_udp64 --frames 1M,2M,4M --rotate 8 --tag s19
-step c3prof 200 rocprofv3 --kernel-trace --stats -T -d $O/c3 -o run --output-format csv -- python3 tools/kbench.py --workload c3_udp64 --iters 20 --rotate 8 --defer
+# s20: the staged kernel's LDS init, table copy and barrier after each wave's first frame stream (DK_STAGED_LATE_INIT)
+step imix_ab 400 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 9 --iters 10 --check build/variants/libase.so build/variants/lateinit.so
+step c1_ab 300 python tools/abtest.py --workload c1_tcp1078 --grids 0 --rotate 3 --defer --reps 11 --iters 20 --check build/variants/libase.so build/variants/lateinit.so
 echo done
