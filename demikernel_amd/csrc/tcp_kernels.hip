@@ -5,9 +5,10 @@
 // within one, order matters (RCV.NXT, the out-of-order store). For a whole dk_rx batch:
 //   1. dk_tcp_key_kernel (one pass over the batch, coalesced): frame -> key (its connection, for delivered TCP segments
 //      of a connection in the table; else nconns) and its {seq, ack, meta, payload} record; skipped frames' outputs;
-//   2. a stable LSD radix sort of (key, frame index) over the key's bits (rocPRIM onesweep, 8 bits per pass): each
-//      connection's segments contiguous, in arrival order;
-//   3. dk_tcp_range_kernel: each connection's range = lower_bound of its key in the sorted keys;
+//   2. a stable sort of (key, frame index): one counting pass over the whole key up to 80 table rows
+//      (dk_tcp_sort_*_kernel), rocPRIM's onesweep radix sort above: each connection's segments contiguous, in
+//      arrival order;
+//   3. each connection's range: from the whole-key pass's scan, else dk_tcp_range_kernel (lower_bound of its key);
 //   4. dk_tcp_walk_kernel: one lane per connection (its out-of-order store in LDS) runs its segments through the
 //      state machine in order, reading each segment's record through the sorted frame index (pipelined: indices two
 //      batches of kBatch ahead, records one batch ahead). The walk is the only sequential part
@@ -182,47 +183,52 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_range_kernel(Params P) {
     P.range[c] = lo;
 }
 
-// ---------------- Few connections: a stable counting sort instead of the radix sort ----------------
-// Keys 0 .. 2 nconns take K = 2 nconns + 1 <= kCsortMaxKeys values: (1) each block counts its tile's keys in LDS
-// (H[k][b], key-major); (2) one block scans H flat, so H[k][b] becomes the position of tile b's first key-k segment
-// in the sorted order and range[k] = H[k][0]; (3) each wave of a block places its quarter of the tile, 64 segments a
-// round in arrival order: per round, one gather of each lane's key's position, then one ballot per distinct key
-// gives each lane its rank among the round's lanes of its key (the wave's running position per key lives in LDS).
-// The radix sort's launches cost ~9 µs each at 1M segments whatever the key width (5 per call); this is three short
-// passes, and its scan yields the ranges.
-#ifndef DK_TCP_CSORT_ROWS
-#define DK_TCP_CSORT_ROWS 24
-#endif
-// table rows up to which the counting sort runs: a round's distinct keys grow with the rows (one ballot each), and
-// at 32 rows the sort cost more than the radix sort's launches (session r6s17b: 1 / 17 rows -12 / -6 % per call,
-// 32 rows +3 %, 64 rows +17 %)
-constexpr uint32_t kCsortMaxRows = DK_TCP_CSORT_ROWS;
-constexpr uint32_t kCsortMaxKeys = 2 * kCsortMaxRows + 1, kCsortTile = 4096, kCsortWaves = kBlock / 64;
-constexpr uint32_t kCsortSub = kCsortTile / kCsortWaves;  // segments a wave places, in rounds of 64
+// ---------------- Few connections: the batch's stable sort by one counting pass (round 6) ----------------
+// Up to kSortMaxRows table rows, a stable counting pass over the whole key instead of the radix sort and the range
+// kernel: (1) each block counts its tile's keys in LDS (H[k][b], key-major); (2) one block scans H flat, so H[k][b]
+// becomes the position of tile b's first key-k segment and range[k] = H[k][0]; (3) each wave of a block places its
+// share of the tile 64 segments a round in arrival order: a gather of each lane's key's next position, then the lanes
+// of equal key found by one ballot per key bit (the AND of each bit's ballot or its complement), the rank among them
+// by popcount, and the group's lowest lane moves the key's position on. rocPRIM's onesweep costs ~9 µs per launch at
+// 1M segments and ~5 µs per lookback-state fill (5 launches + 5 fills at 16 bits); this is three short launches while
+// a round's segments share few keys: with many, its 4-byte writes scatter (one per key per round) and the radix sort's
+// LDS-staged runs win (session r6s21: 255 rows +25 %, two 8-bit passes for 16,384 connections +33 %; 17 / 65 rows
+// -12 / -6 %, 1 row -10 %).
+constexpr uint32_t kSortBlock = 512, kSortWaves = kSortBlock / 64, kSortTile = 8192, kSortSub = kSortTile / kSortWaves;
+constexpr uint32_t kSortMaxRows = 80, kSortMaxBuckets = 2 * kSortMaxRows + 1;
+struct SortPass {
+    const uint32_t* kin;  // keys in
+    const uint32_t* vin;  // values in (nullptr: the element's index)
+    uint32_t* kout;       // keys out (nullptr: not kept)
+    uint32_t* vout;       // values out
+    uint32_t* H;          // [nbuck][ntiles] counts, then positions
+    uint32_t shift, mask, nbuck;
+};
 
-__global__ __launch_bounds__(kBlock) void dk_tcp_csort_count_kernel(Params P, uint32_t* H, uint32_t K) {
-    __shared__ uint32_t hist[kCsortMaxKeys];
+__global__ __launch_bounds__(kSortBlock) void dk_tcp_sort_count_kernel(uint32_t n, SortPass S) {
+    __shared__ uint32_t hist[kSortMaxBuckets];
     const uint32_t b = blockIdx.x, nb = gridDim.x;
-    for (uint32_t k = threadIdx.x; k < K; k += kBlock) hist[k] = 0;
+    for (uint32_t k = threadIdx.x; k < S.nbuck; k += kSortBlock) hist[k] = 0;
     __syncthreads();
-    const uint32_t i0 = b * kCsortTile, i1 = min(P.n, i0 + kCsortTile);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBlock) atomicAdd(&hist[P.keys[i]], 1u);
+    const uint32_t i0 = b * kSortTile, i1 = min(n, i0 + kSortTile);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kSortBlock) atomicAdd(&hist[(S.kin[i] >> S.shift) & S.mask], 1u);
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < K; k += kBlock) H[(size_t)k * nb + b] = hist[k];
+    for (uint32_t k = threadIdx.x; k < S.nbuck; k += kSortBlock) S.H[(size_t)k * nb + b] = hist[k];
 }
 
-// One block: exclusive scan of H's m = K nb entries in place (key-major), and range[k] = H[k][0].
-constexpr uint32_t kCsortScanBlock = 1024, kCsortScanPer = 4;
-__global__ __launch_bounds__(kCsortScanBlock) void dk_tcp_csort_scan_kernel(Params P, uint32_t* H, uint32_t K,
-                                                                            uint32_t nb) {
-    __shared__ uint32_t wsum[kCsortScanBlock / 64];
-    const uint32_t m = K * nb, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// One block: exclusive scan of H's nbuck * nb entries in place (digit-major); range (non-null: a whole-key pass)
+// [k] = H[k][0].
+constexpr uint32_t kSortScanBlock = 1024, kSortScanPer = 8;
+__global__ __launch_bounds__(kSortScanBlock) void dk_tcp_sort_scan_kernel(uint32_t* H, uint32_t m, uint32_t nb,
+                                                                          uint32_t* range) {
+    __shared__ uint32_t wsum[kSortScanBlock / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < m; base += kCsortScanBlock * kCsortScanPer) {
-        const uint32_t j0 = base + tid * kCsortScanPer;
-        uint32_t x[kCsortScanPer], t = 0;
+    for (uint32_t base = 0; base < m; base += kSortScanBlock * kSortScanPer) {
+        const uint32_t j0 = base + tid * kSortScanPer;
+        uint32_t x[kSortScanPer], t = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < kCsortScanPer; q++) {
+        for (uint32_t q = 0; q < kSortScanPer; q++) {
             x[q] = j0 + q < m ? H[j0 + q] : 0u;
             t += x[q];
         }
@@ -235,17 +241,17 @@ __global__ __launch_bounds__(kCsortScanBlock) void dk_tcp_csort_scan_kernel(Para
         if (lane == 63) wsum[wv] = incl;
         __syncthreads();
         uint32_t before = carry, all = 0;
-        for (uint32_t w = 0; w < kCsortScanBlock / 64; w++) {
+        for (uint32_t w = 0; w < kSortScanBlock / 64; w++) {
             const uint32_t ws = wsum[w];
             before += w < wv ? ws : 0u;
             all += ws;
         }
         uint32_t run = before + incl - t;
 #pragma unroll
-        for (uint32_t q = 0; q < kCsortScanPer; q++) {
+        for (uint32_t q = 0; q < kSortScanPer; q++) {
             if (j0 + q < m) {
                 H[j0 + q] = run;
-                if ((j0 + q) % nb == 0) P.range[(j0 + q) / nb] = run;
+                if (range && (j0 + q) % nb == 0) range[(j0 + q) / nb] = run;
             }
             run += x[q];
         }
@@ -254,18 +260,18 @@ __global__ __launch_bounds__(kCsortScanBlock) void dk_tcp_csort_scan_kernel(Para
     }
 }
 
-__global__ __launch_bounds__(kBlock) void dk_tcp_csort_scatter_kernel(Params P, const uint32_t* H, uint32_t K) {
-    __shared__ uint32_t cur[kCsortWaves][kCsortMaxKeys];  // per wave: next position per key
+__global__ __launch_bounds__(kSortBlock) void dk_tcp_sort_scatter_kernel(uint32_t n, SortPass S) {
+    __shared__ uint32_t cur[kSortWaves][kSortMaxBuckets];  // per wave: the next position per digit
     const uint32_t b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (uint32_t k = tid; k < kCsortWaves * kCsortMaxKeys; k += kBlock) (&cur[0][0])[k] = 0;
+    for (uint32_t k = tid; k < kSortWaves * kSortMaxBuckets; k += kSortBlock) (&cur[0][0])[k] = 0;
     __syncthreads();
-    const uint32_t s0 = b * kCsortTile + wv * kCsortSub, s1 = min(P.n, s0 + kCsortSub);
-    for (uint32_t i = s0 + lane; i < s1; i += 64) atomicAdd(&cur[wv][P.keys[i]], 1u);  // this wave's counts
+    const uint32_t s0 = b * kSortTile + wv * kSortSub, s1 = min(n, s0 + kSortSub);
+    for (uint32_t i = s0 + lane; i < s1; i += 64) atomicAdd(&cur[wv][(S.kin[i] >> S.shift) & S.mask], 1u);
     __syncthreads();
-    for (uint32_t k = tid; k < K; k += kBlock) {  // -> each wave's first position per key
-        uint32_t pos = H[(size_t)k * nb + b];
+    for (uint32_t k = tid; k < S.nbuck; k += kSortBlock) {  // -> each wave's first position per digit
+        uint32_t pos = S.H[(size_t)k * nb + b];
 #pragma unroll
-        for (uint32_t w = 0; w < kCsortWaves; w++) {
+        for (uint32_t w = 0; w < kSortWaves; w++) {
             const uint32_t c = cur[w][k];
             cur[w][k] = pos;
             pos += c;
@@ -273,22 +279,24 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_csort_scatter_kernel(Params P, 
     }
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t nbits = 32u - (uint32_t)__builtin_clz(S.mask | 1u);  // digit bits (mask = 2^bits - 1)
     for (uint32_t r = s0; r < s1; r += 64) {
         const uint32_t i = r + lane;
         const bool live = i < s1;
-        const uint32_t key = live ? P.keys[i] : 0u;
-        const uint32_t at = cur[wv][key];  // every lane's key's next position, one gather per round
-        uint64_t todo = __ballot(live);
-        uint32_t rank = 0;
-        while (todo) {  // one ballot per distinct key of the round; the leader moves its key's position on
-            const uint32_t lead = (uint32_t)__builtin_ctzll(todo);
-            const uint32_t kk = __builtin_amdgcn_readlane(key, lead);
-            const uint64_t mk = __ballot(live && key == kk);
-            if (key == kk) rank = (uint32_t)__popcll(mk & lt);
-            if (lane == lead) cur[wv][kk] = at + (uint32_t)__popcll(mk);
-            todo &= ~mk;
+        const uint32_t key = live ? S.kin[i] : 0u, val = live ? (S.vin ? S.vin[i] : i) : 0u;
+        const uint32_t d = (key >> S.shift) & S.mask;
+        uint64_t same = __ballot(live);
+        for (uint32_t bit = 0; bit < nbits; bit++) {  // the lanes whose digit equals this lane's
+            const uint64_t ones = __ballot(live && ((d >> bit) & 1u));
+            same &= ((d >> bit) & 1u) ? ones : ~ones;
         }
-        if (live) P.svals[at + rank] = i;
+        const uint32_t at = cur[wv][d];
+        const uint32_t rank = (uint32_t)__popcll(same & lt);
+        if (live && rank == 0) cur[wv][d] = at + (uint32_t)__popcll(same);
+        if (live) {
+            S.vout[at + rank] = val;
+            if (S.kout) S.kout[at + rank] = key;
+        }
     }
 }
 
@@ -1652,7 +1660,7 @@ struct dk_tcp_ctx {
     bool used = false;
     uint32_t *keys = nullptr, *skeys = nullptr, *svals = nullptr, *range = nullptr, *cls = nullptr, *open_until = nullptr;
     size_t keys_cap = 0, skeys_cap = 0, svals_cap = 0, range_cap = 0, cls_cap = 0, open_cap = 0;
-    uint32_t* csort = nullptr;  // the counting sort's per-tile key counts (few connections)
+    uint32_t* csort = nullptr;  // the counting pass's per-tile key counts
     size_t csort_cap = 0;
     uint4* rec = nullptr;
     size_t rec_cap = 0;
@@ -1781,13 +1789,14 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     int bits = 1;
     while (bits < 32 && (1ull << bits) <= 2ull * nconns) bits++;  // keys are 0 .. 2 nconns
     const rocprim::counting_iterator<uint32_t> index(0);
-    // few connections: the counting sort (its scan writes the ranges); else the radix sort and the range kernel
-    const uint32_t nkeys = 2 * nconns + 1, ntiles = (n + dk_tcp::kCsortTile - 1) / dk_tcp::kCsortTile;
-    const bool csort = nconns && n && nkeys <= dk_tcp::kCsortMaxKeys && t->sort != 1;
+    // the batch's order by connection: one counting pass over the whole key (its scan writes the ranges) up to
+    // kSortMaxRows table rows, else the radix sort and the range kernel
+    const uint32_t nkeys = 2 * nconns + 1, ntiles = (n + dk_tcp::kSortTile - 1) / dk_tcp::kSortTile;
+    const bool csort = nconns && n && nconns <= dk_tcp::kSortMaxRows && t->sort != 1;
     if (csort) {
-        if (t->used && t->csort_cap < (size_t)nkeys * ntiles && hipEventSynchronize(t->last) != hipSuccess)
-            return EINVAL;
-        if ((rc = grow(t->csort, t->csort_cap, (size_t)nkeys * ntiles))) return rc;
+        const size_t hb = (size_t)nkeys * ntiles;
+        if (t->used && t->csort_cap < hb && hipEventSynchronize(t->last) != hipSuccess) return EINVAL;
+        if ((rc = grow(t->csort, t->csort_cap, hb))) return rc;
     } else {
         size_t sort_bytes = 0;
         if (rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, t->keys, t->skeys, index, t->svals, n, 0, bits,
@@ -1824,9 +1833,15 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     const dim3 gn((n + kBlock - 1) / kBlock), gr((2 * nconns + kBlock) / kBlock), gc((nconns + kWalkBlock - 1) / kWalkBlock);
     if (n) hipLaunchKernelGGL(dk_tcp_key_kernel, gn, dim3(kBlock), 0, s, P);
     if (csort) {
-        hipLaunchKernelGGL(dk_tcp_csort_count_kernel, dim3(ntiles), dim3(kBlock), 0, s, P, t->csort, nkeys);
-        hipLaunchKernelGGL(dk_tcp_csort_scan_kernel, dim3(1), dim3(kCsortScanBlock), 0, s, P, t->csort, nkeys, ntiles);
-        hipLaunchKernelGGL(dk_tcp_csort_scatter_kernel, dim3(ntiles), dim3(kBlock), 0, s, P, t->csort, nkeys);
+        const auto pass = [&](const SortPass& S, uint32_t* range) {
+            hipLaunchKernelGGL(dk_tcp_sort_count_kernel, dim3(ntiles), dim3(kSortBlock), 0, s, n, S);
+            hipLaunchKernelGGL(dk_tcp_sort_scan_kernel, dim3(1), dim3(kSortScanBlock), 0, s, S.H, S.nbuck * ntiles,
+                               ntiles, range);
+            hipLaunchKernelGGL(dk_tcp_sort_scatter_kernel, dim3(ntiles), dim3(kSortBlock), 0, s, n, S);
+        };
+        uint32_t mask = 1;  // the key's bits: 2^bits - 1 >= nkeys - 1
+        while (mask < nkeys - 1) mask = 2 * mask + 1;
+        pass(SortPass{t->keys, nullptr, nullptr, t->svals, t->csort, 0u, mask, nkeys}, t->range);
     } else {
         if (n) {
             size_t b = t->temp_cap;

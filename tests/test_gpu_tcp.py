@@ -326,15 +326,16 @@ def test_walk_follows_stream_shape(nconns, reorder):
         assert stored == 0 and want == "scan"
 
 
-@pytest.mark.parametrize("nconns,reorder", [(1, 0.0), (15, 3.0), (23, 3.0), (24, 3.0), (200, 3.0)])
+@pytest.mark.parametrize("nconns,reorder", [(1, 0.0), (23, 3.0), (79, 3.0), (80, 3.0), (3000, 3.0)])
 def test_counting_sort_matches_radix(nconns, reorder):
-    """Up to 24 table rows (tcp_kernels.hip kCsortMaxRows) the batch is ordered by the counting sort (per-tile key
-    counts, one scan that also yields the ranges, a ballot-ranked scatter); above, by the radix sort. Both orders,
-    forced radix against the rule, give bit-exact results vs the oracle at the boundary (23 / 24 flows + the
-    listener row = 24 / 25 rows) and across tiles (4,096 segments per tile, a partial last one)."""
+    """Up to 80 table rows (tcp_kernels.hip kSortMaxRows) the batch is ordered by one counting pass over the whole
+    key (per-tile key counts, one scan that also yields the ranges, a scatter ranked by per-bit ballots); above, by
+    rocPRIM's radix sort. The rule and the forced radix sort (dk_diag_tcp_set_sort) give bit-exact results vs the
+    oracle at the boundary (79 / 80 flows + the listener row = 80 / 81 rows), with thousands of connections, and
+    across tiles (8,192 segments per tile, a partial last one)."""
     import torch
 
-    n = 3 * 4096 + 777
+    n = 3 * 8192 + 777
     _, tr, table = synth.tcp_streams(n, nconns, 1500, buffer_size=1 << 24, reorder=reorder, seed=91 + nconns)
     rx = {"meta": (6 << 8 | tr.flags.astype(np.uint32) << 16 | 0x50 << 24).astype(np.uint32),
           "flow_id": tr.flow.astype(np.uint32), "tcp_seq": tr.seq, "tcp_ack": tr.ack,

@@ -18,7 +18,8 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s20: the staged kernel's LDS init, table copy and barrier after each wave's first frame stream (DK_STAGED_LATE_INIT)
-step imix_ab 400 python tools/abtest.py --workload c4_imix --grids 0 --rotate 2 --defer --reps 9 --iters 10 --check build/variants/libase.so build/variants/lateinit.so
-step c1_ab 300 python tools/abtest.py --workload c1_tcp1078 --grids 0 --rotate 3 --defer --reps 11 --iters 20 --check build/variants/libase.so build/variants/lateinit.so
+# s21b: one counting pass with per-bit ballot ranking up to 80 rows, the radix sort above: GPU suite, A/B
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step sort_ab 300 python tools/tcp_ab.py build/variants/tcpnew.so build/variants/tcpsort.so:radix build/variants/tcpsort.so --nconns 1,16,40,64,79 --reorder 0 --buffer-size 1073741824
+step sort_ab3 300 python tools/tcp_ab.py build/variants/tcpnew.so build/variants/tcpsort.so:radix build/variants/tcpsort.so --nconns 16,64,79,16384 --reorder 3 --buffer-size 16777216
 echo done
