@@ -18,8 +18,9 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s21b: one counting pass with per-bit ballot ranking up to 80 rows, the radix sort above: GPU suite, A/B
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step sort_ab 300 python tools/tcp_ab.py build/variants/tcpnew.so build/variants/tcpsort.so:radix build/variants/tcpsort.so --nconns 1,16,40,64,79 --reorder 0 --buffer-size 1073741824
-step sort_ab3 300 python tools/tcp_ab.py build/variants/tcpnew.so build/variants/tcpsort.so:radix build/variants/tcpsort.so --nconns 16,64,79,16384 --reorder 3 --buffer-size 16777216
+# s22: the round's final tree: GPU suite, smoke(), the default bench line, then the rocprofv3 evidence pass
+step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
+step bench 600 python bench.py
+step profile 900 bash tools/profile_bench.sh r6h
 echo done
