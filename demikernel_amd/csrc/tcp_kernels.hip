@@ -5,7 +5,7 @@
 // within one, order matters (RCV.NXT, the out-of-order store). For a whole dk_rx batch:
 //   1. dk_tcp_key_kernel (one pass over the batch, coalesced): frame -> key (its connection, for delivered TCP segments
 //      of a connection in the table; else nconns) and its {seq, ack, meta, payload} record; skipped frames' outputs;
-//   2. a stable sort of (key, frame index): one counting pass over the whole key up to 80 table rows
+//   2. a stable sort of (key, frame index): one counting pass over the whole key up to 255 table rows
 //      (dk_tcp_sort_*_kernel), rocPRIM's onesweep radix sort above: each connection's segments contiguous, in
 //      arrival order;
 //   3. each connection's range: from the whole-key pass's scan, else dk_tcp_range_kernel (lower_bound of its key);
@@ -183,19 +183,23 @@ __global__ __launch_bounds__(kBlock) void dk_tcp_range_kernel(Params P) {
     P.range[c] = lo;
 }
 
-// ---------------- Few connections: the batch's stable sort by one counting pass (round 6) ----------------
+// ---------------- Up to 255 connections: the batch's stable sort by one counting pass (round 6) ----------------
 // Up to kSortMaxRows table rows, a stable counting pass over the whole key instead of the radix sort and the range
 // kernel: (1) each block counts its tile's keys in LDS (H[k][b], key-major); (2) one block scans H flat, so H[k][b]
 // becomes the position of tile b's first key-k segment and range[k] = H[k][0]; (3) each wave of a block places its
 // share of the tile 64 segments a round in arrival order: a gather of each lane's key's next position, then the lanes
 // of equal key found by one ballot per key bit (the AND of each bit's ballot or its complement), the rank among them
-// by popcount, and the group's lowest lane moves the key's position on. rocPRIM's onesweep costs ~9 µs per launch at
-// 1M segments and ~5 µs per lookback-state fill (5 launches + 5 fills at 16 bits); this is three short launches while
-// a round's segments share few keys: with many, its 4-byte writes scatter (one per key per round) and the radix sort's
-// LDS-staged runs win (session r6s21: 255 rows +25 %, two 8-bit passes for 16,384 connections +33 %; 17 / 65 rows
-// -12 / -6 %, 1 row -10 %).
+// by popcount, and the group's lowest lane moves the key's position on. Each wave loads its keys up front (one load
+// latency, not one per round), counts by key group when the keys are few (same-address LDS adds serialize), and the
+// scan goes through LDS so its global loads and stores coalesce. rocPRIM's onesweep costs ~9 µs per launch at 1M
+// segments and ~5 µs per lookback-state fill (5 launches + 5 fills at 16 bits); the counting pass is three short
+// launches (sessions r6s24-r6s25: -3 % at 1 connection to -17 % at 127 against the radix sort). Many keys need two
+// passes, whose scatter and scan lose to onesweep (session r6s21: +33 % at 16,384 connections).
 constexpr uint32_t kSortBlock = 512, kSortWaves = kSortBlock / 64, kSortTile = 8192, kSortSub = kSortTile / kSortWaves;
-constexpr uint32_t kSortMaxRows = 80, kSortMaxBuckets = 2 * kSortMaxRows + 1;
+#ifndef DK_TCP_SORT_ROWS
+#define DK_TCP_SORT_ROWS 255
+#endif
+constexpr uint32_t kSortMaxRows = DK_TCP_SORT_ROWS, kSortMaxBuckets = 2 * kSortMaxRows + 1;
 struct SortPass {
     const uint32_t* kin;  // keys in
     const uint32_t* vin;  // values in (nullptr: the element's index)
@@ -205,31 +209,83 @@ struct SortPass {
     uint32_t shift, mask, nbuck;
 };
 
-__global__ __launch_bounds__(kSortBlock) void dk_tcp_sort_count_kernel(uint32_t n, SortPass S) {
-    __shared__ uint32_t hist[kSortMaxBuckets];
-    const uint32_t b = blockIdx.x, nb = gridDim.x;
-    for (uint32_t k = threadIdx.x; k < S.nbuck; k += kSortBlock) hist[k] = 0;
-    __syncthreads();
-    const uint32_t i0 = b * kSortTile, i1 = min(n, i0 + kSortTile);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kSortBlock) atomicAdd(&hist[(S.kin[i] >> S.shift) & S.mask], 1u);
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < S.nbuck; k += kSortBlock) S.H[(size_t)k * nb + b] = hist[k];
+// A wave's 64-key round grouped by digit: `same` = the live lanes whose digit equals this lane's (one ballot per digit
+// bit: the AND of each bit's ballot or its complement); the group's lowest lane is its leader.
+__device__ __forceinline__ uint64_t digit_group(uint32_t d, bool live, uint32_t nbits) {
+    uint64_t same = __ballot(live);
+    for (uint32_t bit = 0; bit < nbits; bit++) {
+        const uint64_t ones = __ballot(live && ((d >> bit) & 1u));
+        same &= ((d >> bit) & 1u) ? ones : ~ones;
+    }
+    return same;
+}
+constexpr uint32_t kSortRounds = kSortSub / 64;  // rounds of 64 a wave takes; its keys are loaded up front
+constexpr uint32_t kSortGroupBits = 4;  // up to 16 key values the counts go by digit group (session r6s24)
+
+// Each wave's share of the tile: keys loaded together (one load latency per wave, not one per round), then counted by
+// digit group — one LDS add per group and round from its leader, so a tile of one key costs 16 adds per wave instead
+// of 1,024 serialized on one address.
+__device__ __forceinline__ void sort_load_keys(const SortPass& S, uint32_t s0, uint32_t s1, uint32_t lane,
+                                               uint32_t (&kr)[kSortRounds]) {
+#pragma unroll
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const uint32_t i = s0 + r * 64 + lane;
+        kr[r] = i < s1 ? S.kin[i] : 0u;
+    }
+}
+__device__ __forceinline__ void sort_count_keys(const SortPass& S, uint32_t s0, uint32_t s1, uint32_t lane,
+                                                const uint32_t (&kr)[kSortRounds], uint32_t* cnt, uint32_t nbits) {
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const bool live = s0 + r * 64 + lane < s1;
+        const uint32_t d = (kr[r] >> S.shift) & S.mask;
+        if (nbits <= kSortGroupBits) {  // few keys: one add per group (same-address adds serialize)
+            const uint64_t same = digit_group(d, live, nbits);
+            if (live && !(same & lt)) atomicAdd(&cnt[d], (uint32_t)__popcll(same));
+        } else if (live) {  // many keys: the adds rarely meet, and the ballots would cost more
+            atomicAdd(&cnt[d], 1u);
+        }
+    }
 }
 
-// One block: exclusive scan of H's nbuck * nb entries in place (digit-major); range (non-null: a whole-key pass)
-// [k] = H[k][0].
-constexpr uint32_t kSortScanBlock = 1024, kSortScanPer = 8;
+__global__ __launch_bounds__(kSortBlock) void dk_tcp_sort_count_kernel(uint32_t n, SortPass S) {
+    __shared__ uint32_t hist[kSortMaxBuckets];
+    const uint32_t b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t nbits = 32u - (uint32_t)__builtin_clz(S.mask | 1u);
+    uint32_t kr[kSortRounds];
+    const uint32_t s0 = b * kSortTile + wv * kSortSub, s1 = min(n, s0 + kSortSub);
+    sort_load_keys(S, s0, s1, lane, kr);
+    for (uint32_t k = tid; k < S.nbuck; k += kSortBlock) hist[k] = 0;
+    __syncthreads();
+    sort_count_keys(S, s0, s1, lane, kr, hist, nbits);
+    __syncthreads();
+    for (uint32_t k = tid; k < S.nbuck; k += kSortBlock) S.H[(size_t)k * nb + b] = hist[k];
+}
+
+// One block: exclusive scan of H's m = nbuck * nb entries in place (digit-major); range (non-null: a whole-key pass)
+// [k] = H[k][0]. Per iteration 12,288 entries go through LDS: loaded and stored coalesced (a thread's consecutive
+// entries straight from global memory put 64 lanes on 64 lines per load and store: 17 µs for 16,768 entries, session
+// r6s24), summed per thread over 12 consecutive ones (padded rows: no bank conflicts), one wave scan, one barrier.
+constexpr uint32_t kSortScanBlock = 1024, kSortScanPer = 12, kSortScanRow = kSortScanPer + 1;
 __global__ __launch_bounds__(kSortScanBlock) void dk_tcp_sort_scan_kernel(uint32_t* H, uint32_t m, uint32_t nb,
                                                                           uint32_t* range) {
     __shared__ uint32_t wsum[kSortScanBlock / 64];
+    __shared__ uint32_t buf[kSortScanBlock * kSortScanRow];  // entry e at (e / 12) * 13 + e % 12
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const auto at = [](uint32_t e) { return (e / kSortScanPer) * kSortScanRow + e % kSortScanPer; };
     uint32_t carry = 0;
     for (uint32_t base = 0; base < m; base += kSortScanBlock * kSortScanPer) {
-        const uint32_t j0 = base + tid * kSortScanPer;
+#pragma unroll
+        for (uint32_t q = 0; q < kSortScanPer; q++) {
+            const uint32_t e = q * kSortScanBlock + tid, j = base + e;
+            buf[at(e)] = j < m ? H[j] : 0u;
+        }
+        __syncthreads();
         uint32_t x[kSortScanPer], t = 0;
 #pragma unroll
         for (uint32_t q = 0; q < kSortScanPer; q++) {
-            x[q] = j0 + q < m ? H[j0 + q] : 0u;
+            x[q] = buf[tid * kSortScanRow + q];
             t += x[q];
         }
         uint32_t incl = t;  // the thread's total, scanned over the wave
@@ -241,6 +297,7 @@ __global__ __launch_bounds__(kSortScanBlock) void dk_tcp_sort_scan_kernel(uint32
         if (lane == 63) wsum[wv] = incl;
         __syncthreads();
         uint32_t before = carry, all = 0;
+#pragma unroll
         for (uint32_t w = 0; w < kSortScanBlock / 64; w++) {
             const uint32_t ws = wsum[w];
             before += w < wv ? ws : 0u;
@@ -249,24 +306,34 @@ __global__ __launch_bounds__(kSortScanBlock) void dk_tcp_sort_scan_kernel(uint32
         uint32_t run = before + incl - t;
 #pragma unroll
         for (uint32_t q = 0; q < kSortScanPer; q++) {
-            if (j0 + q < m) {
-                H[j0 + q] = run;
-                if (range && (j0 + q) % nb == 0) range[(j0 + q) / nb] = run;
-            }
+            buf[tid * kSortScanRow + q] = run;
             run += x[q];
         }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kSortScanPer; q++) {
+            const uint32_t e = q * kSortScanBlock + tid, j = base + e;
+            if (j < m) {
+                const uint32_t v = buf[at(e)];
+                H[j] = v;
+                if (range && j % nb == 0) range[j / nb] = v;
+            }
+        }
         carry += all;
-        __syncthreads();  // wsum reused
+        __syncthreads();  // buf and wsum reused
     }
 }
 
 __global__ __launch_bounds__(kSortBlock) void dk_tcp_sort_scatter_kernel(uint32_t n, SortPass S) {
     __shared__ uint32_t cur[kSortWaves][kSortMaxBuckets];  // per wave: the next position per digit
     const uint32_t b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t nbits = 32u - (uint32_t)__builtin_clz(S.mask | 1u);  // digit bits (mask = 2^bits - 1)
+    const uint32_t s0 = b * kSortTile + wv * kSortSub, s1 = min(n, s0 + kSortSub);
+    uint32_t kr[kSortRounds];
+    sort_load_keys(S, s0, s1, lane, kr);
     for (uint32_t k = tid; k < kSortWaves * kSortMaxBuckets; k += kSortBlock) (&cur[0][0])[k] = 0;
     __syncthreads();
-    const uint32_t s0 = b * kSortTile + wv * kSortSub, s1 = min(n, s0 + kSortSub);
-    for (uint32_t i = s0 + lane; i < s1; i += 64) atomicAdd(&cur[wv][(S.kin[i] >> S.shift) & S.mask], 1u);
+    sort_count_keys(S, s0, s1, lane, kr, cur[wv], nbits);  // this wave's counts
     __syncthreads();
     for (uint32_t k = tid; k < S.nbuck; k += kSortBlock) {  // -> each wave's first position per digit
         uint32_t pos = S.H[(size_t)k * nb + b];
@@ -279,22 +346,17 @@ __global__ __launch_bounds__(kSortBlock) void dk_tcp_sort_scatter_kernel(uint32_
     }
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
-    const uint32_t nbits = 32u - (uint32_t)__builtin_clz(S.mask | 1u);  // digit bits (mask = 2^bits - 1)
-    for (uint32_t r = s0; r < s1; r += 64) {
-        const uint32_t i = r + lane;
+#pragma unroll
+    for (uint32_t r = 0; r < kSortRounds; r++) {
+        const uint32_t i = s0 + r * 64 + lane;
         const bool live = i < s1;
-        const uint32_t key = live ? S.kin[i] : 0u, val = live ? (S.vin ? S.vin[i] : i) : 0u;
-        const uint32_t d = (key >> S.shift) & S.mask;
-        uint64_t same = __ballot(live);
-        for (uint32_t bit = 0; bit < nbits; bit++) {  // the lanes whose digit equals this lane's
-            const uint64_t ones = __ballot(live && ((d >> bit) & 1u));
-            same &= ((d >> bit) & 1u) ? ones : ~ones;
-        }
+        const uint32_t key = kr[r], d = (key >> S.shift) & S.mask;
+        const uint64_t same = digit_group(d, live, nbits);
         const uint32_t at = cur[wv][d];
         const uint32_t rank = (uint32_t)__popcll(same & lt);
         if (live && rank == 0) cur[wv][d] = at + (uint32_t)__popcll(same);
         if (live) {
-            S.vout[at + rank] = val;
+            S.vout[at + rank] = S.vin ? S.vin[i] : i;
             if (S.kout) S.kout[at + rank] = key;
         }
     }

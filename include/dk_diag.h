@@ -68,7 +68,7 @@ int dk_diag_tcp_set_walk(struct dk_tcp_ctx* ctx, int32_t walk, int32_t relay_wav
 /* The walk the context's last dk_tcp_rx_process call ran (0 lane, 1 wave, 2 relay, 3 scan; -1 none yet). */
 int dk_diag_tcp_last_walk(const struct dk_tcp_ctx* ctx);
 /* How dk_tcp_rx_process orders the batch by connection: sort -1 the rule (one stable counting pass over the whole
- * key up to 80 table rows, rocPRIM's radix sort beyond), 1 the radix sort always. 0 or EINVAL. */
+ * key up to 255 table rows, rocPRIM's radix sort beyond), 1 the radix sort always. 0 or EINVAL. */
 int dk_diag_tcp_set_sort(struct dk_tcp_ctx* ctx, int32_t sort);
 
 #ifdef __cplusplus

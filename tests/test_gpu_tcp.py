@@ -326,13 +326,13 @@ def test_walk_follows_stream_shape(nconns, reorder):
         assert stored == 0 and want == "scan"
 
 
-@pytest.mark.parametrize("nconns,reorder", [(1, 0.0), (23, 3.0), (79, 3.0), (80, 3.0), (3000, 3.0)])
+@pytest.mark.parametrize("nconns,reorder", [(1, 0.0), (23, 3.0), (254, 3.0), (255, 3.0), (3000, 3.0)])
 def test_counting_sort_matches_radix(nconns, reorder):
-    """Up to 80 table rows (tcp_kernels.hip kSortMaxRows) the batch is ordered by one counting pass over the whole
-    key (per-tile key counts, one scan that also yields the ranges, a scatter ranked by per-bit ballots); above, by
-    rocPRIM's radix sort. The rule and the forced radix sort (dk_diag_tcp_set_sort) give bit-exact results vs the
-    oracle at the boundary (79 / 80 flows + the listener row = 80 / 81 rows), with thousands of connections, and
-    across tiles (8,192 segments per tile, a partial last one)."""
+    """Up to 255 table rows (tcp_kernels.hip kSortMaxRows: 2 rows + 1 <= 511 key values) the batch is ordered by one
+    counting pass over the whole key (per-tile key counts, one scan that also yields the ranges, a scatter ranked by
+    per-bit ballots); above, by rocPRIM's radix sort. The rule and the forced radix sort (dk_diag_tcp_set_sort) give
+    bit-exact results vs the oracle at the boundary (254 / 255 flows + the listener row = 255 / 256 rows), with
+    thousands of connections, and across tiles (8,192 segments per tile, a partial last one)."""
     import torch
 
     n = 3 * 8192 + 777
