@@ -18,9 +18,9 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s26: the counting pass up to 255 rows as the default: GPU suite (the boundary test at 255 / 256 rows), A/B against
-# the committed build, the bench's TCP lines
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step sort_ab 300 python tools/tcp_ab.py build/variants/sortold.so build/variants/sort255.so --nconns 1,64,200 --reorder 0 --buffer-size 1073741824
-step sort_ab3 300 python tools/tcp_ab.py build/variants/sortold.so build/variants/sort255.so --nconns 64,200,16384 --reorder 3 --buffer-size 16777216
+# s27: the round's final tree: GPU suite, smoke(), the default bench line, then the rocprofv3 evidence pass
+step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
+step bench 600 python bench.py
+step profile 900 bash tools/profile_bench.sh r6i
 echo done
