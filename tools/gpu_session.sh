@@ -18,9 +18,8 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s27: the round's final tree: GPU suite, smoke(), the default bench line, then the rocprofv3 evidence pass
-step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
-step bench 600 python bench.py
-step profile 900 bash tools/profile_bench.sh r6i
+# s28: the TCP key pass with 1 / 2 / 4 frames a thread (every load before the first store) against the committed one
+step key_ab 400 python tools/tcp_ab.py build/variants/keyold.so build/variants/key1.so build/variants/key2.so build/variants/key4.so --nconns 16384,64 --reorder 3 --buffer-size 16777216
+step key_ab1 300 python tools/tcp_ab.py build/variants/keyold.so build/variants/key1.so build/variants/key2.so build/variants/key4.so --nconns 1 --reorder 0 --buffer-size 1073741824
+step keyprof 200 rocprofv3 --kernel-trace --stats -T -d $O/k4 -o run --output-format csv -- python3 tools/tcp_ab.py build/variants/key4.so --nconns 16384 --reorder 3 --buffer-size 16777216 --reps 2
 echo done
