@@ -78,6 +78,8 @@ struct Params {
     uint4* scan_sum;   // [3 ws]: {A, U, window maximum, A2} against the connection's state at the call's start (decided
                        // iff A <= R <= U or R >= A2); {n0, lo, e0, e1}, {e2, e3}: the count summary (pre kernel)
     int* scan_ends;    // [ws][lane]: each lane's candidate end if it delivers at R below it, else INT_MIN
+    uint32_t* scan_idx;  // [ws][lane]: the window's frame indices and their records, copied by the pre kernel (the
+    uint4* scan_rec;     // slow path and the post kernel read them in one round trip instead of index -> record)
     uint4* scan_post;  // [ws]: {R, deliveries before the window, 1 = decided by the scan (written by the post kernel)}
     uint32_t* scan_head;  // [8 nconns]: the connection's state at the call's start {rn0, wend, snd, nooo, front,
                           // fin_pending, fin_seq}, saved by the scan kernel for the post kernel
@@ -1283,6 +1285,10 @@ constexpr uint32_t kScanBlock = 256, kScanWaves = kScanBlock / kWave;
 #define DK_TCP_SCAN_DEPTH 8
 #endif
 constexpr uint32_t kScanDepth = DK_TCP_SCAN_DEPTH;  // summary batches of 64 windows the scan kernel keeps in flight
+#ifndef DK_TCP_SCAN_PREFETCH
+#define DK_TCP_SCAN_PREFETCH 1
+#endif
+constexpr bool kScanPrefetch = DK_TCP_SCAN_PREFETCH != 0;
 constexpr uint32_t kScanSum = 3;  // uint4 per window in scan_sum: thresholds, then the delivery-count summary
 constexpr uint32_t kScanLow = 4;  // smallest delivering ends a window's count summary carries
 constexpr uint32_t kScanPost = 1024;  // decided windows' post records the scan kernel gathers in LDS per burst
@@ -1301,7 +1307,10 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_pre_kernel(Params P) {
     for (uint32_t v = blockIdx.x * kScanWaves + wv; v < nwin; v += gridDim.x * kScanWaves) {
         const uint32_t base = v * kWave, lim = min(cnt - base, kWave);
         const uint32_t i = P.svals[k0 + min(base + lane, last)];
-        const Seg q(P.rec[i], lane < lim, h.snd);
+        const uint4 g = P.rec[i];
+        P.scan_idx[(size_t)(ws0 + v) * kWave + lane] = i;
+        P.scan_rec[(size_t)(ws0 + v) * kWave + lane] = g;
+        const Seg q(g, lane < lim, h.snd);
         const Pre pr = pre_window(q, h.rn0, h.wend, scan_tmp[wv]);
         // lane j is decided by classify() iff max(R, pm_j) >= T_j, or for a SYN at or past RCV.NXT iff R <= U_j
         // (the relay walk's thresholds, against the state at the call's start) — or, for that SYN, once R is past its
@@ -1476,9 +1485,10 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         st_slow++;
         const uint64_t ck_s = wall_clock64();
 #endif
+        const uint32_t base = v * kWave, lim = min(cnt - base, kWave);
+        const uint32_t i = P.scan_idx[(size_t)(ws0 + v) * kWave + lane];
+        const uint4 g = P.scan_rec[(size_t)(ws0 + v) * kWave + lane];
         if (lane == 0) P.scan_post[ws0 + v] = make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t base = v * kWave, lim = min(cnt - base, kWave), i = idx(v);
-        const uint4 g = P.rec[i];
         const Seg q(g, lane < lim, h.snd);
         const Pre pr = pre_window(q, h.rn0, h.wend, scan_tmp[0]);
         const uint32_t R = w.rn - h.rn0;
@@ -1547,6 +1557,7 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
     // reload's latency every other step.)
     Batch b[kScanDepth];
     uint32_t last_slow = 0xFFFFFFFEu, run = kScanRingRun;  // the last window the slow path took, the next ring run
+    uint32_t pre = 0xFFFFFFFFu;  // the window b[] was loaded for ahead of the super-round (the slow path's successor)
     while (v < nwin && !stale) {
 #if DK_TCP_SCAN_STATS
         st_restart++;
@@ -1554,9 +1565,12 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         bool more = true;
         while (more && v < nwin) {
             if (v + kScanDepth * kWave > vflush + kScanPost) flush_post();  // room for this round's records
+            if (pre != v) {
 #pragma unroll
-            for (uint32_t j = 0; j < kScanDepth; j++)
-                if (v + j * kWave < nwin) load_batch(v + j * kWave, b[j]);  // (wave-uniform: no loads past the end)
+                for (uint32_t j = 0; j < kScanDepth; j++)
+                    if (v + j * kWave < nwin) load_batch(v + j * kWave, b[j]);  // (wave-uniform: no loads past the end)
+            }
+            pre = 0xFFFFFFFFu;
 #pragma unroll
             for (uint32_t j = 0; j < kScanDepth; j++)
                 if (more && batch_step(b[j]) < kWave) more = false;
@@ -1570,6 +1584,13 @@ __global__ __launch_bounds__(kWave) void dk_tcp_scan_kernel(Params P) {
         } else {
             if (v - last_slow > kWave) run = kScanRingRun;
             last_slow = v;
+            // the batches after this window, loaded under the slow path's own round trip (DK_TCP_SCAN_PREFETCH)
+            if (kScanPrefetch) {
+#pragma unroll
+                for (uint32_t j = 0; j < kScanDepth; j++)
+                    if (v + 1 + j * kWave < nwin) load_batch(v + 1 + j * kWave, b[j]);
+                pre = v + 1;
+            }
             slow_window();
         }
         vflush = v;
@@ -1620,10 +1641,11 @@ __global__ __launch_bounds__(kScanBlock) void dk_tcp_scan_post_kernel(Params P) 
                    finp = DK_U(hd[5]), fins = DK_U(hd[6]);
     for (uint32_t v = blockIdx.x * kScanWaves + wv; v < nwin; v += gridDim.x * kScanWaves) {
         const uint4 po = P.scan_post[ws0 + v];
+        const uint32_t i = P.scan_idx[(size_t)(ws0 + v) * kWave + lane];  // (issued with po: one round trip)
+        const uint4 g = P.scan_rec[(size_t)(ws0 + v) * kWave + lane];
         if (DK_U(po.z) != 1u) continue;
         const uint32_t base = v * kWave, lim = min(cnt - base, kWave);
-        const uint32_t i = P.svals[k0 + min(base + lane, last)];
-        const Seg q(P.rec[i], lane < lim, snd);
+        const Seg q(g, lane < lim, snd);
         const Pre pr = pre_window(q, rn0, wend, scan_tmp[wv]);
         const int Rq = (int)DK_U(po.x), pmi = (int)pr.pm;
         const int er = (int)(q.seg_end - rn0), dr = (int)(q.dend - rn0);
@@ -1730,6 +1752,9 @@ struct dk_tcp_ctx {
     size_t temp_cap = 0;
     uint4 *scan_sum = nullptr, *scan_post = nullptr;  // the scan walk's per-window scratch (dk_tcp::Params)
     int* scan_ends = nullptr;
+    uint32_t* scan_idx = nullptr;
+    uint4* scan_rec = nullptr;
+    size_t scan_idx_cap = 0, scan_rec_cap = 0;
     uint32_t* scan_head = nullptr;
     size_t scan_sum_cap = 0, scan_post_cap = 0, scan_ends_cap = 0, scan_head_cap = 0;
     // the stream's shape (pick_walk): the fix kernel's STORED count of each call, in host-mapped memory
@@ -1794,6 +1819,7 @@ void dk_tcp_ctx_destroy(dk_tcp_ctx* t) {
     if (t->used) (void)hipEventSynchronize(t->last);
     for (void* p : {(void*)t->keys, (void*)t->skeys, (void*)t->svals, (void*)t->range, (void*)t->rec, (void*)t->temp,
                     (void*)t->cls, (void*)t->open_until, (void*)t->scan_sum, (void*)t->scan_post, (void*)t->scan_ends,
+                    (void*)t->scan_idx, (void*)t->scan_rec,
                     (void*)t->scan_head, (void*)t->shape, (void*)t->csort})
         if (p) (void)hipFree(p);
     if (t->shape_host) (void)hipHostFree(const_cast<uint32_t*>(t->shape_host));
@@ -1840,11 +1866,13 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     if (walker == dk_tcp::kScanWalk) {  // windows: ws = range[2c] / 64 + c + v < n / 64 + nconns + 1
         const size_t nw = (size_t)n / 64 + nconns + 1;
         if (t->used &&
-            (t->scan_sum_cap < dk_tcp::kScanSum * nw || t->scan_ends_cap < nw * 64 || t->scan_head_cap < 8ull * nconns) &&
+            (t->scan_sum_cap < dk_tcp::kScanSum * nw || t->scan_ends_cap < nw * 64 || t->scan_head_cap < 8ull * nconns ||
+             t->scan_idx_cap < nw * 64 || t->scan_rec_cap < nw * 64) &&
             hipEventSynchronize(t->last) != hipSuccess)
             return EINVAL;
         if ((rc = grow(t->scan_sum, t->scan_sum_cap, dk_tcp::kScanSum * nw)) || (rc = grow(t->scan_post, t->scan_post_cap, nw)) ||
-            (rc = grow(t->scan_ends, t->scan_ends_cap, nw * 64)) ||
+            (rc = grow(t->scan_ends, t->scan_ends_cap, nw * 64)) || (rc = grow(t->scan_idx, t->scan_idx_cap, nw * 64)) ||
+            (rc = grow(t->scan_rec, t->scan_rec_cap, nw * 64)) ||
             (rc = grow(t->scan_head, t->scan_head_cap, 8 * (size_t)nconns)))
             return rc;
     }
@@ -1887,6 +1915,8 @@ int dk_tcp_rx_process(dk_tcp_ctx* t, const dk_rx_results* rx, uint32_t n, dk_tcp
     P.scan_sum = t->scan_sum;
     P.scan_post = t->scan_post;
     P.scan_ends = t->scan_ends;
+    P.scan_idx = t->scan_idx;
+    P.scan_rec = t->scan_rec;
     P.scan_head = t->scan_head;
     P.shape = t->shape;
     P.shape_host = t->shape_host_dev;

@@ -18,8 +18,10 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s28: the TCP key pass with 1 / 2 / 4 frames a thread (every load before the first store) against the committed one
-step key_ab 400 python tools/tcp_ab.py build/variants/keyold.so build/variants/key1.so build/variants/key2.so build/variants/key4.so --nconns 16384,64 --reorder 3 --buffer-size 16777216
-step key_ab1 300 python tools/tcp_ab.py build/variants/keyold.so build/variants/key1.so build/variants/key2.so build/variants/key4.so --nconns 1 --reorder 0 --buffer-size 1073741824
-step keyprof 200 rocprofv3 --kernel-trace --stats -T -d $O/k4 -o run --output-format csv -- python3 tools/tcp_ab.py build/variants/key4.so --nconns 16384 --reorder 3 --buffer-size 16777216 --reps 2
+# s29: the scan walk with each window's frame indices and records copied by the pre kernel (one round trip for the
+# slow path and the post kernel) and the next batches loaded under the slow path: GPU suite, A/B, step attribution
+step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step scan_ab 400 python tools/tcp_ab.py build/variants/scanhead.so build/variants/scannopf.so build/variants/scanpf.so --nconns 1,16,64,256 --reorder 0 --buffer-size 1073741824 --walk scan
+step scan_ab3 300 python tools/tcp_ab.py build/variants/scanhead.so build/variants/scanpf.so --nconns 16,64 --reorder 3 --buffer-size 16777216 --walk scan
+step scan1 200 python tools/tcp_scan_stats.py build/variants/tcpstats.so --nconns 1 --reorder 0 --buffer-size 1073741824
 echo done
