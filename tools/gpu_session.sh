@@ -18,10 +18,9 @@ export TMPDIR=/tmp
 # the in-tree library must be the checked-out tree's build (a stale library fails every GPU test)
 python -c "import __graft_entry__ as g; assert g.lib_build_id() == g.tree_build_id(), (g.lib_build_id(), g.tree_build_id())" || exit 9
 
-# s29: the scan walk with each window's frame indices and records copied by the pre kernel (one round trip for the
-# slow path and the post kernel) and the next batches loaded under the slow path: GPU suite, A/B, step attribution
-step gputest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step scan_ab 400 python tools/tcp_ab.py build/variants/scanhead.so build/variants/scannopf.so build/variants/scanpf.so --nconns 1,16,64,256 --reorder 0 --buffer-size 1073741824 --walk scan
-step scan_ab3 300 python tools/tcp_ab.py build/variants/scanhead.so build/variants/scanpf.so --nconns 16,64 --reorder 3 --buffer-size 16777216 --walk scan
-step scan1 200 python tools/tcp_scan_stats.py build/variants/tcpstats.so --nconns 1 --reorder 0 --buffer-size 1073741824
+# s30: the round's final tree: GPU suite, smoke(), the default bench line, then the rocprofv3 evidence pass
+step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('{\"smoke\": \"ok\"}')"
+step bench 600 python bench.py
+step profile 900 bash tools/profile_bench.sh r6j
 echo done
